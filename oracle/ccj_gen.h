@@ -1,0 +1,120 @@
+/* ccj_gen.h — fully specified synthetic-input generators shared by the oracle, the
+ * reference driver and the tests.  TEST INFRASTRUCTURE (see oracle/README.md): the product
+ * library carries its own device copy of the same generator in csrc/ccj_gen_device.h.
+ *
+ * Nothing here exists in the reference; the reference's main.cpp draws probe keys with
+ * std::mt19937(2) + std::uniform_int_distribution<int>(0, n) (main.cpp:43,53), whose algorithm
+ * is implementation-defined.  We restate the libstdc++-11 algorithm (Lemire's nearly
+ * divisionless method, bits/uniform_int_dist.h:245-268,311-316) so main.cpp-shaped fixtures can
+ * be regenerated bit-for-bit, and we add a counter-based SplitMix64 stream for every other
+ * config so any element can be produced independently on host or device.
+ */
+#ifndef CCJ_GEN_H
+#define CCJ_GEN_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* SplitMix64 finaliser (Steele, Lea, Flood 2014). */
+static inline uint64_t ccj_fmix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
+#define CCJ_GOLDEN_GAMMA 0x9e3779b97f4a7c15ULL
+
+/* i-th output of a SplitMix64 generator whose initial state is `seed`. */
+static inline uint64_t ccj_splitmix_at(uint64_t seed, uint64_t i) {
+  return ccj_fmix64(seed + (i + 1) * CCJ_GOLDEN_GAMMA);
+}
+
+/* Uniform probe key in [0, range): the i-th key of the stream (seed, range). */
+static inline int64_t ccj_uniform_key(uint64_t seed, uint64_t i, uint64_t range) {
+  return (int64_t)(ccj_splitmix_at(seed, i) % range);
+}
+
+/* ---- mt19937 / mt19937_64 (Matsumoto & Nishimura), std:: parameterisation ---- */
+typedef struct { uint32_t mt[624]; int idx; } ccj_mt19937;
+typedef struct { uint64_t mt[312]; int idx; } ccj_mt19937_64;
+
+static inline void ccj_mt19937_seed(ccj_mt19937 *g, uint32_t s) {
+  g->mt[0] = s;
+  for (int i = 1; i < 624; ++i) g->mt[i] = 1812433253u * (g->mt[i - 1] ^ (g->mt[i - 1] >> 30)) + (uint32_t)i;
+  g->idx = 624;
+}
+static inline uint32_t ccj_mt19937_next(ccj_mt19937 *g) {
+  if (g->idx >= 624) {
+    for (int i = 0; i < 624; ++i) {
+      uint32_t y = (g->mt[i] & 0x80000000u) | (g->mt[(i + 1) % 624] & 0x7fffffffu);
+      uint32_t v = g->mt[(i + 397) % 624] ^ (y >> 1);
+      if (y & 1u) v ^= 0x9908b0dfu;
+      g->mt[i] = v;
+    }
+    g->idx = 0;
+  }
+  uint32_t y = g->mt[g->idx++];
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= y >> 18;
+  return y;
+}
+static inline void ccj_mt19937_64_seed(ccj_mt19937_64 *g, uint64_t s) {
+  g->mt[0] = s;
+  for (int i = 1; i < 312; ++i)
+    g->mt[i] = 6364136223846793005ULL * (g->mt[i - 1] ^ (g->mt[i - 1] >> 62)) + (uint64_t)i;
+  g->idx = 312;
+}
+static inline uint64_t ccj_mt19937_64_next(ccj_mt19937_64 *g) {
+  if (g->idx >= 312) {
+    for (int i = 0; i < 312; ++i) {
+      uint64_t y = (g->mt[i] & 0xFFFFFFFF80000000ULL) | (g->mt[(i + 1) % 312] & 0x7FFFFFFFULL);
+      uint64_t v = g->mt[(i + 156) % 312] ^ (y >> 1);
+      if (y & 1ULL) v ^= 0xB5026F5AA96619E9ULL;
+      g->mt[i] = v;
+    }
+    g->idx = 0;
+  }
+  uint64_t x = g->mt[g->idx++];
+  x ^= (x >> 29) & 0x5555555555555555ULL;
+  x ^= (x << 17) & 0x71D67FFFEDA60000ULL;
+  x ^= (x << 37) & 0xFFF7EEE000000000ULL;
+  x ^= x >> 43;
+  return x;
+}
+
+/* std::uniform_int_distribution<int>(0, b)(mt19937) as implemented by libstdc++ 11
+ * (bits/uniform_int_dist.h:311-316 -> _S_nd<uint64_t>, :245-268): 32-bit engine, downscale. */
+static inline int32_t ccj_uniform_int_0_b(ccj_mt19937 *g, int32_t b) {
+  uint32_t range = (uint32_t)b + 1u; /* __uerange */
+  uint64_t product = (uint64_t)ccj_mt19937_next(g) * (uint64_t)range;
+  uint32_t low = (uint32_t)product;
+  if (low < range) {
+    uint32_t threshold = (uint32_t)(-range) % range;
+    while (low < threshold) {
+      product = (uint64_t)ccj_mt19937_next(g) * (uint64_t)range;
+      low = (uint32_t)product;
+    }
+  }
+  return (int32_t)(product >> 32);
+}
+
+/* ---- result checksums (defined here, used identically by oracle, driver, tests, bench) ----
+ * L2 (order-insensitive): sum over matches of ccj_l2_term(global probe row, payload) mod 2^64.
+ * L3 (order-sensitive):   h = ccj_l3_fold(h, row, payload) over the emission order, h0 = CCJ_L3_SEED.
+ * SURVEY chk: sum of payload * 1315423911 + chunk-local physical row. */
+static inline uint64_t ccj_l2_term(uint64_t row, int64_t payload) {
+  return ccj_fmix64(row * CCJ_GOLDEN_GAMMA + ccj_fmix64((uint64_t)payload + 1ULL));
+}
+#define CCJ_L3_SEED 0x243F6A8885A308D3ULL
+static inline uint64_t ccj_l3_fold(uint64_t h, uint64_t row, int64_t payload) {
+  return ccj_fmix64(ccj_fmix64(h ^ row) ^ (uint64_t)payload);
+}
+
+#ifdef __cplusplus
+}
+#endif
+#endif

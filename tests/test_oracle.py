@@ -1,0 +1,138 @@
+"""Pins the CPU oracle (our C restatement) against vectors produced by the reference itself.
+
+Golden data: tests/golden/*.npz + known_answers.json, made by tests/golden/make_golden.py from
+oracle/_ref/ref_driver (reference sources compiled from /root/reference).  Parity level L3
+(ordered per-Next stream) on every trace case, both the round view and chaining's merged view.
+"""
+import numpy as np
+import pytest
+
+from helpers import (assert_trace_equal, known_answers, load_trace, ref_keys, trace_inputs,
+                     views_from_rounds)
+from oracle import oracle as O
+
+KA = known_answers()
+
+
+def test_murmurhash64_known_values():
+    # hash_functions.h:8-16: h(0) = 0; constants checked against a direct restatement.
+    assert O.murmurhash64(0) == 0
+    M = 0xFFFFFFFFFFFFFFFF
+
+    def h(x):
+        x ^= x >> 32
+        x = (x * 0xD6E8FEB86659FD93) & M
+        x ^= x >> 32
+        x = (x * 0xD6E8FEB86659FD93) & M
+        x ^= x >> 32
+        return x
+
+    for x in [1, 2, 12345, 2**63 - 1, 2**64 - 1, 0xDEADBEEF]:
+        assert O.murmurhash64(x) == h(x)
+
+
+@pytest.mark.parametrize("n,cf", [(1, 1), (5, 3), (4096, 1), (4096, 4), (4096, 64), (1000, 7), (1000000, 5)])
+def test_ref_generator_and_membership(n, cf):
+    keys = ref_keys(n, cf)
+    vals, cnt = np.unique(keys, return_counts=True)
+    for v, c in zip(vals[:50], cnt[:50]):
+        assert O.ref_multiplicity(int(v), n, cf) == c
+    probe = np.arange(0, int(keys.max()) + 3)
+    got = sum(O.ref_multiplicity(int(k), n, cf) for k in probe[:2000])
+    want = int(np.isin(keys, probe[:2000]).sum())
+    assert got == want
+
+
+@pytest.mark.parametrize("name", sorted(KA["trace_cases"]))
+def test_oracle_matches_reference_traces(name):
+    entry = KA["trace_cases"][name]
+    spec = entry["spec"]
+    kind = O.LP if spec["kind"] == "lp" else O.CHAIN
+    table = O.Table(kind, ref_keys(spec["n_build"], spec["cf"]))
+    for view, info in entry["views"].items():
+        trace = load_trace(name, view)
+        keys, sel, counts = trace_inputs(spec, trace)
+        out = table.probe(keys, spec["B"], sel=sel, counts=counts, cap_factor=spec["cf"], max_rounds=512)
+        got = views_from_rounds(out["count"], out["sel"], out["payload"], out["rounds"], out["round_counts"],
+                                out["cap"], out["max_rounds"], merged=(view == "merged"))
+        assert_trace_equal(got, trace)
+        assert int(out["count"].sum()) == info["matches"]
+
+
+@pytest.mark.parametrize("name", [k for k in sorted(KA["sum_cases"]) if "64M" not in k])
+def test_oracle_matches_reference_sums(name):
+    entry = KA["sum_cases"][name]
+    spec = entry["spec"]
+    want = entry["variants"]["next"]
+    kind = O.LP if spec["kind"] == "lp" else O.CHAIN
+    table = O.Table(kind, ref_keys(spec["n_build"], spec["cf"]))
+    if spec["gen"] == 1:
+        # mt19937_64 stream (SURVEY §4 driver); generated in C to stay fast.
+        import ctypes as C
+        keys = _mt64_keys(spec["seed"], spec["n_probe"], spec["range"])
+    else:
+        keys = O.uniform_keys(spec["seed"], 0, spec["n_probe"], spec["range"])
+    out = table.probe(keys, spec["B"], cap_factor=spec["cf"], max_rounds=512)
+    cap, B = out["cap"], spec["B"]
+    n_chunks = len(out["count"])
+    valid = np.arange(cap)[None, :] < out["count"][:, None].astype(np.int64)
+    sel = out["sel"].reshape(n_chunks, cap)[valid].astype(np.uint64)
+    pay = out["payload"].reshape(n_chunks, cap)[valid]
+    chunk_of = np.repeat(np.arange(n_chunks, dtype=np.uint64), out["count"].astype(np.int64))
+    rows = chunk_of * np.uint64(B) + sel
+    assert int(out["count"].sum()) == want["matches"]
+    with np.errstate(over="ignore"):
+        chk = int(np.sum(pay.view(np.uint64) * np.uint64(1315423911) + sel, dtype=np.uint64))
+    assert chk == want["survey_chk"]
+    assert O.l2_sum(rows, pay) == want["l2"]
+    # size-independent exact counter (membership oracle) agrees too
+    if spec["gen"] == 0:
+        m, l2 = O.count_uniform(spec["seed"], 0, spec["n_probe"], spec["range"], spec["n_build"], spec["cf"])
+        assert (m, l2) == (want["matches"], want["l2"])
+
+
+def _mt64_keys(seed, n, rng):
+    import ctypes as C
+    import os
+    import subprocess
+    import tempfile
+    src = r'''
+#include "ccj_gen.h"
+void gen(unsigned long long seed, unsigned long long n, unsigned long long rng, long long *out) {
+  ccj_mt19937_64 g; ccj_mt19937_64_seed(&g, seed);
+  for (unsigned long long i = 0; i < n; ++i) out[i] = (long long)(ccj_mt19937_64_next(&g) % rng);
+}'''
+    d = tempfile.mkdtemp()
+    with open(os.path.join(d, "g.c"), "w") as f:
+        f.write(src)
+    so = os.path.join(d, "g.so")
+    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-I", os.path.dirname(O.__file__), "-o", so,
+                    os.path.join(d, "g.c")], check=True)
+    lib = C.CDLL(so)
+    out = np.empty(n, np.int64)
+    lib.gen(C.c_ulonglong(seed), C.c_ulonglong(n), C.c_ulonglong(rng), out.ctypes.data_as(C.POINTER(C.c_longlong)))
+    return out
+
+
+def test_count_uniform_micro_bench_shape():
+    # simd_micro_bench.cpp:78-81 with kHitFreq 1: every probe key lies in [0, kRHSTuples) and the
+    # table holds 0..kRHSTuples-1 once, so #tuples == #probes (134217728 for 2^27).
+    m, _ = O.count_uniform(9, 0, 1 << 20, 128, 128, 1)
+    assert m == 1 << 20
+
+
+@pytest.mark.parametrize("B", [4, 8, 2048])
+def test_compact_plan_properties(B):
+    rng = np.random.default_rng(B)
+    segs = rng.integers(0, B + 1, size=300).astype(np.uint32)
+    segs[::17] = B  # full chunks bypass the cache (compactor.cpp:6)
+    dest, occ = O.compact_plan(segs, B)
+    # a permutation into ceil-packed chunks, every chunk full except possibly the last
+    assert len(np.unique(dest)) == len(dest)
+    assert (occ[:-1] == B).all() and 0 < occ[-1] <= B
+    assert int(occ.sum()) == int(segs.sum())
+    # full segments land in one output chunk each, in order
+    start = np.concatenate([[0], np.cumsum(segs.astype(np.int64))[:-1]])
+    for s in np.flatnonzero(segs == B):
+        d = dest[start[s]:start[s] + B]
+        assert d[0] % B == 0 and (np.diff(d.astype(np.int64)) == 1).all()
