@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""bench.py — probe throughput of the MI355X hash-join hot path (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c5] [--no-cpu]
+  N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Step = one pass of the hot path over one batch:
+  c2 (default; BASELINE configs[1]): LP table of 2^26 reference-generator keys (2 GiB, alpha 1/4),
+      2^30 uniform probe keys in [0, 2^26) resident in HBM, chunk 2048 -> one ccj_probe launch
+      (hash, probe rounds, ballot packs, payload) writing row ids + payloads + per-round counts.
+  N > 1 (C4 shape, weak scaling): every rank owns the build keys with owner = h(k) >> (64-log2 N)
+      and 2^30 probe keys of its own; a step = owner partition + RCCL all-to-all (xGMI) + local
+      probe.
+Prints ONE JSON line on rank 0 with roofline and cpu_baseline objects.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "chunk-compaction-in-vectorized-execution-simd_amd")
+sys.path.insert(0, PKG)
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import ccj  # noqa: E402
+
+METRIC = "probe tuples/sec + achieved HBM GB/s, 1B-row int64 join at 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
+SEED = 42
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c2", choices=["c2"])
+    ap.add_argument("--n-build", type=int, default=1 << 26)
+    ap.add_argument("--n-probe", type=int, default=1 << 30, help="probe keys per GPU")
+    ap.add_argument("--chunk", type=int, default=2048)
+    ap.add_argument("--layout", default="device", choices=["device", "reference"])
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-sample", type=int, default=1 << 26, help="probe keys in the multi-thread CPU sample")
+    ap.add_argument("--no-verify", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def cpu_baseline(args):
+    """Our scalar C restatement of main.cpp's no-compact LP probe path (oracle/, 'port'), timed on
+    this box's host cores on a bounded sample of the same workload."""
+    from oracle import oracle as O
+    import numpy as np
+
+    t0 = time.perf_counter()
+    table = O.Table(O.LP, O.ref_build_keys(args.n_build, 1))
+    build_s = time.perf_counter() - t0
+    res = {}
+    for threads, n in ((1, min(args.cpu_sample // 8, 1 << 23)), (args.cpu_threads, args.cpu_sample)):
+        keys = O.uniform_keys(SEED, 0, n, args.n_build)
+        table.probe_totals(keys[: 1 << 16], args.chunk, threads=threads)  # warm
+        t0 = time.perf_counter()
+        m, l2 = table.probe_totals(keys, args.chunk, threads=threads)
+        dt = time.perf_counter() - t0
+        res[threads] = (n / dt, n, dt, m)
+    thr = args.cpu_threads
+    v, n, dt, m = res[thr]
+    v1, n1, dt1, _ = res[1]
+    return {
+        "value": v, "unit": "probe tuples/s", "cores": thr, "kind": "port",
+        "sample": (f"first {n} of the same 2^30-key uniform probe stream (seed {SEED}) against the same "
+                   f"{args.n_build}-key LP table built on the host, chunk {args.chunk}, {thr} threads "
+                   f"(one per contiguous chunk range), {dt:.2f} s; 1 thread on {n1} keys: "
+                   f"{v1 / 1e6:.1f} M tuples/s ({dt1:.2f} s); table build {build_s:.1f} s untimed"),
+        "single_thread_value": v1,
+        "cpu_model": cpu_model(),
+        "nproc": os.cpu_count(),
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    ccj.device_init(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.Stream(device=dev)
+
+    n_build, n_probe, chunk = args.n_build, args.n_probe, args.chunk
+    layout = ccj.LAYOUT_DEVICE if args.layout == "device" else ccj.LAYOUT_REFERENCE
+    if world > 1:
+        raise SystemExit("multi-GPU C4 path: see bench_c4 (not wired in this build)")
+
+    # ---- setup (untimed, as the reference builds before its timer: main.cpp:62-68 vs :92-94) ----
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        table = ccj.Table.reference(ccj.LP, n_build, 1, layout, stream=stream)
+        keys = ccj.gen_uniform_keys(n_probe, SEED, n_build, first_row=rank * n_probe, stream=stream)
+        out = table.alloc_outputs(n_probe, chunk, rounds=True)
+    stream.synchronize()
+    log(f"[setup] table {table.size} slots, max_rounds {table.max_rounds}, keys {n_probe}: "
+        f"{time.perf_counter() - t0:.1f} s")
+
+    def step():
+        table.probe(keys, chunk, out=out, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    stream.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record(stream)
+        step()
+        evs[i][1].record(stream)
+    stream.synchronize()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([wall], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    ms_per_step = wall * 1e3 / args.steps
+    total_tuples = n_probe * world
+    value = total_tuples / (wall / args.steps)
+
+    # ---- verification + work accounting (untimed) ----
+    status = int(out["status"].item())
+    matches, l2 = ccj.result_checksum(out, chunk, row_base=rank * n_probe, stream=stream)
+    examined, cost_matches = table.probe_cost(keys, stream=stream)
+    parity = {"status_flags": status, "matches": matches, "l2": hex(l2)}
+    if not args.no_verify:
+        from oracle import oracle as O
+        want_m, want_l2 = O.count_uniform(SEED, rank * n_probe, (rank + 1) * n_probe, n_build, n_build, 1,
+                                          threads=args.cpu_threads)
+        parity.update(expected_matches=want_m, l1_ok=(want_m == matches), l2_ok=(want_l2 == l2))
+    s_bar = examined / n_probe
+    m_bar = matches / n_probe
+    alg_bytes_per_tuple = 8 + 8 * s_bar + m_bar * 12
+    alg_bytes = alg_bytes_per_tuple * n_probe
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_c2.json")
+    if os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+            if pmc.get("n_probe") == n_probe and pmc.get("n_build") == n_build:
+                traffic = pmc.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": value, "unit": "probe tuples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+            "data": "synthetic (reference key generator build side; SplitMix64 uniform probe keys, seed 42)",
+            "config": {"workload": "C2: 1xMI355X linear-probe, 64M build / 1B probe int64 uniform keys, chunk=2048",
+                       "table": "linear_probing", "layout": args.layout, "n_build": n_build,
+                       "n_probe_per_gpu": n_probe, "chunk": chunk, "parallelism": f"dp{world}"},
+            "hbm_gbs_algorithmic": achieved,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "probe_chunks<LP,32>", "kernel_ms": kern_ms,
+                         "alg_bytes_per_tuple": alg_bytes_per_tuple, "s_bar": s_bar, "m_bar": m_bar},
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

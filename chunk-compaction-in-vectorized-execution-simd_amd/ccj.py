@@ -1,0 +1,204 @@
+"""Python binding of libccj.so (include/ccj.h) over ctypes.
+
+PyTorch is plumbing here: device buffers are torch tensors on `cuda:N` and streams are torch
+streams; every computation runs in the HIP kernels of libccj.so.  There is no CPU fallback —
+loading fails loudly when the library is missing, and every call fails without a gfx950 device.
+
+Mirrors the reference operator surface for the probe path:
+  Table.reference(kind, n, cf)   <- LPHashTable(n, cf) / HashTable(n, cf)  (linear_probing_ht.cpp:4-37,
+                                    chaining_ht.cpp:4-36)
+  Table.probe(keys, chunk, ...)  <- Probe + `while HasNext(): Next(...)`    (linear_probing_ht.cpp:39-115,
+                                    chaining_ht.cpp:38-136), batched over chunks
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libccj.so")
+
+LP, CHAIN = 0, 1
+LAYOUT_REFERENCE, LAYOUT_DEVICE = 0, 1
+FLAG_CAP_OVERFLOW, FLAG_ROUND_OVERFLOW, FLAG_BAD_INPUT = 1, 2, 4
+
+_lib = None
+
+
+class CCJError(RuntimeError):
+    pass
+
+
+class TableInfo(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("layout", C.c_int32), ("n_keys", C.c_uint64), ("size", C.c_uint64),
+                ("max_dup", C.c_uint64), ("max_rounds", C.c_uint32), ("reserved", C.c_uint32),
+                ("d_table", C.c_void_p), ("d_bucket_off", C.c_void_p)]
+
+
+class ProbeArgs(C.Structure):
+    _fields_ = [("keys", C.c_void_p), ("sel", C.c_void_p), ("counts", C.c_void_p), ("n_rows", C.c_uint64),
+                ("chunk", C.c_uint32), ("max_rounds", C.c_uint32), ("cap", C.c_uint64),
+                ("out_count", C.c_void_p), ("out_sel", C.c_void_p), ("out_payload", C.c_void_p),
+                ("out_rounds", C.c_void_p), ("out_round_counts", C.c_void_p), ("status", C.c_void_p)]
+
+
+EXPORTS = ["ccj_last_error", "ccj_abi_version", "ccj_device_init", "ccj_table_build_reference",
+           "ccj_table_build_from_host", "ccj_table_build_on_device", "ccj_table_get_info", "ccj_table_free",
+           "ccj_probe", "ccj_gen_uniform_keys", "ccj_probe_cost", "ccj_result_checksum"]
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-C", HERE, "-j8"], check=True)
+    return LIB_PATH
+
+
+def lib():
+    """Load libccj.so (in-tree).  Raises if it is missing: there is no fallback path."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise CCJError(f"{LIB_PATH} missing: run `make -C {HERE}` (or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        vp, u64, i32 = C.c_void_p, C.c_uint64, C.c_int
+        L.ccj_last_error.restype = C.c_char_p
+        L.ccj_abi_version.restype = i32
+        L.ccj_device_init.argtypes = [i32]
+        L.ccj_table_build_reference.argtypes = [i32, u64, u64, i32, vp, C.POINTER(vp)]
+        L.ccj_table_build_from_host.argtypes = [i32, vp, u64, C.POINTER(vp)]
+        L.ccj_table_build_on_device.argtypes = [i32, vp, u64, vp, C.POINTER(vp)]
+        L.ccj_table_get_info.argtypes = [vp, C.POINTER(TableInfo)]
+        L.ccj_table_free.argtypes = [vp]
+        L.ccj_probe.argtypes = [vp, C.POINTER(ProbeArgs), vp]
+        L.ccj_gen_uniform_keys.argtypes = [vp, u64, u64, u64, u64, vp]
+        L.ccj_probe_cost.argtypes = [vp, vp, u64, vp, vp]
+        L.ccj_result_checksum.argtypes = [vp, vp, vp, u64, u64, C.c_uint32, u64, vp, vp]
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise CCJError(f"{what} failed ({rc}): {lib().ccj_last_error().decode()}")
+
+
+def _stream(stream):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def device_init(device: int = 0):
+    check(lib().ccj_device_init(device), "ccj_device_init")
+
+
+def gen_uniform_keys(n: int, seed: int, rng: int, first_row: int = 0, out=None, stream=None):
+    """Device column of SplitMix64 keys (oracle/ccj_gen.h ccj_uniform_key stream)."""
+    import torch
+    if out is None:
+        out = torch.empty(n, dtype=torch.int64, device=torch.device("cuda", torch.cuda.current_device()))
+    check(lib().ccj_gen_uniform_keys(_ptr(out), n, seed, first_row, rng, _stream(stream)), "ccj_gen_uniform_keys")
+    return out
+
+
+def result_checksum(out, chunk: int, row_base: int = 0, stream=None):
+    """(matches, L2 checksum) of a probe output, computed on the device."""
+    import torch
+    acc = torch.zeros(2, dtype=torch.int64, device=out["count"].device)
+    check(lib().ccj_result_checksum(_ptr(out["count"]), _ptr(out["sel"]), _ptr(out["payload"]), out["n_chunks"],
+                                    out["cap"], chunk, row_base, _ptr(acc), _stream(stream)), "ccj_result_checksum")
+    torch.cuda.synchronize()
+    m, l2 = acc.cpu().tolist()
+    return m, l2 & 0xFFFFFFFFFFFFFFFF
+
+
+class Table:
+    def __init__(self, handle: C.c_void_p):
+        self._h = handle
+        info = TableInfo()
+        check(lib().ccj_table_get_info(handle, C.byref(info)), "ccj_table_get_info")
+        self.kind, self.layout = info.kind, info.layout
+        self.n_keys, self.size = info.n_keys, info.size
+        self.max_dup, self.max_rounds = info.max_dup, info.max_rounds
+        self.d_table, self.d_bucket_off = info.d_table, info.d_bucket_off
+
+    @classmethod
+    def reference(cls, kind: int, n: int, cf: int = 1, layout: int = LAYOUT_REFERENCE, stream=None):
+        h = C.c_void_p()
+        check(lib().ccj_table_build_reference(kind, n, cf, layout, _stream(stream), C.byref(h)),
+              "ccj_table_build_reference")
+        return cls(h)
+
+    @classmethod
+    def from_host(cls, kind: int, keys):
+        import numpy as np
+        keys = np.ascontiguousarray(keys, dtype=np.int64)
+        h = C.c_void_p()
+        check(lib().ccj_table_build_from_host(kind, keys.ctypes.data_as(C.c_void_p), len(keys), C.byref(h)),
+              "ccj_table_build_from_host")
+        return cls(h)
+
+    @classmethod
+    def on_device(cls, kind: int, d_keys, stream=None):
+        h = C.c_void_p()
+        check(lib().ccj_table_build_on_device(kind, _ptr(d_keys), d_keys.numel(), _stream(stream), C.byref(h)),
+              "ccj_table_build_on_device")
+        return cls(h)
+
+    def free(self):
+        if self._h:
+            lib().ccj_table_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def probe_cost(self, keys, stream=None):
+        """(table words examined, matches) over a key column — roofline accounting."""
+        import torch
+        acc = torch.zeros(2, dtype=torch.int64, device=keys.device)
+        check(lib().ccj_probe_cost(self._h, _ptr(keys), keys.numel(), _ptr(acc), _stream(stream)), "ccj_probe_cost")
+        torch.cuda.synchronize()
+        a = acc.cpu().tolist()
+        return a[0], a[1]
+
+    def alloc_outputs(self, n_rows: int, chunk: int, cap: int | None = None, rounds: bool = True,
+                      payload: bool = True, device=None):
+        import torch
+        dev = device or torch.device("cuda", torch.cuda.current_device())
+        n_chunks = (n_rows + chunk - 1) // chunk
+        cap = cap if cap is not None else chunk * max(1, int(self.max_dup))
+        mr = max(1, int(self.max_rounds)) + 1 if rounds else 0
+        o = dict(
+            cap=cap, max_rounds=mr, n_chunks=n_chunks,
+            count=torch.empty(n_chunks, dtype=torch.int32, device=dev),
+            sel=torch.empty(n_chunks * cap, dtype=torch.int32, device=dev),
+            payload=torch.empty(n_chunks * cap, dtype=torch.int64, device=dev) if payload else None,
+            rounds=torch.empty(n_chunks, dtype=torch.int32, device=dev) if rounds else None,
+            round_counts=torch.zeros(n_chunks * mr, dtype=torch.int32, device=dev) if rounds else None,
+            status=torch.zeros(1, dtype=torch.int32, device=dev),
+        )
+        return o
+
+    def probe(self, keys, chunk: int, sel=None, counts=None, out=None, stream=None, **alloc_kw):
+        """Batched Probe + Next loop (include/ccj.h ccj_probe).  Returns the output dict."""
+        if out is None:
+            out = self.alloc_outputs(keys.numel(), chunk, **alloc_kw)
+        a = ProbeArgs(keys=_ptr(keys).value, sel=_ptr(sel).value if sel is not None else None,
+                      counts=_ptr(counts).value if counts is not None else None, n_rows=keys.numel(), chunk=chunk,
+                      max_rounds=out["max_rounds"], cap=out["cap"], out_count=_ptr(out["count"]).value,
+                      out_sel=_ptr(out["sel"]).value,
+                      out_payload=_ptr(out["payload"]).value if out["payload"] is not None else None,
+                      out_rounds=_ptr(out["rounds"]).value if out["rounds"] is not None else None,
+                      out_round_counts=_ptr(out["round_counts"]).value if out["round_counts"] is not None else None,
+                      status=_ptr(out["status"]).value)
+        check(lib().ccj_probe(self._h, C.byref(a), _stream(stream)), "ccj_probe")
+        return out

@@ -1,0 +1,370 @@
+// ccj_api.hip — the C ABI (include/ccj.h): device selection, table builds, probe dispatch.
+//
+// No CPU fallback: every entry point requires a gfx950 device and reports CCJ_ERR_NO_DEVICE
+// otherwise.  Host-side work here is limited to building tables in the reference's sequential
+// insertion order (CCJ_LAYOUT_REFERENCE), which is inherently serial and untimed in the
+// reference too (main.cpp:62-68 builds tables before the timed loop at :92-94).
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "ccj_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+  return fail(CCJ_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr, what)                  \
+  do {                                       \
+    hipError_t e_ = (expr);                  \
+    if (e_ != hipSuccess) return hip_fail(e_, what); \
+  } while (0)
+
+int check_device() {
+  int dev = -1;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return fail(CCJ_ERR_NO_DEVICE, std::string("no HIP device: ") + hipGetErrorString(e));
+  hipDeviceProp_t prop;
+  e = hipGetDeviceProperties(&prop, dev);
+  if (e != hipSuccess) return fail(CCJ_ERR_NO_DEVICE, std::string("no HIP device: ") + hipGetErrorString(e));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(CCJ_ERR_NO_DEVICE, std::string("device is ") + prop.gcnArchName + ", need gfx950");
+  return CCJ_OK;
+}
+
+uint64_t lp_num_slots(uint64_t n) {  // linear_probing_ht.cpp:5-6
+  uint64_t s = 1;
+  while (s < (n << 2)) s <<= 1;
+  return s;
+}
+uint64_t chain_num_buckets(uint64_t n) {  // chaining_ht.cpp:5-6
+  uint64_t b = 1;
+  while (b < 2 * n) b *= 2;
+  return b;
+}
+
+std::vector<int64_t> reference_keys(uint64_t n, uint64_t cf) {  // linear_probing_ht.cpp:14-25
+  std::vector<int64_t> k(n);
+  const uint64_t num_unique = n / cf + (n % cf != 0);
+  const uint64_t step = n / num_unique;
+  for (uint64_t t = 0; t < n; ++t) k[t] = (int64_t)((t / cf) * step);
+  return k;
+}
+
+// Longest occupied run (circular) and largest multiplicity of one key inside a run.
+void lp_host_stats(const std::vector<int64_t> &slots, uint32_t *max_run, uint64_t *max_dup) {
+  const uint64_t n = slots.size();
+  uint64_t start = 0;
+  while (start < n && slots[start] != -1) ++start;  // an empty slot always exists (alpha <= 1/4)
+  uint64_t best = 0, dup = slots.empty() ? 0 : 1;
+  uint64_t run = 0;
+  std::vector<int64_t> cl;
+  for (uint64_t t = 1; t <= n; ++t) {
+    const uint64_t i = (start + t) % n;
+    if (slots[i] != -1) {
+      ++run;
+      cl.push_back(slots[i]);
+    } else {
+      best = std::max(best, run);
+      if (cl.size() > 1) {
+        std::sort(cl.begin(), cl.end());
+        uint64_t r = 1;
+        for (size_t a = 1; a < cl.size(); ++a) {
+          r = cl[a] == cl[a - 1] ? r + 1 : 1;
+          dup = std::max(dup, r);
+        }
+      }
+      cl.clear();
+      run = 0;
+    }
+  }
+  *max_run = (uint32_t)best;
+  *max_dup = dup;
+}
+
+int upload(void **dst, const void *src, size_t bytes, const char *what) {
+  if (bytes == 0) bytes = 8;
+  hipError_t e = hipMalloc(dst, bytes);
+  if (e != hipSuccess) return fail(CCJ_ERR_OOM, std::string(what) + ": hipMalloc failed");
+  if (src) HIP_TRY(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice), what);
+  return CCJ_OK;
+}
+
+int build_lp_host(const int64_t *keys, uint64_t n, ccj_table **out) {
+  const uint64_t size = lp_num_slots(n);
+  if (size > (1ull << 32)) return fail(CCJ_ERR_LIMIT, "LP table larger than 2^32 slots");
+  std::vector<int64_t> slots(size, -1);
+  const uint64_t mask = size - 1;
+  for (uint64_t i = 0; i < n; ++i) {  // linear_probing_ht.cpp:28-36
+    uint64_t s = ccj::murmurhash64((uint64_t)keys[i]) & mask;
+    while (slots[s] != -1) s = (s + 1) & mask;
+    slots[s] = keys[i];
+  }
+  std::unique_ptr<ccj_table> t(new ccj_table());
+  t->info.kind = CCJ_TABLE_LP;
+  t->info.layout = CCJ_LAYOUT_REFERENCE;
+  t->info.n_keys = n;
+  t->info.size = size;
+  lp_host_stats(slots, &t->info.max_rounds, &t->info.max_dup);
+  void *d = nullptr;
+  int rc = upload(&d, slots.data(), size * sizeof(int64_t), "LP slots");
+  if (rc) return rc;
+  t->d_table = (int64_t *)d;
+  t->info.d_table = t->d_table;
+  (void)hipGetDevice(&t->device);
+  *out = t.release();
+  return CCJ_OK;
+}
+
+int build_chain_host(const int64_t *keys, uint64_t n, ccj_table **out) {
+  if (n >= (1ull << 32)) return fail(CCJ_ERR_LIMIT, "chaining table needs < 2^32 keys (uint32 CSR)");
+  const uint64_t size = chain_num_buckets(n);
+  const uint64_t mask = size - 1;
+  // chaining_ht.cpp:29-35: push_back in order == stable counting sort by bucket.
+  std::vector<uint32_t> off(size + 1, 0);
+  std::vector<uint32_t> bucket(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    bucket[i] = (uint32_t)(ccj::murmurhash64((uint64_t)keys[i]) & mask);
+    off[bucket[i] + 1]++;
+  }
+  uint32_t longest = 0;
+  for (uint64_t b = 0; b < size; ++b) {
+    longest = std::max(longest, off[b + 1]);
+    off[b + 1] += off[b];
+  }
+  std::vector<int64_t> chain(n);
+  {
+    std::vector<uint32_t> fill(off.begin(), off.end() - 1);
+    for (uint64_t i = 0; i < n; ++i) chain[fill[bucket[i]]++] = keys[i];
+  }
+  uint64_t dup = n ? 1 : 0;
+  for (uint64_t b = 0; b < size; ++b) {
+    const uint32_t lo = off[b], hi = off[b + 1];
+    if (hi - lo < 2) continue;
+    std::vector<int64_t> cl(chain.begin() + lo, chain.begin() + hi);
+    std::sort(cl.begin(), cl.end());
+    uint64_t r = 1;
+    for (size_t a = 1; a < cl.size(); ++a) {
+      r = cl[a] == cl[a - 1] ? r + 1 : 1;
+      dup = std::max(dup, r);
+    }
+  }
+  std::unique_ptr<ccj_table> t(new ccj_table());
+  t->info.kind = CCJ_TABLE_CHAIN;
+  t->info.layout = CCJ_LAYOUT_REFERENCE;
+  t->info.n_keys = n;
+  t->info.size = size;
+  t->info.max_rounds = longest;
+  t->info.max_dup = dup;
+  void *d = nullptr;
+  int rc = upload(&d, chain.data(), n * sizeof(int64_t), "chain keys");
+  if (rc) return rc;
+  t->d_table = (int64_t *)d;
+  rc = upload(&d, off.data(), (size + 1) * sizeof(uint32_t), "chain offsets");
+  if (rc) {
+    (void)hipFree(t->d_table);
+    return rc;
+  }
+  t->d_off = (uint32_t *)d;
+  t->info.d_table = t->d_table;
+  t->info.d_bucket_off = t->d_off;
+  (void)hipGetDevice(&t->device);
+  *out = t.release();
+  return CCJ_OK;
+}
+
+int build_lp_device(const int64_t *d_keys, uint64_t n, hipStream_t s, uint64_t known_dup, ccj_table **out) {
+  const uint64_t size = lp_num_slots(n);
+  if (size > (1ull << 32)) return fail(CCJ_ERR_LIMIT, "LP table larger than 2^32 slots");
+  std::unique_ptr<ccj_table> t(new ccj_table());
+  void *d = nullptr;
+  if (hipMalloc(&d, size * sizeof(int64_t)) != hipSuccess) return fail(CCJ_ERR_OOM, "LP slots: hipMalloc failed");
+  t->d_table = (int64_t *)d;
+  auto cleanup = [&]() { (void)hipFree(t->d_table); };
+  hipError_t e = ccj::launch_fill(t->d_table, size, -1, s);
+  if (e == hipSuccess) e = ccj::launch_lp_insert(d_keys, n, t->d_table, (uint32_t)(size - 1), s);
+  const uint64_t n_seg = (size + ccj::kRunSegment - 1) / ccj::kRunSegment;
+  uint32_t *d_stats = nullptr;
+  if (e == hipSuccess) e = hipMalloc(&d_stats, n_seg * 4 * sizeof(uint32_t));
+  if (e == hipSuccess) e = ccj::launch_lp_runs(t->d_table, size, d_stats, s);
+  std::vector<uint32_t> st(n_seg * 4);
+  if (e == hipSuccess) e = hipMemcpyAsync(st.data(), d_stats, st.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (d_stats) (void)hipFree(d_stats);
+  if (e != hipSuccess) {
+    cleanup();
+    return hip_fail(e, "device LP build");
+  }
+  // combine per-segment run stats (circular)
+  uint64_t best = 0, carry = 0;
+  for (uint64_t g = 0; g < n_seg; ++g) {
+    const uint32_t lead = st[g * 4], trail = st[g * 4 + 1], inner = st[g * 4 + 2], full = st[g * 4 + 3];
+    if (full) {
+      carry += lead;
+      continue;
+    }
+    best = std::max<uint64_t>(best, std::max<uint64_t>(inner, carry + lead));
+    carry = trail;
+  }
+  if (n_seg) best = std::max<uint64_t>(best, carry + st[0]);
+  t->info.kind = CCJ_TABLE_LP;
+  t->info.layout = CCJ_LAYOUT_DEVICE;
+  t->info.n_keys = n;
+  t->info.size = size;
+  t->info.max_rounds = (uint32_t)best;
+  // all copies of a key share a home slot, so they sit in one run: multiplicity <= longest run.
+  t->info.max_dup = known_dup ? known_dup : best;
+  t->info.d_table = t->d_table;
+  (void)hipGetDevice(&t->device);
+  *out = t.release();
+  return CCJ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *ccj_last_error(void) { return g_err.c_str(); }
+
+int ccj_abi_version(void) { return CCJ_ABI_VERSION; }
+
+int ccj_device_init(int device) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0) return fail(CCJ_ERR_NO_DEVICE, "no HIP device visible");
+  if (device < 0 || device >= n) return fail(CCJ_ERR_INVALID, "device index out of range");
+  HIP_TRY(hipSetDevice(device), "hipSetDevice");
+  return check_device();
+}
+
+int ccj_table_build_reference(int kind, uint64_t n, uint64_t cf, int layout, ccj_stream stream, ccj_table **out) {
+  if (!out || cf == 0) return fail(CCJ_ERR_INVALID, "ccj_table_build_reference: bad argument");
+  if (kind != CCJ_TABLE_LP && kind != CCJ_TABLE_CHAIN) return fail(CCJ_ERR_INVALID, "bad table kind");
+  if (int rc = check_device()) return rc;
+  *out = nullptr;
+  if (layout == CCJ_LAYOUT_REFERENCE || kind == CCJ_TABLE_CHAIN) {
+    std::vector<int64_t> keys = reference_keys(n, cf);
+    return kind == CCJ_TABLE_LP ? build_lp_host(keys.data(), n, out) : build_chain_host(keys.data(), n, out);
+  }
+  if (layout != CCJ_LAYOUT_DEVICE) return fail(CCJ_ERR_INVALID, "bad layout");
+  hipStream_t s = (hipStream_t)stream;
+  int64_t *d_keys = nullptr;
+  if (hipMalloc(&d_keys, std::max<uint64_t>(n, 1) * sizeof(int64_t)) != hipSuccess)
+    return fail(CCJ_ERR_OOM, "reference keys: hipMalloc failed");
+  hipError_t e = ccj::launch_gen_reference_keys(d_keys, n, cf, s);
+  if (e != hipSuccess) {
+    (void)hipFree(d_keys);
+    return hip_fail(e, "gen reference keys");
+  }
+  const uint64_t dup = std::max<uint64_t>(1, std::min<uint64_t>(cf, n));  // first group: min(cf, n) copies
+  int rc = build_lp_device(d_keys, n, s, dup, out);
+  (void)hipStreamSynchronize(s);
+  (void)hipFree(d_keys);
+  return rc;
+}
+
+int ccj_table_build_from_host(int kind, const int64_t *h_keys, uint64_t n, ccj_table **out) {
+  if (!out || (!h_keys && n)) return fail(CCJ_ERR_INVALID, "ccj_table_build_from_host: bad argument");
+  if (int rc = check_device()) return rc;
+  *out = nullptr;
+  if (kind == CCJ_TABLE_LP) return build_lp_host(h_keys, n, out);
+  if (kind == CCJ_TABLE_CHAIN) return build_chain_host(h_keys, n, out);
+  return fail(CCJ_ERR_INVALID, "bad table kind");
+}
+
+int ccj_table_build_on_device(int kind, const int64_t *d_keys, uint64_t n, ccj_stream stream, ccj_table **out) {
+  if (!out || (!d_keys && n)) return fail(CCJ_ERR_INVALID, "ccj_table_build_on_device: bad argument");
+  if (int rc = check_device()) return rc;
+  *out = nullptr;
+  if (kind == CCJ_TABLE_LP) return build_lp_device(d_keys, n, (hipStream_t)stream, 0, out);
+  if (kind == CCJ_TABLE_CHAIN) {
+    // Chain order must equal insertion order; until the device counting sort lands, stage on host.
+    std::vector<int64_t> h(n);
+    if (n) HIP_TRY(hipMemcpy(h.data(), d_keys, n * sizeof(int64_t), hipMemcpyDeviceToHost), "download keys");
+    return build_chain_host(h.data(), n, out);
+  }
+  return fail(CCJ_ERR_INVALID, "bad table kind");
+}
+
+int ccj_table_get_info(const ccj_table *t, ccj_table_info *info) {
+  if (!t || !info) return fail(CCJ_ERR_INVALID, "ccj_table_get_info: null");
+  *info = t->info;
+  return CCJ_OK;
+}
+
+int ccj_table_free(ccj_table *t) {
+  if (!t) return CCJ_OK;
+  if (t->d_table) (void)hipFree(t->d_table);
+  if (t->d_off) (void)hipFree(t->d_off);
+  delete t;
+  return CCJ_OK;
+}
+
+int ccj_probe(const ccj_table *t, const ccj_probe_args *a, ccj_stream stream) {
+  if (!t || !a) return fail(CCJ_ERR_INVALID, "ccj_probe: null table/args");
+  if (a->chunk == 0 || a->chunk > ccj::kMaxChunk) return fail(CCJ_ERR_INVALID, "ccj_probe: chunk must be 1..2048");
+  if (a->n_rows == 0) return CCJ_OK;  // no chunks: nothing to launch
+  if (!a->out_count || !a->out_sel || !a->keys) return fail(CCJ_ERR_INVALID, "ccj_probe: missing buffer");
+  if (a->out_round_counts && a->max_rounds == 0) return fail(CCJ_ERR_INVALID, "ccj_probe: max_rounds == 0");
+  ccj::ProbeParams p{};
+  p.table = t->d_table;
+  p.off = t->d_off;
+  p.mask = (uint32_t)(t->info.size - 1);
+  p.keys = a->keys;
+  p.sel = a->sel;
+  p.counts = a->counts;
+  p.n_rows = a->n_rows;
+  p.n_chunks = (a->n_rows + a->chunk - 1) / a->chunk;
+  p.chunk = a->chunk;
+  p.max_rounds = a->max_rounds;
+  p.cap = a->cap;
+  p.out_count = a->out_count;
+  p.out_sel = a->out_sel;
+  p.out_payload = a->out_payload;
+  p.out_rounds = a->out_rounds;
+  p.out_round_counts = a->out_round_counts;
+  p.status = a->status;
+  HIP_TRY(ccj::launch_probe(t->info.kind, p, (hipStream_t)stream), "probe launch");
+  return CCJ_OK;
+}
+
+int ccj_gen_uniform_keys(int64_t *d_out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t range,
+                         ccj_stream stream) {
+  if ((!d_out && n) || range == 0) return fail(CCJ_ERR_INVALID, "ccj_gen_uniform_keys: bad argument");
+  HIP_TRY(ccj::launch_gen_uniform(d_out, n, seed, first_row, range, (hipStream_t)stream), "gen uniform keys");
+  return CCJ_OK;
+}
+
+int ccj_probe_cost(const ccj_table *t, const int64_t *d_keys, uint64_t n, uint64_t *d_acc, ccj_stream stream) {
+  if (!t || (!d_keys && n) || !d_acc) return fail(CCJ_ERR_INVALID, "ccj_probe_cost: bad argument");
+  HIP_TRY(ccj::launch_probe_cost(t->info.kind, t->d_table, t->d_off, (uint32_t)(t->info.size - 1), d_keys, n,
+                                 (unsigned long long *)d_acc, (hipStream_t)stream),
+          "probe cost");
+  return CCJ_OK;
+}
+
+int ccj_result_checksum(const uint32_t *out_count, const uint32_t *out_sel, const int64_t *out_payload,
+                        uint64_t n_chunks, uint64_t cap, uint32_t chunk, uint64_t row_base, uint64_t *d_acc,
+                        ccj_stream stream) {
+  if ((!out_count || !out_sel || !out_payload) && n_chunks) return fail(CCJ_ERR_INVALID, "ccj_result_checksum: null");
+  if (!d_acc) return fail(CCJ_ERR_INVALID, "ccj_result_checksum: null acc");
+  HIP_TRY(ccj::launch_result_checksum(out_count, out_sel, out_payload, n_chunks, cap, chunk, row_base,
+                                      (unsigned long long *)d_acc, (hipStream_t)stream),
+          "result checksum");
+  return CCJ_OK;
+}
+
+}  // extern "C"

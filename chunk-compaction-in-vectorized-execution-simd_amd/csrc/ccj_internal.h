@@ -1,0 +1,71 @@
+// ccj_internal.h — shared between the HIP kernels (ccj_kernels.hip) and the C ABI (ccj_api.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "ccj.h"
+
+struct ccj_table {
+  ccj_table_info info;
+  int64_t *d_table = nullptr;   // LP slots / chain keys
+  uint32_t *d_off = nullptr;    // chain CSR offsets (size + 1)
+  int device = 0;
+};
+
+namespace ccj {
+
+// hash_functions.h:8-16 — the reference's bucket/slot function (NOT MurmurHash3 fmix64).
+__host__ __device__ __forceinline__ uint64_t murmurhash64(uint64_t x) {
+  x ^= x >> 32;
+  x *= 0xd6e8feb86659fd93ULL;
+  x ^= x >> 32;
+  x *= 0xd6e8feb86659fd93ULL;
+  x ^= x >> 32;
+  return x;
+}
+
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr uint32_t kMaxChunk = 2048;
+
+struct ProbeParams {
+  const int64_t *table;
+  const uint32_t *off;
+  uint32_t mask;  // size - 1 (size <= 2^32)
+  const int64_t *keys;
+  const uint32_t *sel;
+  const uint32_t *counts;
+  uint64_t n_rows;
+  uint64_t n_chunks;
+  uint32_t chunk;
+  uint32_t max_rounds;
+  uint64_t cap;
+  uint32_t *out_count;
+  uint32_t *out_sel;
+  int64_t *out_payload;
+  uint32_t *out_rounds;
+  uint32_t *out_round_counts;
+  uint32_t *status;
+};
+
+// Launchers (ccj_kernels.hip).  Return hipError_t of the launch.
+hipError_t launch_probe(int kind, const ProbeParams &p, hipStream_t s);
+hipError_t launch_gen_reference_keys(int64_t *out, uint64_t n, uint64_t cf, hipStream_t s);
+hipError_t launch_fill(int64_t *p, uint64_t n, int64_t v, hipStream_t s);
+hipError_t launch_lp_insert(const int64_t *keys, uint64_t n, int64_t *slots, uint32_t mask, hipStream_t s);
+// Per-segment run statistics of an LP slot array (segment = 4096 slots): 4 x uint32 per segment:
+// {leading run, trailing run, longest run, all occupied}.
+hipError_t launch_lp_runs(const int64_t *slots, uint64_t n_slots, uint32_t *seg_stats, hipStream_t s);
+constexpr uint64_t kRunSegment = 4096;
+hipError_t launch_gen_uniform(int64_t *out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t range,
+                              hipStream_t s);
+hipError_t launch_probe_cost(int kind, const int64_t *table, const uint32_t *off, uint32_t mask,
+                             const int64_t *keys, uint64_t n, unsigned long long *acc, hipStream_t s);
+hipError_t launch_result_checksum(const uint32_t *count, const uint32_t *sel, const int64_t *payload,
+                                  uint64_t n_chunks, uint64_t cap, uint32_t chunk, uint64_t row_base,
+                                  unsigned long long *acc, hipStream_t s);
+
+}  // namespace ccj

@@ -1,0 +1,382 @@
+// ccj_kernels.hip — gfx950 kernels for the hash-join probe hot path.
+//
+// probe_chunks<KIND, R>: one wavefront per chunk (up to 64*R rows; lane l owns rows j*64 + l).
+// It runs the reference's Probe + Next loop for the whole chunk in one pass:
+//   Probe   linear_probing_ht.cpp:45-57 / chaining_ht.cpp:44-55: hash, first candidate, active set
+//   Next    match-pack  (:72-80 / :88-99)   -> wave ballot + mbcnt prefix, ordered store
+//           payload     (:90-94 / :126-136) -> the matched table value, stored beside the row id
+//           advance     (:100-110 / :109-124) -> next slot / next chain node; its candidate is
+//                                               compared right away, so the next round's match
+//                                               bits are ready without re-reading the table.
+// Emission order is round-major, idx ascending within a round: exactly the reference's
+// result_vector order (L3).  Per-row state lives in VGPRs (key, slot/chain position, chain end);
+// active/match sets are bitmasks over the lane's R rows.
+#include "ccj_internal.h"
+
+namespace ccj {
+namespace {
+
+__device__ __forceinline__ uint32_t lane_prefix(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+template <int KIND, int R>
+__global__ __launch_bounds__(kWave *kWavesPerBlock) void probe_chunks(ProbeParams p) {
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint64_t c = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x / kWave);
+  if (c >= p.n_chunks) return;  // wave-uniform
+  const uint64_t base = c * p.chunk;
+  const uint64_t rem = p.n_rows - base;
+  const uint32_t phys = rem < p.chunk ? (uint32_t)rem : p.chunk;
+  uint32_t count = p.counts ? p.counts[c] : phys;
+  uint32_t flags = 0;
+  if (count > p.chunk) {
+    flags |= CCJ_FLAG_BAD_INPUT;
+    count = p.chunk;
+  }
+
+  int64_t key[R];
+  uint32_t pos[R];
+  uint32_t end[R];
+  uint32_t act = 0, mat = 0;
+
+  // Probe: gather keys through sel, hash, bucket/slot.
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const uint32_t i = j * kWave + lane;
+    key[j] = 0;
+    pos[j] = 0;
+    end[j] = 0;
+    if (i < count) {
+      const uint32_t r = p.sel ? p.sel[base + i] : i;
+      if (r < phys) {
+        key[j] = p.keys[base + r];
+        act |= 1u << j;
+      } else {
+        flags |= CCJ_FLAG_BAD_INPUT;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    if ((act >> j) & 1u) {
+      const uint32_t h = (uint32_t)murmurhash64((uint64_t)key[j]) & p.mask;
+      if (KIND == CCJ_TABLE_LP) {
+        pos[j] = h;
+      } else {
+        pos[j] = p.off[h];
+        end[j] = p.off[h + 1];
+      }
+    }
+  }
+  // First candidate of every row: the non-empty pack of Probe and the round-0 match bits.
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    if ((act >> j) & 1u) {
+      if (KIND == CCJ_TABLE_LP) {
+        const int64_t v = p.table[pos[j]];
+        if (v == -1) act &= ~(1u << j);        // empty slot: not in the active set
+        else if (v == key[j]) mat |= 1u << j;  // (a probe key of -1 never matches)
+      } else {
+        if (pos[j] == end[j]) {
+          act &= ~(1u << j);
+        } else if (p.table[pos[j]] == key[j]) {
+          mat |= 1u << j;
+        }
+      }
+    }
+  }
+
+  const uint64_t obase = c * p.cap;
+  uint64_t total = 0;  // wave-uniform
+  uint32_t round = 0;
+  while (__ballot(act != 0u) != 0ull) {
+    uint32_t rc = 0;
+    // match-pack + payload, idx ascending = (j, lane) ascending
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const bool m = (mat >> j) & 1u;
+      const uint64_t mb = __ballot(m);
+      if (mb != 0ull) {
+        if (m) {
+          const uint64_t o = total + lane_prefix(mb);
+          if (o < p.cap) {
+            const uint32_t i = j * kWave + lane;
+            p.out_sel[obase + o] = p.sel ? p.sel[base + i] : i;
+            if (p.out_payload) p.out_payload[obase + o] = key[j];  // matched value == probe key
+          }
+        }
+        const uint32_t n = (uint32_t)__popcll(mb);
+        total += n;
+        rc += n;
+      }
+    }
+    if (p.out_round_counts) {
+      if (round < p.max_rounds) {
+        if (lane == 0) p.out_round_counts[c * p.max_rounds + round] = rc;
+      } else {
+        flags |= CCJ_FLAG_ROUND_OVERFLOW;
+      }
+    }
+    ++round;
+    // advance-pack: step every active row, drop rows that ran into an empty slot / chain end,
+    // and pre-compute the next round's match bits.
+    mat = 0;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      if ((act >> j) & 1u) {
+        if (KIND == CCJ_TABLE_LP) {
+          pos[j] = (pos[j] + 1u) & p.mask;
+          const int64_t v = p.table[pos[j]];
+          if (v == -1) act &= ~(1u << j);
+          else if (v == key[j]) mat |= 1u << j;
+        } else {
+          pos[j] += 1u;
+          if (pos[j] == end[j]) {
+            act &= ~(1u << j);
+          } else if (p.table[pos[j]] == key[j]) {
+            mat |= 1u << j;
+          }
+        }
+      }
+    }
+  }
+
+  if (total > p.cap) flags |= CCJ_FLAG_CAP_OVERFLOW;
+  if (lane == 0) {
+    p.out_count[c] = (uint32_t)(total < p.cap ? total : p.cap);
+    if (p.out_rounds) p.out_rounds[c] = round;
+  }
+  if (p.status) {
+    const uint64_t any = __ballot(flags != 0u);
+    if (any && flags) atomicOr(p.status, flags);
+  }
+}
+
+template <int KIND>
+hipError_t launch_kind(const ProbeParams &p, hipStream_t s) {
+  const dim3 block(kWave * kWavesPerBlock);
+  const dim3 grid((unsigned)((p.n_chunks + kWavesPerBlock - 1) / kWavesPerBlock));
+  const uint32_t r = (p.chunk + kWave - 1) / kWave;
+  if (r <= 1) hipLaunchKernelGGL((probe_chunks<KIND, 1>), grid, block, 0, s, p);
+  else if (r <= 2) hipLaunchKernelGGL((probe_chunks<KIND, 2>), grid, block, 0, s, p);
+  else if (r <= 4) hipLaunchKernelGGL((probe_chunks<KIND, 4>), grid, block, 0, s, p);
+  else if (r <= 8) hipLaunchKernelGGL((probe_chunks<KIND, 8>), grid, block, 0, s, p);
+  else if (r <= 16) hipLaunchKernelGGL((probe_chunks<KIND, 16>), grid, block, 0, s, p);
+  else if (r <= 32) hipLaunchKernelGGL((probe_chunks<KIND, 32>), grid, block, 0, s, p);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+// linear_probing_ht.cpp:16-25: key t of the generator is (t / cf) * step.
+__global__ void gen_reference_keys(int64_t *out, uint64_t n, uint64_t cf, uint64_t step) {
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x)
+    out[t] = (int64_t)((t / cf) * step);
+}
+
+__global__ void fill_i64(int64_t *p, uint64_t n, int64_t v) {
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x)
+    p[t] = v;
+}
+
+// Parallel linear-probing insert (CCJ_LAYOUT_DEVICE): CAS into the first empty slot at or after
+// h(k) & mask.  Occupied-slot set and per-cluster key sets equal the sequential build's.
+__global__ void lp_insert(const int64_t *keys, uint64_t n, int64_t *slots, uint32_t mask) {
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+    const int64_t k = keys[t];
+    if (k == -1) continue;  // the reference "stores" -1 into an empty slot: a no-op
+    uint32_t s = (uint32_t)murmurhash64((uint64_t)k) & mask;
+    while (true) {
+      const unsigned long long old =
+          atomicCAS(reinterpret_cast<unsigned long long *>(slots + s), ~0ull, (unsigned long long)k);
+      if (old == ~0ull) break;
+      s = (s + 1u) & mask;
+    }
+  }
+}
+
+// Longest occupied run per 4096-slot segment: one wave per segment, 64 slots per step.
+__global__ __launch_bounds__(256) void lp_runs(const int64_t *slots, uint64_t n_slots, uint32_t *stats) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t seg = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t n_seg = (n_slots + kRunSegment - 1) / kRunSegment;
+  if (seg >= n_seg) return;
+  const uint64_t b = seg * kRunSegment;
+  uint32_t lead = 0, cur = 0, best = 0;
+  bool in_lead = true;
+  for (uint64_t s = 0; s < kRunSegment; s += 64) {
+    const uint64_t i = b + s + lane;
+    const bool occ = i < n_slots && slots[i] != -1;
+    uint64_t m = __ballot(occ);
+    if (i - lane >= n_slots) break;  // wave-uniform
+    // run continuing from the previous step
+    const uint32_t lo = m == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~m);
+    if (in_lead) {
+      lead += lo;
+      if (lo < 64) in_lead = false;
+    }
+    if (lo == 64) {
+      cur += 64;
+    } else {
+      cur += lo;
+      best = cur > best ? cur : best;
+      // longest run strictly inside the mask
+      uint64_t x = m >> lo;
+      uint32_t inner = 0;
+      uint64_t y = x;
+      while (y) {
+        y &= y >> 1;
+        ++inner;
+      }
+      best = inner > best ? inner : best;
+      cur = m == 0 ? 0u : (uint32_t)__builtin_clzll(~m);  // trailing run (top bits)
+    }
+    best = cur > best ? cur : best;
+  }
+  if (lane == 0) {
+    stats[seg * 4 + 0] = lead;
+    stats[seg * 4 + 1] = cur;
+    stats[seg * 4 + 2] = best;
+    stats[seg * 4 + 3] = in_lead ? 1u : 0u;
+  }
+}
+
+// SplitMix64 stream (oracle/ccj_gen.h ccj_splitmix_at): output i of a generator seeded `seed`.
+__device__ __forceinline__ uint64_t splitmix_at(uint64_t seed, uint64_t i) {
+  uint64_t z = seed + (i + 1) * 0x9e3779b97f4a7c15ULL;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
+__global__ void gen_uniform(int64_t *out, uint64_t n, uint64_t seed, uint64_t first, uint64_t range) {
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x)
+    out[t] = (int64_t)(splitmix_at(seed, first + t) % range);
+}
+
+template <int KIND>
+__global__ void probe_cost(const int64_t *table, const uint32_t *off, uint32_t mask, const int64_t *keys,
+                           uint64_t n, unsigned long long *acc) {
+  unsigned long long ex = 0, mt = 0;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+    const int64_t k = keys[t];
+    const uint32_t h = (uint32_t)murmurhash64((uint64_t)k) & mask;
+    if (KIND == CCJ_TABLE_LP) {
+      uint32_t s = h;
+      while (true) {
+        const int64_t v = table[s];
+        ++ex;
+        if (v == -1) break;
+        mt += v == k;
+        s = (s + 1u) & mask;
+      }
+    } else {
+      for (uint32_t q = off[h], e = off[h + 1]; q < e; ++q) {
+        ++ex;
+        mt += table[q] == k;
+      }
+    }
+  }
+  for (int d = 32; d > 0; d >>= 1) {
+    ex += __shfl_xor(ex, d);
+    mt += __shfl_xor(mt, d);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(acc, ex);
+    atomicAdd(acc + 1, mt);
+  }
+}
+
+__device__ __forceinline__ uint64_t fmix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
+// One wave per output chunk region; matches + L2 checksum (oracle/ccj_gen.h ccj_l2_term).
+__global__ __launch_bounds__(256) void result_checksum(const uint32_t *count, const uint32_t *sel,
+                                                       const int64_t *payload, uint64_t n_chunks, uint64_t cap,
+                                                       uint32_t chunk, uint64_t row_base,
+                                                       unsigned long long *acc) {
+  const uint32_t lane = threadIdx.x & 63u;
+  unsigned long long m = 0, l2 = 0;
+  for (uint64_t c = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < n_chunks; c += (uint64_t)gridDim.x * 4) {
+    const uint32_t n = count[c];
+    m += n;
+    for (uint32_t j = lane; j < n; j += 64) {
+      const uint64_t row = row_base + c * chunk + sel[c * cap + j];
+      l2 += fmix64(row * 0x9e3779b97f4a7c15ULL + fmix64((uint64_t)payload[c * cap + j] + 1ULL));
+    }
+  }
+  for (int d = 32; d > 0; d >>= 1) l2 += __shfl_xor(l2, d);
+  if (lane == 0) {
+    atomicAdd(acc, m);
+    atomicAdd(acc + 1, l2);
+  }
+}
+
+unsigned grid_for(uint64_t n, unsigned block) {
+  uint64_t g = (n + block - 1) / block;
+  if (g > 65536) g = 65536;
+  if (g == 0) g = 1;
+  return (unsigned)g;
+}
+
+}  // namespace
+
+hipError_t launch_probe(int kind, const ProbeParams &p, hipStream_t s) {
+  if (p.n_chunks == 0) return hipSuccess;
+  return kind == CCJ_TABLE_LP ? launch_kind<CCJ_TABLE_LP>(p, s) : launch_kind<CCJ_TABLE_CHAIN>(p, s);
+}
+
+hipError_t launch_gen_reference_keys(int64_t *out, uint64_t n, uint64_t cf, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint64_t num_unique = n / cf + (n % cf != 0);
+  const uint64_t step = n / num_unique;
+  hipLaunchKernelGGL(gen_reference_keys, dim3(grid_for(n, 256)), dim3(256), 0, s, out, n, cf, step);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill(int64_t *p, uint64_t n, int64_t v, hipStream_t s) {
+  hipLaunchKernelGGL(fill_i64, dim3(grid_for(n, 256)), dim3(256), 0, s, p, n, v);
+  return hipGetLastError();
+}
+
+hipError_t launch_lp_insert(const int64_t *keys, uint64_t n, int64_t *slots, uint32_t mask, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(lp_insert, dim3(grid_for(n, 256)), dim3(256), 0, s, keys, n, slots, mask);
+  return hipGetLastError();
+}
+
+hipError_t launch_gen_uniform(int64_t *out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t range,
+                              hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(gen_uniform, dim3(grid_for(n, 256)), dim3(256), 0, s, out, n, seed, first_row, range);
+  return hipGetLastError();
+}
+
+hipError_t launch_probe_cost(int kind, const int64_t *table, const uint32_t *off, uint32_t mask,
+                             const int64_t *keys, uint64_t n, unsigned long long *acc, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const dim3 g(grid_for(n, 256)), b(256);
+  if (kind == CCJ_TABLE_LP) hipLaunchKernelGGL(probe_cost<CCJ_TABLE_LP>, g, b, 0, s, table, off, mask, keys, n, acc);
+  else hipLaunchKernelGGL(probe_cost<CCJ_TABLE_CHAIN>, g, b, 0, s, table, off, mask, keys, n, acc);
+  return hipGetLastError();
+}
+
+hipError_t launch_result_checksum(const uint32_t *count, const uint32_t *sel, const int64_t *payload,
+                                  uint64_t n_chunks, uint64_t cap, uint32_t chunk, uint64_t row_base,
+                                  unsigned long long *acc, hipStream_t s) {
+  if (n_chunks == 0) return hipSuccess;
+  hipLaunchKernelGGL(result_checksum, dim3(grid_for(n_chunks, 4)), dim3(256), 0, s, count, sel, payload, n_chunks,
+                     cap, chunk, row_base, acc);
+  return hipGetLastError();
+}
+
+hipError_t launch_lp_runs(const int64_t *slots, uint64_t n_slots, uint32_t *seg_stats, hipStream_t s) {
+  const uint64_t n_seg = (n_slots + kRunSegment - 1) / kRunSegment;
+  hipLaunchKernelGGL(lp_runs, dim3((unsigned)((n_seg + 3) / 4)), dim3(256), 0, s, slots, n_slots, seg_stats);
+  return hipGetLastError();
+}
+
+}  // namespace ccj

@@ -1,0 +1,150 @@
+/* ccj.h — C ABI of the MI355X hash-join probe / chunk-compaction engine (libccj.so).
+ *
+ * This is the drop-in boundary for the reference's hot path.  The reference has
+ * no FFI: its operator surface is C++ in namespace simd_compaction.  Each entry point below names
+ * the reference interface it replaces; the C++ host facade (host/ccj_operators.h) re-exposes that
+ * surface on top of this ABI, and INTEGRATION.md shows the bindings a maintainer would add.
+ *
+ * Conventions
+ *  - C linkage, no exceptions cross the boundary.  Every call returns CCJ_OK (0) or a negative
+ *    status; ccj_last_error() (thread-local) describes the last failure.
+ *  - Device pointers are caller-owned unless created by ccj_table_*; calls taking a stream are
+ *    stream-ordered and never synchronise the host (graph-capturable), except the table builders.
+ *  - A built table is immutable: concurrent probes on different streams are allowed.
+ *  - There is no CPU fallback.  Without a usable gfx950 device every call fails with
+ *    CCJ_ERR_NO_DEVICE.
+ *  - All keys are int64; -1 is the reserved empty marker (linear_probing_ht.cpp:7, base.h:52).
+ */
+#ifndef CCJ_H
+#define CCJ_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CCJ_ABI_VERSION 1
+
+enum ccj_status {
+  CCJ_OK = 0,
+  CCJ_ERR_INVALID = -1,   /* bad argument */
+  CCJ_ERR_HIP = -2,       /* HIP runtime error */
+  CCJ_ERR_NO_DEVICE = -3, /* no gfx950 device */
+  CCJ_ERR_OOM = -4,       /* device allocation failed */
+  CCJ_ERR_LIMIT = -5      /* size outside the supported range */
+};
+
+/* Device-side status bits a probe / compaction may raise (ccj_probe_args.status). */
+enum ccj_flag {
+  CCJ_FLAG_CAP_OVERFLOW = 1u,   /* a chunk produced more than `cap` matches (extra matches dropped) */
+  CCJ_FLAG_ROUND_OVERFLOW = 2u, /* a chunk took more than `max_rounds` rounds (counts not recorded) */
+  CCJ_FLAG_BAD_INPUT = 4u       /* count > chunk or a sel entry outside the chunk (rows skipped) */
+};
+
+enum ccj_table_kind {
+  CCJ_TABLE_LP = 0,   /* LPHashTable      linear_probing_ht.h:56-71 */
+  CCJ_TABLE_CHAIN = 1 /* HashTable        chaining_ht.h:86-101      */
+};
+
+enum ccj_layout {
+  /* Slot/chain order identical to the reference's sequential insertion (L3 parity).
+   * LP: inserted on the host, uploaded.  Chain: stable order on device or host. */
+  CCJ_LAYOUT_REFERENCE = 0,
+  /* Built on the device.  LP: parallel atomicCAS insert — same occupied slots and same per-probe
+   * match multiset as the reference, slot order inside a cluster may differ (L1/L2 parity).
+   * Chain: stable counting sort — identical to the reference order (L3). */
+  CCJ_LAYOUT_DEVICE = 1
+};
+
+typedef void *ccj_stream; /* hipStream_t; NULL = the default stream */
+typedef struct ccj_table ccj_table;
+
+typedef struct ccj_table_info {
+  int32_t kind;           /* ccj_table_kind */
+  int32_t layout;         /* ccj_layout */
+  uint64_t n_keys;        /* build tuples inserted */
+  uint64_t size;          /* LP: n_slots (pow2 >= 4n, linear_probing_ht.cpp:5-6);
+                             chain: n_buckets (pow2 >= 2n, chaining_ht.cpp:5-6) */
+  uint64_t max_dup;       /* largest multiplicity of one key = max matches per probe row */
+  uint32_t max_rounds;    /* largest number of Next rounds any probe chunk can take
+                             (LP: longest occupied run; chain: longest chain) */
+  uint32_t reserved;
+  const int64_t *d_table; /* LP: slots int64[size]; chain: chain keys int64[n_keys] */
+  const uint32_t *d_bucket_off; /* chain: uint32[size + 1] CSR offsets; LP: NULL */
+} ccj_table_info;
+
+/* ---- device / errors ---------------------------------------------------------------------- */
+const char *ccj_last_error(void);
+int ccj_abi_version(void);
+/* Selects the HIP device for this thread and checks it is gfx950. */
+int ccj_device_init(int device);
+
+/* ---- tables ------------------------------------------------------------------------------- */
+/* Replaces LPHashTable::LPHashTable(n_rhs_tuples, chunk_factor) (linear_probing_ht.cpp:4-37) and
+ * HashTable::HashTable(n_rhs_tuples, chunk_factor) (chaining_ht.cpp:4-36): generates the
+ * reference's build keys (:14-25) and builds the table in the requested layout. */
+int ccj_table_build_reference(int kind, uint64_t n_rhs_tuples, uint64_t chunk_factor, int layout,
+                              ccj_stream stream, ccj_table **out);
+/* Same tables from caller keys, inserted in array order (host keys; CCJ_LAYOUT_REFERENCE). */
+int ccj_table_build_from_host(int kind, const int64_t *h_keys, uint64_t n, ccj_table **out);
+/* Same tables from device-resident keys, built on the device (CCJ_LAYOUT_DEVICE). */
+int ccj_table_build_on_device(int kind, const int64_t *d_keys, uint64_t n, ccj_stream stream,
+                              ccj_table **out);
+int ccj_table_get_info(const ccj_table *table, ccj_table_info *info);
+int ccj_table_free(ccj_table *table);
+
+/* ---- probe -------------------------------------------------------------------------------- */
+/* Batched form of Probe + the whole `while (HasNext()) Next(...)` loop
+ *   LPHashTable::Probe / LPScanStructure::Next   linear_probing_ht.cpp:39-60, :62-115
+ *   HashTable::Probe   / ScanStructure::Next     chaining_ht.cpp:38-58,  :60-136
+ * over many chunks in one launch (one wavefront per chunk).
+ *
+ * Input chunk c = physical rows [c*chunk, min((c+1)*chunk, n_rows)) of `keys`; its active rows
+ * are sel[c*chunk + i] for i < count_c (sel NULL = identity, counts NULL = all physical rows).
+ * Output, per chunk, in the reference's emission order (round-major, idx ascending — L3):
+ *   out_sel[c*cap + j]     = result.selection_vector_[...] (chunk-local physical row)
+ *   out_payload[c*cap + j] = the matched table value       (result col m+1 at that row)
+ *   out_count[c]           = matches;  out_rounds[c] = rounds (LP: Next calls)
+ *   out_round_counts[c*max_rounds + r] = matches of round r (optional)
+ * cap >= chunk * max_dup can never overflow. */
+typedef struct ccj_probe_args {
+  const int64_t *keys;       /* device int64[n_rows] */
+  const uint32_t *sel;       /* device uint32[n_chunks*chunk] or NULL */
+  const uint32_t *counts;    /* device uint32[n_chunks] or NULL */
+  uint64_t n_rows;
+  uint32_t chunk;            /* kBlockSize, 1..2048 */
+  uint32_t max_rounds;       /* stride of out_round_counts (0 if NULL) */
+  uint64_t cap;              /* per-chunk output capacity */
+  uint32_t *out_count;       /* device uint32[n_chunks] (required) */
+  uint32_t *out_sel;         /* device uint32[n_chunks*cap] (required) */
+  int64_t *out_payload;      /* device int64[n_chunks*cap] or NULL */
+  uint32_t *out_rounds;      /* device uint32[n_chunks] or NULL */
+  uint32_t *out_round_counts;/* device uint32[n_chunks*max_rounds] or NULL */
+  uint32_t *status;          /* device word, OR-ed with ccj_flag bits, or NULL */
+} ccj_probe_args;
+
+int ccj_probe(const ccj_table *table, const ccj_probe_args *args, ccj_stream stream);
+
+/* ---- workload + measurement helpers (not on the reference's path) ------------------------- */
+/* Synthetic probe column: d_out[i] = SplitMix64(seed) output (first_row + i) mod range — the
+ * stream of oracle/ccj_gen.h ccj_uniform_key, so any row can be regenerated on the host.
+ * Replaces the reference's host-side source (main.cpp:41-55 + DataCollection::FetchChunk). */
+int ccj_gen_uniform_keys(int64_t *d_out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t range,
+                         ccj_stream stream);
+/* Work accounting for the roofline: d_acc[0] += table words examined (LP: slots read including
+ * the terminating empty; chain: chain keys visited), d_acc[1] += matches, over n probe keys. */
+int ccj_probe_cost(const ccj_table *table, const int64_t *d_keys, uint64_t n, uint64_t *d_acc,
+                   ccj_stream stream);
+/* Result verification without a download: d_acc[0] += matches, d_acc[1] += sum of the L2 term
+ * fmix(row * gamma + fmix(payload + 1)) (oracle/ccj_gen.h ccj_l2_term) over every match of a
+ * ccj_probe output, row = row_base + c*chunk + out_sel. */
+int ccj_result_checksum(const uint32_t *out_count, const uint32_t *out_sel, const int64_t *out_payload,
+                        uint64_t n_chunks, uint64_t cap, uint32_t chunk, uint64_t row_base, uint64_t *d_acc,
+                        ccj_stream stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CCJ_H */

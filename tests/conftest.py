@@ -9,3 +9,6 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box via gpurun)")
     config.addinivalue_line("markers", "slow: larger CPU-side cases")
+
+PKG = os.path.join(ROOT, "chunk-compaction-in-vectorized-execution-simd_amd")
+sys.path.insert(0, PKG)

@@ -1,0 +1,160 @@
+"""Parity of the HIP probe path (through the C ABI) against the reference and the oracle.
+
+  L3  every reference golden trace, replayed on device with the reference-order table
+  L2  device-built (atomicCAS) LP tables vs the oracle: multiset of (global row, payload)
+  L1+L2 at larger sizes via the exact membership oracle (size-independent)
+  edge cases: empty input, ragged chunks, every chunk width, -1 keys, overflow flags
+"""
+import numpy as np
+import pytest
+
+from helpers import (assert_trace_equal, known_answers, load_trace, ref_keys, trace_inputs,
+                     views_from_rounds)
+from oracle import oracle as O
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import ccj  # noqa: E402
+
+KA = known_answers()
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ccj.device_init(0)
+
+
+def to_dev(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.to(DEV)
+
+
+def host(o):
+    torch.cuda.synchronize()
+    return {k: (v.cpu().numpy() if isinstance(v, torch.Tensor) else v) for k, v in o.items()}
+
+
+def matches_of(out, chunk):
+    """(global rows, payloads) of every match, in emission order."""
+    n_chunks, cap = out["n_chunks"], out["cap"]
+    cnt = out["count"].astype(np.int64)
+    valid = np.arange(cap)[None, :] < cnt[:, None]
+    sel = out["sel"].reshape(n_chunks, cap)[valid].astype(np.uint32).astype(np.uint64)
+    pay = out["payload"].reshape(n_chunks, cap)[valid]
+    rows = np.repeat(np.arange(n_chunks, dtype=np.uint64), cnt) * np.uint64(chunk) + sel
+    return rows, pay
+
+
+@pytest.mark.parametrize("name", sorted(KA["trace_cases"]))
+def test_l3_reference_traces(name):
+    entry = KA["trace_cases"][name]
+    spec = entry["spec"]
+    kind = ccj.LP if spec["kind"] == "lp" else ccj.CHAIN
+    table = ccj.Table.reference(kind, spec["n_build"], spec["cf"], ccj.LAYOUT_REFERENCE)
+    assert table.max_dup == min(spec["cf"], spec["n_build"])
+    for view in entry["views"]:
+        trace = load_trace(name, view)
+        keys, sel, counts = trace_inputs(spec, trace)
+        out = host(table.probe(to_dev(keys), spec["B"], sel=to_dev(sel.view(np.int32)),
+                               counts=to_dev(counts.view(np.int32))))
+        assert out["status"][0] == 0
+        got = views_from_rounds(out["count"], out["sel"].view(np.uint32), out["payload"], out["rounds"],
+                                out["round_counts"], out["cap"], out["max_rounds"], merged=(view == "merged"))
+        assert_trace_equal(got, trace)
+
+
+@pytest.mark.parametrize("kind", [ccj.LP, ccj.CHAIN])
+@pytest.mark.parametrize("chunk", [1, 63, 64, 65, 256, 1000, 2047, 2048])
+def test_l3_every_chunk_width_vs_oracle(kind, chunk):
+    bk = ref_keys(20000, 3)
+    table = ccj.Table.from_host(kind, bk)
+    otab = O.Table(kind, bk)
+    keys = O.uniform_keys(11, 0, 50000, 30000)
+    keys[::97] = -1  # the empty marker as a probe key never matches (slot == -1 ends the run)
+    out = host(table.probe(to_dev(keys), chunk))
+    want = otab.probe(keys, chunk, cap_factor=3, max_rounds=out["max_rounds"])
+    assert out["status"][0] == 0
+    for view_merged in (False, True):
+        g = views_from_rounds(out["count"], out["sel"].view(np.uint32), out["payload"], out["rounds"],
+                              out["round_counts"], out["cap"], out["max_rounds"], merged=view_merged)
+        w = views_from_rounds(want["count"], want["sel"], want["payload"], want["rounds"], want["round_counts"],
+                              want["cap"], want["max_rounds"], merged=view_merged)
+        assert_trace_equal(g, w)
+
+
+def test_empty_and_tiny_inputs():
+    table = ccj.Table.reference(ccj.LP, 1000, 1)
+    out = host(table.probe(torch.empty(0, dtype=torch.int64, device=DEV), 2048))
+    assert out["n_chunks"] == 0
+    out = host(table.probe(to_dev(np.array([5], np.int64)), 2048))
+    assert out["count"][0] == 1 and out["sel"][0] == 0 and out["payload"][0] == 5
+    # counts = 0 for a chunk: no active row, zero rounds
+    keys = to_dev(np.arange(4096, dtype=np.int64))
+    out = host(table.probe(keys, 2048, counts=to_dev(np.array([0, 2048], np.int32))))
+    assert out["count"][0] == 0 and out["rounds"][0] == 0 and out["count"][1] == 0  # keys >= 1000 miss
+    out = host(table.probe(keys, 2048, counts=to_dev(np.array([1000, 5], np.int32))))
+    assert out["count"][0] == 1000 and out["count"][1] == 0
+
+
+def test_overflow_and_bad_input_flags():
+    table = ccj.Table.reference(ccj.LP, 4096, 4)
+    keys = to_dev(O.uniform_keys(3, 0, 4096, 4096))
+    out = host(table.probe(keys, 2048, cap=100))
+    assert out["status"][0] & ccj.FLAG_CAP_OVERFLOW
+    assert (out["count"] <= 100).all()
+    o2 = table.alloc_outputs(4096, 2048)
+    o2["max_rounds"] = 1
+    out = host(table.probe(keys, 2048, out=o2))
+    assert out["status"][0] & ccj.FLAG_ROUND_OVERFLOW
+    sel = np.tile(np.arange(2048, dtype=np.int32), 2)
+    sel[5] = 5000
+    out = host(table.probe(keys, 2048, sel=to_dev(sel)))
+    assert out["status"][0] & ccj.FLAG_BAD_INPUT
+
+
+@pytest.mark.parametrize("cf", [1, 2, 5])
+def test_l2_device_built_lp_vs_oracle(cf):
+    n = 1 << 20
+    d_keys = to_dev(ref_keys(n, cf))
+    table = ccj.Table.on_device(ccj.LP, d_keys)
+    otab = O.Table(O.LP, ref_keys(n, cf))
+    probe = O.uniform_keys(99, 0, 4 << 20, 3 * n // 2)
+    out = host(table.probe(to_dev(probe), 2048))
+    assert out["status"][0] == 0
+    rows, pay = matches_of(out, 2048)
+    m, l2 = O.count_uniform(99, 0, 4 << 20, 3 * n // 2, n, cf)
+    assert len(rows) == m
+    assert O.l2_sum(rows, pay) == l2
+    want = otab.probe(probe, 2048, cap_factor=cf, max_rounds=4096)
+    assert table.max_rounds >= int(want["rounds"].max())
+    assert int(out["rounds"].max()) == int(want["rounds"].max())  # rounds depend only on the occupied set
+
+
+def test_device_lp_build_run_stats_match_host_layout():
+    n = 1 << 18
+    host_t = ccj.Table.reference(ccj.LP, n, 1, ccj.LAYOUT_REFERENCE)
+    dev_t = ccj.Table.reference(ccj.LP, n, 1, ccj.LAYOUT_DEVICE)
+    assert host_t.size == dev_t.size
+    assert host_t.max_rounds == dev_t.max_rounds  # the occupied set is insertion-order independent
+
+
+@pytest.mark.parametrize("kind", [ccj.LP, ccj.CHAIN])
+def test_l1_l2_large_membership(kind):
+    n, n_probe, rng = 1 << 22, 1 << 26, 3 << 21
+    table = ccj.Table.reference(kind, n, 1, ccj.LAYOUT_DEVICE)
+    keys = to_dev(O.uniform_keys(7, 0, n_probe, rng))
+    out = table.probe(keys, 2048, rounds=False)
+    torch.cuda.synchronize()
+    assert int(out["status"].item()) == 0
+    cnt = out["count"].to(torch.int64)
+    m, l2 = O.count_uniform(7, 0, n_probe, rng, n, 1)
+    assert int(cnt.sum().item()) == m
+    # L2 checksum computed on the device side of the test with torch integer ops
+    rows, pay = matches_of(host(out), 2048)
+    assert O.l2_sum(rows, pay) == l2
