@@ -119,8 +119,10 @@ int build_lp_host(const int64_t *keys, uint64_t n, ccj_table **out) {
   t->info.n_keys = n;
   t->info.size = size;
   lp_host_stats(slots, &t->info.max_rounds, &t->info.max_dup);
+  // storage padded to >= 4 slots: the probe reads aligned 4-slot windows (n_slots = 1 when n = 0)
+  if (slots.size() < 4) slots.resize(4, -1);
   void *d = nullptr;
-  int rc = upload(&d, slots.data(), size * sizeof(int64_t), "LP slots");
+  int rc = upload(&d, slots.data(), slots.size() * sizeof(int64_t), "LP slots");
   if (rc) return rc;
   t->d_table = (int64_t *)d;
   t->info.d_table = t->d_table;
@@ -169,8 +171,10 @@ int build_chain_host(const int64_t *keys, uint64_t n, ccj_table **out) {
   t->info.size = size;
   t->info.max_rounds = longest;
   t->info.max_dup = dup;
+  // padded to a multiple of 4 keys (>= 4): the probe reads aligned 4-key windows
+  chain.resize(((n + 3) / 4) * 4 + (n == 0 ? 4 : 0), -1);
   void *d = nullptr;
-  int rc = upload(&d, chain.data(), n * sizeof(int64_t), "chain keys");
+  int rc = upload(&d, chain.data(), chain.size() * sizeof(int64_t), "chain keys");
   if (rc) return rc;
   t->d_table = (int64_t *)d;
   rc = upload(&d, off.data(), (size + 1) * sizeof(uint32_t), "chain offsets");
@@ -191,10 +195,11 @@ int build_lp_device(const int64_t *d_keys, uint64_t n, hipStream_t s, uint64_t k
   if (size > (1ull << 32)) return fail(CCJ_ERR_LIMIT, "LP table larger than 2^32 slots");
   std::unique_ptr<ccj_table> t(new ccj_table());
   void *d = nullptr;
-  if (hipMalloc(&d, size * sizeof(int64_t)) != hipSuccess) return fail(CCJ_ERR_OOM, "LP slots: hipMalloc failed");
+  const uint64_t alloc = size < 4 ? 4 : size;  // aligned 4-slot windows
+  if (hipMalloc(&d, alloc * sizeof(int64_t)) != hipSuccess) return fail(CCJ_ERR_OOM, "LP slots: hipMalloc failed");
   t->d_table = (int64_t *)d;
   auto cleanup = [&]() { (void)hipFree(t->d_table); };
-  hipError_t e = ccj::launch_fill(t->d_table, size, -1, s);
+  hipError_t e = ccj::launch_fill(t->d_table, alloc, -1, s);
   if (e == hipSuccess) e = ccj::launch_lp_insert(d_keys, n, t->d_table, (uint32_t)(size - 1), s);
   const uint64_t n_seg = (size + ccj::kRunSegment - 1) / ccj::kRunSegment;
   uint32_t *d_stats = nullptr;

@@ -20,14 +20,112 @@ __device__ __forceinline__ uint32_t lane_prefix(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-template <int KIND, int R>
-__global__ __launch_bounds__(kWave *kWavesPerBlock) void probe_chunks(ProbeParams p) {
-  const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint64_t c = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x / kWave);
-  if (c >= p.n_chunks) return;  // wave-uniform
+// Emits one match: ordered by (round, j, lane) through the wave ballot `mb`.
+__device__ __forceinline__ void emit_match(const ProbeParams &p, uint64_t base, uint64_t obase, uint64_t total,
+                                           uint64_t mb, uint32_t i, int64_t payload) {
+  const uint64_t o = total + lane_prefix(mb);
+  if (o < p.cap) {
+    p.out_sel[obase + o] = p.sel ? p.sel[base + i] : i;
+    if (p.out_payload) p.out_payload[obase + o] = payload;  // matched table value == probe key
+  }
+}
+
+__device__ __forceinline__ uint32_t wave_or(uint32_t x) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) x |= (uint32_t)__shfl_xor((int)x, d);
+  return x;
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    const uint32_t o = (uint32_t)__shfl_xor((int)x, d);
+    x = o > x ? o : x;
+  }
+  return x;
+}
+
+__device__ __forceinline__ void record_round(const ProbeParams &p, uint64_t c, uint32_t r, uint32_t rc,
+                                             uint32_t lane, uint32_t &flags) {
+  if (p.out_round_counts) {
+    if (r < p.max_rounds) {
+      if (lane == 0) p.out_round_counts[c * p.max_rounds + r] = rc;
+    } else {
+      flags |= CCJ_FLAG_ROUND_OVERFLOW;
+    }
+  }
+}
+
+// Generic round-synchronous Next loop for chunks containing a run/chain longer than the
+// kMaxFastRounds rounds the windowed path records: round r reads candidate r of every active row
+// (position recomputed from the key, no per-row position state).  Rare; correctness path.
+template <int KIND>
+__device__ void rounds_generic(const ProbeParams &p, uint64_t c, uint64_t base, const int64_t *s_key, uint32_t nj,
+                               uint32_t act, uint32_t &flags, uint64_t &total_out, uint32_t &rounds_out) {
+  const uint32_t lane = threadIdx.x;
+  const uint64_t obase = c * p.cap;
+  uint64_t total = 0;
+  uint32_t round = 0;
+  while (true) {
+    uint32_t mat = 0;
+    for (uint32_t j = 0; j < nj; ++j) {
+      if ((act >> j) & 1u) {
+        const int64_t k = s_key[j * kWave + lane];
+        const uint32_t h = (uint32_t)murmurhash64((uint64_t)k) & p.mask;
+        if (KIND == CCJ_TABLE_LP) {
+          const int64_t v = p.table[(h + round) & p.mask];
+          if (v == -1) act &= ~(1u << j);  // empty slot ends the run
+          else if (v == k) mat |= 1u << j;  // (a probe key of -1 never matches)
+        } else {
+          const uint32_t q = p.off[h] + round;
+          if (q >= p.off[h + 1]) act &= ~(1u << j);
+          else if (p.table[q] == k) mat |= 1u << j;
+        }
+      }
+    }
+    if (wave_or(act) == 0u) break;
+    uint32_t rc = 0;
+    for (uint32_t any = wave_or(mat); any != 0u; any &= any - 1u) {
+      const uint32_t j = (uint32_t)__builtin_ctz(any);
+      const bool m = (mat >> j) & 1u;
+      const uint64_t mb = __ballot(m);
+      if (m) emit_match(p, base, obase, total, mb, j * kWave + lane, s_key[j * kWave + lane]);
+      const uint32_t n = (uint32_t)__popcll(mb);
+      total += n;
+      rc += n;
+    }
+    record_round(p, c, round, rc, lane, flags);
+    ++round;
+  }
+  total_out = total;
+  rounds_out = round;
+}
+
+constexpr int kWin = 4;             // slots (LP) / chain keys per window load: 32 B, one aligned sector
+constexpr int kMaxFastRounds = 32;  // rounds recorded by the windowed path (bits of a u32)
+
+// One wave per 64-thread workgroup = one chunk of up to 64*nj rows (row (j, lane) = j*64 + lane).
+// LDS (dynamic): s_key[nj*64] int64 probe keys, s_rm[kMaxFastRounds*64] u32 where bit j of
+// s_rm[r*64 + lane] says row (j, lane) matches in round r.
+//
+// Walk: every row's whole run (LP: home slot up to the first empty slot; chain: the bucket's CSR
+// range) is read once through aligned 32-byte windows, G rows per lane in flight; a window is one
+// sector of a 64-byte line, so a continuation re-reads a line fetched moments earlier (L2-resident)
+// rather than one fetched a whole round of 2048 rows earlier (the reference's round-by-round
+// re-read, linear_probing_ht.cpp:72-80 / :100-110, loses L2 residency at GPU occupancy).
+// Emit: for each round r (Next call r), the rows matching in r are packed idx-ascending with a
+// wave ballot + mbcnt prefix: the reference's result_vector order (L3).
+template <int KIND, int G>
+__global__ __launch_bounds__(kWave) void probe_chunks(ProbeParams p) {
+  extern __shared__ __attribute__((aligned(16))) int64_t s_mem[];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t c = blockIdx.x;
   const uint64_t base = c * p.chunk;
   const uint64_t rem = p.n_rows - base;
   const uint32_t phys = rem < p.chunk ? (uint32_t)rem : p.chunk;
+  const uint32_t nj = (p.chunk + kWave - 1) / kWave;
+  int64_t *s_key = s_mem;
+  uint32_t *s_rm = reinterpret_cast<uint32_t *>(s_mem + nj * kWave);
   uint32_t count = p.counts ? p.counts[c] : phys;
   uint32_t flags = 0;
   if (count > p.chunk) {
@@ -35,117 +133,129 @@ __global__ __launch_bounds__(kWave *kWavesPerBlock) void probe_chunks(ProbeParam
     count = p.chunk;
   }
 
-  int64_t key[R];
-  uint32_t pos[R];
-  uint32_t end[R];
-  uint32_t act = 0, mat = 0;
-
-  // Probe: gather keys through sel, hash, bucket/slot.
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
+  // Probe (linear_probing_ht.cpp:45-49 / chaining_ht.cpp:46-50): keys through sel -> LDS.
+  uint32_t act = 0;
+  for (uint32_t j = 0; j < nj; ++j) {
     const uint32_t i = j * kWave + lane;
-    key[j] = 0;
-    pos[j] = 0;
-    end[j] = 0;
+    int64_t k = 0;
     if (i < count) {
       const uint32_t r = p.sel ? p.sel[base + i] : i;
       if (r < phys) {
-        key[j] = p.keys[base + r];
+        k = p.keys[base + r];
         act |= 1u << j;
       } else {
         flags |= CCJ_FLAG_BAD_INPUT;
       }
     }
+    s_key[i] = k;
   }
 #pragma unroll
-  for (int j = 0; j < R; ++j) {
-    if ((act >> j) & 1u) {
-      const uint32_t h = (uint32_t)murmurhash64((uint64_t)key[j]) & p.mask;
-      if (KIND == CCJ_TABLE_LP) {
-        pos[j] = h;
-      } else {
-        pos[j] = p.off[h];
-        end[j] = p.off[h + 1];
+  for (int r = 0; r < kMaxFastRounds; ++r) s_rm[r * kWave + lane] = 0u;
+
+  // Walk.
+  uint32_t lane_rounds = 0;
+  bool long_run = false;
+  for (uint32_t jb = 0; jb < nj; jb += G) {
+    uint32_t cur[G], r0[G], lim[G];
+    int64_t kj[G];
+    uint32_t need = 0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const uint32_t j = jb + g;
+      cur[g] = 0;
+      r0[g] = 0;
+      lim[g] = 0;
+      kj[g] = 0;
+      if (j < nj && ((act >> j) & 1u)) {
+        kj[g] = s_key[j * kWave + lane];
+        const uint32_t h = (uint32_t)murmurhash64((uint64_t)kj[g]) & p.mask;
+        if (KIND == CCJ_TABLE_LP) {
+          cur[g] = h;
+          need |= 1u << g;
+        } else {
+          cur[g] = p.off[h];
+          lim[g] = p.off[h + 1];
+          if (cur[g] != lim[g]) need |= 1u << g;
+        }
       }
     }
-  }
-  // First candidate of every row: the non-empty pack of Probe and the round-0 match bits.
+    while (__ballot(need != 0u) != 0ull) {
+      longlong2 v[G][kWin / 2];
 #pragma unroll
-  for (int j = 0; j < R; ++j) {
-    if ((act >> j) & 1u) {
-      if (KIND == CCJ_TABLE_LP) {
-        const int64_t v = p.table[pos[j]];
-        if (v == -1) act &= ~(1u << j);        // empty slot: not in the active set
-        else if (v == key[j]) mat |= 1u << j;  // (a probe key of -1 never matches)
-      } else {
-        if (pos[j] == end[j]) {
-          act &= ~(1u << j);
-        } else if (p.table[pos[j]] == key[j]) {
-          mat |= 1u << j;
+      for (int g = 0; g < G; ++g) {
+        if ((need >> g) & 1u) {
+          const longlong2 *w = reinterpret_cast<const longlong2 *>(p.table + (cur[g] & ~(uint32_t)(kWin - 1)));
+#pragma unroll
+          for (int q = 0; q < kWin / 2; ++q) v[g][q] = w[q];
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        if ((need >> g) & 1u) {
+          const uint32_t j = jb + g;
+          const uint32_t blk = cur[g] & ~(uint32_t)(kWin - 1);
+          const uint32_t off = cur[g] - blk;
+          bool go = true;
+#pragma unroll
+          for (int q = 0; q < kWin; ++q) {
+            const int64_t val = (q & 1) ? v[g][q >> 1].y : v[g][q >> 1].x;
+            if (go && (uint32_t)q >= off) {
+              const uint32_t r = r0[g] + (uint32_t)q - off;
+              const bool stop = KIND == CCJ_TABLE_LP ? (val == -1) : (blk + (uint32_t)q == lim[g]);
+              if (stop) {
+                go = false;
+                lane_rounds = r > lane_rounds ? r : lane_rounds;
+              } else if (r >= (uint32_t)kMaxFastRounds) {
+                go = false;
+                long_run = true;
+              } else if (val == kj[g]) {
+                atomicOr(&s_rm[r * kWave + lane], 1u << j);  // ds_or_b32, this lane's own word
+              }
+            }
+          }
+          if (go) {
+            r0[g] += (uint32_t)kWin - off;
+            cur[g] = KIND == CCJ_TABLE_LP ? ((blk + kWin) & p.mask) : blk + kWin;
+            if (KIND == CCJ_TABLE_CHAIN && cur[g] == lim[g]) {
+              lane_rounds = r0[g] > lane_rounds ? r0[g] : lane_rounds;
+              need &= ~(1u << g);
+            }
+          } else {
+            need &= ~(1u << g);
+          }
         }
       }
     }
   }
 
-  const uint64_t obase = c * p.cap;
-  uint64_t total = 0;  // wave-uniform
-  uint32_t round = 0;
-  while (__ballot(act != 0u) != 0ull) {
-    uint32_t rc = 0;
-    // match-pack + payload, idx ascending = (j, lane) ascending
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      const bool m = (mat >> j) & 1u;
-      const uint64_t mb = __ballot(m);
-      if (mb != 0ull) {
-        if (m) {
-          const uint64_t o = total + lane_prefix(mb);
-          if (o < p.cap) {
-            const uint32_t i = j * kWave + lane;
-            p.out_sel[obase + o] = p.sel ? p.sel[base + i] : i;
-            if (p.out_payload) p.out_payload[obase + o] = key[j];  // matched value == probe key
-          }
-        }
+  uint64_t total = 0;
+  uint32_t rounds = 0;
+  if (__ballot(long_run) != 0ull) {
+    rounds_generic<KIND>(p, c, base, s_key, nj, act, flags, total, rounds);
+  } else {
+    // Emit: Next loop (linear_probing_ht.cpp:62-115 / chaining_ht.cpp:60-136).
+    rounds = wave_max(lane_rounds);
+    const uint64_t obase = c * p.cap;
+    for (uint32_t r = 0; r < rounds; ++r) {
+      const uint32_t bits = s_rm[r * kWave + lane];
+      uint32_t rc = 0;
+      for (uint32_t any = wave_or(bits); any != 0u; any &= any - 1u) {
+        const uint32_t j = (uint32_t)__builtin_ctz(any);
+        const bool m = (bits >> j) & 1u;
+        const uint64_t mb = __ballot(m);
+        if (m) emit_match(p, base, obase, total, mb, j * kWave + lane, s_key[j * kWave + lane]);
         const uint32_t n = (uint32_t)__popcll(mb);
         total += n;
         rc += n;
       }
-    }
-    if (p.out_round_counts) {
-      if (round < p.max_rounds) {
-        if (lane == 0) p.out_round_counts[c * p.max_rounds + round] = rc;
-      } else {
-        flags |= CCJ_FLAG_ROUND_OVERFLOW;
-      }
-    }
-    ++round;
-    // advance-pack: step every active row, drop rows that ran into an empty slot / chain end,
-    // and pre-compute the next round's match bits.
-    mat = 0;
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      if ((act >> j) & 1u) {
-        if (KIND == CCJ_TABLE_LP) {
-          pos[j] = (pos[j] + 1u) & p.mask;
-          const int64_t v = p.table[pos[j]];
-          if (v == -1) act &= ~(1u << j);
-          else if (v == key[j]) mat |= 1u << j;
-        } else {
-          pos[j] += 1u;
-          if (pos[j] == end[j]) {
-            act &= ~(1u << j);
-          } else if (p.table[pos[j]] == key[j]) {
-            mat |= 1u << j;
-          }
-        }
-      }
+      record_round(p, c, r, rc, lane, flags);
     }
   }
 
   if (total > p.cap) flags |= CCJ_FLAG_CAP_OVERFLOW;
   if (lane == 0) {
     p.out_count[c] = (uint32_t)(total < p.cap ? total : p.cap);
-    if (p.out_rounds) p.out_rounds[c] = round;
+    if (p.out_rounds) p.out_rounds[c] = rounds;
   }
   if (p.status) {
     const uint64_t any = __ballot(flags != 0u);
@@ -155,16 +265,9 @@ __global__ __launch_bounds__(kWave *kWavesPerBlock) void probe_chunks(ProbeParam
 
 template <int KIND>
 hipError_t launch_kind(const ProbeParams &p, hipStream_t s) {
-  const dim3 block(kWave * kWavesPerBlock);
-  const dim3 grid((unsigned)((p.n_chunks + kWavesPerBlock - 1) / kWavesPerBlock));
-  const uint32_t r = (p.chunk + kWave - 1) / kWave;
-  if (r <= 1) hipLaunchKernelGGL((probe_chunks<KIND, 1>), grid, block, 0, s, p);
-  else if (r <= 2) hipLaunchKernelGGL((probe_chunks<KIND, 2>), grid, block, 0, s, p);
-  else if (r <= 4) hipLaunchKernelGGL((probe_chunks<KIND, 4>), grid, block, 0, s, p);
-  else if (r <= 8) hipLaunchKernelGGL((probe_chunks<KIND, 8>), grid, block, 0, s, p);
-  else if (r <= 16) hipLaunchKernelGGL((probe_chunks<KIND, 16>), grid, block, 0, s, p);
-  else if (r <= 32) hipLaunchKernelGGL((probe_chunks<KIND, 32>), grid, block, 0, s, p);
-  else return hipErrorInvalidValue;
+  const uint32_t nj = (p.chunk + kWave - 1) / kWave;
+  const size_t lds = nj * kWave * sizeof(int64_t) + kMaxFastRounds * kWave * sizeof(uint32_t);
+  hipLaunchKernelGGL((probe_chunks<KIND, 4>), dim3((unsigned)p.n_chunks), dim3(kWave), lds, s, p);
   return hipGetLastError();
 }
 

@@ -1,0 +1,22 @@
+#!/bin/bash
+# tools/profile.sh TAG [bench args...] — run ON THE GPU BOX (via gpurun).
+# 1) kernel trace + stats of the bench command; 2) PMC passes, one counter group per run (FETCH_SIZE
+# and WRITE_SIZE cannot share a pass on gfx950: MI355X_MICROARCH.md §rocprofv3 PMC slots).
+# Outputs under gpurun_out/prof_TAG/; tools/prof_summary.py turns them into profiles/ files.
+set -o pipefail
+TAG=$1; shift
+ARGS="$@"
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT" || exit 1
+OUT=gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+echo "[profile] kernel trace: bench.py $ARGS"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -f csv -d "$OUT/kt" -o kt -- python3 bench.py $ARGS > "$OUT/kt_bench.log" 2>&1 || exit $?
+for grp in FETCH_SIZE WRITE_SIZE "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" "TCC_HIT_sum TCC_MISS_sum" \
+           "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES" "GRBM_GUI_ACTIVE"; do
+  name=$(echo "$grp" | tr ' ' '+')
+  echo "[profile] pmc $grp"
+  timeout -k 10 600 rocprofv3 --pmc $grp --kernel-include-regex "${PMC_KERNEL:-probe_chunks}" -T -f csv -d "$OUT/pmc_$name" -o pmc \
+      -- python3 bench.py $ARGS --steps 2 --warmup 1 > "$OUT/pmc_$name.log" 2>&1 || { echo "pmc $grp failed rc=$?"; tail -5 "$OUT/pmc_$name.log"; }
+done
+echo "[profile] done"
