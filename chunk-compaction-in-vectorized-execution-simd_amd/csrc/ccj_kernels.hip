@@ -11,6 +11,8 @@
 // Emission order is round-major, idx ascending within a round: exactly the reference's
 // result_vector order (L3).  Per-row state lives in VGPRs (key, slot/chain position, chain end);
 // active/match sets are bitmasks over the lane's R rows.
+#include <cstdlib>
+
 #include "ccj_internal.h"
 
 namespace ccj {
@@ -20,13 +22,15 @@ __device__ __forceinline__ uint32_t lane_prefix(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// Emits one match: ordered by (round, j, lane) through the wave ballot `mb`.
-__device__ __forceinline__ void emit_match(const ProbeParams &p, uint64_t base, uint64_t obase, uint64_t total,
-                                           uint64_t mb, uint32_t i, int64_t payload) {
+// Emits one match: ordered by (round, j, lane) through the wave ballot `mb`.  The payload is the
+// matched table value, which equals the probe key: it is re-read from the key column (the chunk's
+// 16 KB were read moments earlier by the walk) instead of being held through the walk.
+__device__ __forceinline__ void emit_match(const ProbeParams &p, uint64_t obase, uint64_t total, uint64_t mb,
+                                           uint32_t r, uint64_t base) {
   const uint64_t o = total + lane_prefix(mb);
   if (o < p.cap) {
-    p.out_sel[obase + o] = p.sel ? p.sel[base + i] : i;
-    if (p.out_payload) p.out_payload[obase + o] = payload;  // matched table value == probe key
+    p.out_sel[obase + o] = r;
+    if (p.out_payload) p.out_payload[obase + o] = p.keys[base + r];
   }
 }
 
@@ -59,9 +63,13 @@ __device__ __forceinline__ void record_round(const ProbeParams &p, uint64_t c, u
 // Generic round-synchronous Next loop for chunks containing a run/chain longer than the
 // kMaxFastRounds rounds the windowed path records: round r reads candidate r of every active row
 // (position recomputed from the key, no per-row position state).  Rare; correctness path.
+__device__ __forceinline__ uint32_t phys_row(const ProbeParams &p, uint64_t base, uint32_t i) {
+  return p.sel ? p.sel[base + i] : i;
+}
+
 template <int KIND>
-__device__ void rounds_generic(const ProbeParams &p, uint64_t c, uint64_t base, const int64_t *s_key, uint32_t nj,
-                               uint32_t act, uint32_t &flags, uint64_t &total_out, uint32_t &rounds_out) {
+__device__ void rounds_generic(const ProbeParams &p, uint64_t c, uint64_t base, uint32_t nj, uint32_t act,
+                               uint32_t &flags, uint64_t &total_out, uint32_t &rounds_out) {
   const uint32_t lane = threadIdx.x;
   const uint64_t obase = c * p.cap;
   uint64_t total = 0;
@@ -70,7 +78,7 @@ __device__ void rounds_generic(const ProbeParams &p, uint64_t c, uint64_t base, 
     uint32_t mat = 0;
     for (uint32_t j = 0; j < nj; ++j) {
       if ((act >> j) & 1u) {
-        const int64_t k = s_key[j * kWave + lane];
+        const int64_t k = p.keys[base + phys_row(p, base, j * kWave + lane)];
         const uint32_t h = (uint32_t)murmurhash64((uint64_t)k) & p.mask;
         if (KIND == CCJ_TABLE_LP) {
           const int64_t v = p.table[(h + round) & p.mask];
@@ -89,7 +97,7 @@ __device__ void rounds_generic(const ProbeParams &p, uint64_t c, uint64_t base, 
       const uint32_t j = (uint32_t)__builtin_ctz(any);
       const bool m = (mat >> j) & 1u;
       const uint64_t mb = __ballot(m);
-      if (m) emit_match(p, base, obase, total, mb, j * kWave + lane, s_key[j * kWave + lane]);
+      if (m) emit_match(p, obase, total, mb, phys_row(p, base, j * kWave + lane), base);
       const uint32_t n = (uint32_t)__popcll(mb);
       total += n;
       rc += n;
@@ -103,29 +111,37 @@ __device__ void rounds_generic(const ProbeParams &p, uint64_t c, uint64_t base, 
 
 constexpr int kWin = 4;             // slots (LP) / chain keys per window load: 32 B, one aligned sector
 constexpr int kMaxFastRounds = 32;  // rounds recorded by the windowed path (bits of a u32)
+#ifndef CCJ_WALK_ROWS
+#define CCJ_WALK_ROWS 4
+#endif
+constexpr int kWalkRows = CCJ_WALK_ROWS;  // rows per lane walked concurrently (loads in flight)
+
+constexpr int kEmitRows = 8;  // rows per lane whose key/sel loads are issued together in the emit
 
 // One wave per 64-thread workgroup = one chunk of up to 64*nj rows (row (j, lane) = j*64 + lane).
-// LDS (dynamic): s_key[nj*64] int64 probe keys, s_rm[kMaxFastRounds*64] u32 where bit j of
-// s_rm[r*64 + lane] says row (j, lane) matches in round r.
+// LDS (12 KB per wave): s_mm[nj*64] u32 — bit r set iff row (j, lane) matches in round r (Next
+// call r); s_off[kMaxFastRounds*32] u32 — matches of (round r, row group j), then its exclusive
+// prefix in round-major order: the output slot where that (r, j) group's ballot-pack starts.
 //
 // Walk: every row's whole run (LP: home slot up to the first empty slot; chain: the bucket's CSR
-// range) is read once through aligned 32-byte windows, G rows per lane in flight; a window is one
+// range) is read once through aligned 32-byte windows, G rows per lane in flight.  A window is one
 // sector of a 64-byte line, so a continuation re-reads a line fetched moments earlier (L2-resident)
-// rather than one fetched a whole round of 2048 rows earlier (the reference's round-by-round
-// re-read, linear_probing_ht.cpp:72-80 / :100-110, loses L2 residency at GPU occupancy).
-// Emit: for each round r (Next call r), the rows matching in r are packed idx-ascending with a
-// wave ballot + mbcnt prefix: the reference's result_vector order (L3).
+// rather than one fetched a whole round of 2048 rows earlier — the reference's round-by-round
+// re-read (linear_probing_ht.cpp:72-80 then :100-110) loses L2 residency at GPU occupancy.
+// Count + scan: per (round, row group) match counts by ballot, exclusive scan across the wave.
+// Emit: row-group-major, but every match goes to offset s_off[r][j] + its ballot prefix, i.e.
+// exactly where the reference's round-major, idx-ascending result_vector order puts it (L3);
+// the payload/sel loads of kEmitRows row groups are then in flight together.
 template <int KIND, int G>
 __global__ __launch_bounds__(kWave) void probe_chunks(ProbeParams p) {
-  extern __shared__ __attribute__((aligned(16))) int64_t s_mem[];
+  __shared__ uint32_t s_mm[kMaxChunk];
+  __shared__ uint32_t s_off[kMaxFastRounds * 32];
   const uint32_t lane = threadIdx.x;
   const uint64_t c = blockIdx.x;
   const uint64_t base = c * p.chunk;
   const uint64_t rem = p.n_rows - base;
   const uint32_t phys = rem < p.chunk ? (uint32_t)rem : p.chunk;
   const uint32_t nj = (p.chunk + kWave - 1) / kWave;
-  int64_t *s_key = s_mem;
-  uint32_t *s_rm = reinterpret_cast<uint32_t *>(s_mem + nj * kWave);
   uint32_t count = p.counts ? p.counts[c] : phys;
   uint32_t flags = 0;
   if (count > p.chunk) {
@@ -133,95 +149,129 @@ __global__ __launch_bounds__(kWave) void probe_chunks(ProbeParams p) {
     count = p.chunk;
   }
 
-  // Probe (linear_probing_ht.cpp:45-49 / chaining_ht.cpp:46-50): keys through sel -> LDS.
+  // Active rows: idx < count whose sel entry addresses a physical row of the chunk.
   uint32_t act = 0;
   for (uint32_t j = 0; j < nj; ++j) {
     const uint32_t i = j * kWave + lane;
-    int64_t k = 0;
     if (i < count) {
-      const uint32_t r = p.sel ? p.sel[base + i] : i;
-      if (r < phys) {
-        k = p.keys[base + r];
-        act |= 1u << j;
-      } else {
-        flags |= CCJ_FLAG_BAD_INPUT;
-      }
+      if (phys_row(p, base, i) < phys) act |= 1u << j;
+      else flags |= CCJ_FLAG_BAD_INPUT;
     }
-    s_key[i] = k;
   }
 #pragma unroll
-  for (int r = 0; r < kMaxFastRounds; ++r) s_rm[r * kWave + lane] = 0u;
+  for (int q = 0; q < kMaxFastRounds * 32 / kWave; ++q) s_off[q * kWave + lane] = 0u;
+  for (uint32_t q = 0; q < nj; ++q) s_mm[q * kWave + lane] = 0u;
 
-  // Walk.
+  // Walk.  G independent cursors per lane; cursor g owns rows j = g, g+G, ... of this lane and moves
+  // to its next active row as soon as the current run ends, so every iteration keeps ~G window loads
+  // per lane in flight instead of waiting for the slowest lane of a row group.  The next row's key
+  // is prefetched while the current row is walked.
   uint32_t lane_rounds = 0;
   bool long_run = false;
-  for (uint32_t jb = 0; jb < nj; jb += G) {
-    uint32_t cur[G], r0[G], lim[G];
-    int64_t kj[G];
-    uint32_t need = 0;
+  {
+    uint32_t j[G], nj_next[G], cur[G], r0[G], lim[G], mm[G];
+    int64_t kj[G], nk[G];
+    uint32_t live = 0, start = 0, nk_ok = 0;  // bit g: cursor has a row / row needs its CSR range / nk loaded
+    auto next_active = [&](uint32_t from, int g) -> uint32_t {  // first active row >= from, == g mod G
+      for (uint32_t t = from; t < nj; t += G)
+        if ((act >> t) & 1u) return t;
+      return nj;
+    };
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const uint32_t j = jb + g;
-      cur[g] = 0;
-      r0[g] = 0;
-      lim[g] = 0;
-      kj[g] = 0;
-      if (j < nj && ((act >> j) & 1u)) {
-        kj[g] = s_key[j * kWave + lane];
+      j[g] = next_active(g, g);
+      nj_next[g] = j[g] < nj ? next_active(j[g] + G, g) : nj;
+      cur[g] = r0[g] = lim[g] = mm[g] = 0;
+      kj[g] = nk[g] = 0;
+      if (j[g] < nj) kj[g] = p.keys[base + phys_row(p, base, j[g] * kWave + lane)];
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (j[g] < nj) {
+        live |= 1u << g;
         const uint32_t h = (uint32_t)murmurhash64((uint64_t)kj[g]) & p.mask;
-        if (KIND == CCJ_TABLE_LP) {
-          cur[g] = h;
-          need |= 1u << g;
-        } else {
-          cur[g] = p.off[h];
-          lim[g] = p.off[h + 1];
-          if (cur[g] != lim[g]) need |= 1u << g;
+        if (KIND == CCJ_TABLE_LP) cur[g] = h;
+        else {
+          cur[g] = h;  // bucket index until the CSR range is loaded
+          start |= 1u << g;
         }
       }
     }
-    while (__ballot(need != 0u) != 0ull) {
+    while (__ballot(live != 0u) != 0ull) {
       longlong2 v[G][kWin / 2];
+      uint32_t o0[G], o1[G];
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        if ((need >> g) & 1u) {
-          const longlong2 *w = reinterpret_cast<const longlong2 *>(p.table + (cur[g] & ~(uint32_t)(kWin - 1)));
+        if ((live >> g) & 1u) {
+          if (KIND == CCJ_TABLE_CHAIN && ((start >> g) & 1u)) {
+            o0[g] = p.off[cur[g]];  // chaining_ht.cpp:46-49: bucket -> chain (CSR range)
+            o1[g] = p.off[cur[g] + 1];
+          } else {
+            const longlong2 *w = reinterpret_cast<const longlong2 *>(p.table + (cur[g] & ~(uint32_t)(kWin - 1)));
 #pragma unroll
-          for (int q = 0; q < kWin / 2; ++q) v[g][q] = w[q];
+            for (int q = 0; q < kWin / 2; ++q) v[g][q] = w[q];
+          }
+          if (!((nk_ok >> g) & 1u) && nj_next[g] < nj) {
+            nk[g] = p.keys[base + phys_row(p, base, nj_next[g] * kWave + lane)];
+            nk_ok |= 1u << g;
+          }
         }
       }
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        if ((need >> g) & 1u) {
-          const uint32_t j = jb + g;
-          const uint32_t blk = cur[g] & ~(uint32_t)(kWin - 1);
-          const uint32_t off = cur[g] - blk;
-          bool go = true;
+        if ((live >> g) & 1u) {
+          bool done = false;
+          if (KIND == CCJ_TABLE_CHAIN && ((start >> g) & 1u)) {
+            start &= ~(1u << g);
+            cur[g] = o0[g];
+            lim[g] = o1[g];
+            done = cur[g] == lim[g];  // empty bucket: not in the active set (chaining_ht.cpp:52-55)
+          } else {
+            const uint32_t blk = cur[g] & ~(uint32_t)(kWin - 1);
+            const uint32_t off = cur[g] - blk;
+            bool go = true;
 #pragma unroll
-          for (int q = 0; q < kWin; ++q) {
-            const int64_t val = (q & 1) ? v[g][q >> 1].y : v[g][q >> 1].x;
-            if (go && (uint32_t)q >= off) {
-              const uint32_t r = r0[g] + (uint32_t)q - off;
-              const bool stop = KIND == CCJ_TABLE_LP ? (val == -1) : (blk + (uint32_t)q == lim[g]);
-              if (stop) {
-                go = false;
-                lane_rounds = r > lane_rounds ? r : lane_rounds;
-              } else if (r >= (uint32_t)kMaxFastRounds) {
-                go = false;
-                long_run = true;
-              } else if (val == kj[g]) {
-                atomicOr(&s_rm[r * kWave + lane], 1u << j);  // ds_or_b32, this lane's own word
+            for (int q = 0; q < kWin; ++q) {
+              const int64_t val = (q & 1) ? v[g][q >> 1].y : v[g][q >> 1].x;
+              if (go && (uint32_t)q >= off) {
+                const uint32_t r = r0[g] + (uint32_t)q - off;
+                const bool stop = KIND == CCJ_TABLE_LP ? (val == -1) : (blk + (uint32_t)q == lim[g]);
+                if (stop) {
+                  go = false;
+                  lane_rounds = r > lane_rounds ? r : lane_rounds;
+                } else if (r >= (uint32_t)kMaxFastRounds) {
+                  go = false;
+                  long_run = true;
+                } else if (val == kj[g]) {
+                  mm[g] |= 1u << r;
+                }
               }
             }
-          }
-          if (go) {
-            r0[g] += (uint32_t)kWin - off;
-            cur[g] = KIND == CCJ_TABLE_LP ? ((blk + kWin) & p.mask) : blk + kWin;
-            if (KIND == CCJ_TABLE_CHAIN && cur[g] == lim[g]) {
-              lane_rounds = r0[g] > lane_rounds ? r0[g] : lane_rounds;
-              need &= ~(1u << g);
+            if (go) {
+              r0[g] += (uint32_t)kWin - off;
+              cur[g] = KIND == CCJ_TABLE_LP ? ((blk + kWin) & p.mask) : blk + kWin;
+              if (KIND == CCJ_TABLE_CHAIN && cur[g] == lim[g]) {
+                lane_rounds = r0[g] > lane_rounds ? r0[g] : lane_rounds;
+                go = false;
+              }
             }
-          } else {
-            need &= ~(1u << g);
+            done = !go;
+          }
+          if (done) {
+            s_mm[j[g] * kWave + lane] = mm[g];
+            j[g] = nj_next[g];
+            if (j[g] < nj) {
+              nj_next[g] = next_active(j[g] + G, g);
+              kj[g] = nk[g];
+              nk_ok &= ~(1u << g);
+              mm[g] = 0;
+              r0[g] = 0;
+              const uint32_t h = (uint32_t)murmurhash64((uint64_t)kj[g]) & p.mask;
+              cur[g] = h;
+              if (KIND == CCJ_TABLE_CHAIN) start |= 1u << g;
+            } else {
+              live &= ~(1u << g);
+            }
           }
         }
       }
@@ -231,24 +281,80 @@ __global__ __launch_bounds__(kWave) void probe_chunks(ProbeParams p) {
   uint64_t total = 0;
   uint32_t rounds = 0;
   if (__ballot(long_run) != 0ull) {
-    rounds_generic<KIND>(p, c, base, s_key, nj, act, flags, total, rounds);
+    rounds_generic<KIND>(p, c, base, nj, act, flags, total, rounds);
   } else {
-    // Emit: Next loop (linear_probing_ht.cpp:62-115 / chaining_ht.cpp:60-136).
     rounds = wave_max(lane_rounds);
-    const uint64_t obase = c * p.cap;
-    for (uint32_t r = 0; r < rounds; ++r) {
-      const uint32_t bits = s_rm[r * kWave + lane];
-      uint32_t rc = 0;
-      for (uint32_t any = wave_or(bits); any != 0u; any &= any - 1u) {
-        const uint32_t j = (uint32_t)__builtin_ctz(any);
-        const bool m = (bits >> j) & 1u;
-        const uint64_t mb = __ballot(m);
-        if (m) emit_match(p, base, obase, total, mb, j * kWave + lane, s_key[j * kWave + lane]);
-        const uint32_t n = (uint32_t)__popcll(mb);
-        total += n;
-        rc += n;
+    // Count: matches per (round r, row group j).
+    for (uint32_t j = 0; j < nj; ++j) {
+      const uint32_t m = s_mm[j * kWave + lane];
+      for (uint32_t any = wave_or(m); any != 0u; any &= any - 1u) {
+        const uint32_t r = (uint32_t)__builtin_ctz(any);
+        const uint32_t n = (uint32_t)__popcll(__ballot((m >> r) & 1u));
+        if (lane == 0) s_off[r * 32 + j] = n;
       }
-      record_round(p, c, r, rc, lane, flags);
+    }
+    // Scan: exclusive prefix over (r, j) in round-major order, 16 entries per lane.
+    {
+      uint32_t loc[16], sum = 0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        loc[q] = s_off[lane * 16 + q];
+        sum += loc[q];
+      }
+      uint32_t incl = sum;
+#pragma unroll
+      for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
+        if (lane >= (uint32_t)d) incl += o;
+      }
+      uint32_t run = incl - sum;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        s_off[lane * 16 + q] = run;
+        run += loc[q];
+      }
+      total = (uint64_t)(uint32_t)__shfl((int)incl, kWave - 1);
+    }
+    // Per-round counts (Next return values): differences of the round starts.
+    if (p.out_round_counts) {
+      for (uint32_t r = lane; r < rounds; r += kWave) {
+        const uint32_t a = s_off[r * 32], b = r + 1 < rounds ? s_off[(r + 1) * 32] : (uint32_t)total;
+        if (r < p.max_rounds) p.out_round_counts[c * p.max_rounds + r] = b - a;
+      }
+      if (rounds > p.max_rounds) flags |= CCJ_FLAG_ROUND_OVERFLOW;
+    }
+    // Emit.
+    const uint64_t obase = c * p.cap;
+    for (uint32_t jb = 0; jb < nj; jb += kEmitRows) {
+      uint32_t m[kEmitRows], rr[kEmitRows];
+      int64_t pay[kEmitRows];
+#pragma unroll
+      for (int g = 0; g < kEmitRows; ++g) {
+        const uint32_t j = jb + g;
+        m[g] = j < nj ? s_mm[j * kWave + lane] : 0u;
+        rr[g] = 0;
+        pay[g] = 0;
+        if (m[g]) {
+          rr[g] = phys_row(p, base, j * kWave + lane);
+          if (p.out_payload) pay[g] = p.keys[base + rr[g]];  // matched table value == probe key
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < kEmitRows; ++g) {
+        const uint32_t j = jb + g;
+        for (uint32_t any = wave_or(m[g]); any != 0u; any &= any - 1u) {
+          const uint32_t r = (uint32_t)__builtin_ctz(any);
+          const bool bit = (m[g] >> r) & 1u;
+          const uint64_t mb = __ballot(bit);
+          if (bit) {
+            const uint64_t o = (uint64_t)s_off[r * 32 + j] + lane_prefix(mb);
+            if (o < p.cap) {
+              p.out_sel[obase + o] = rr[g];
+              if (p.out_payload) p.out_payload[obase + o] = pay[g];
+            }
+          }
+        }
+      }
     }
   }
 
@@ -265,9 +371,16 @@ __global__ __launch_bounds__(kWave) void probe_chunks(ProbeParams p) {
 
 template <int KIND>
 hipError_t launch_kind(const ProbeParams &p, hipStream_t s) {
-  const uint32_t nj = (p.chunk + kWave - 1) / kWave;
-  const size_t lds = nj * kWave * sizeof(int64_t) + kMaxFastRounds * kWave * sizeof(uint32_t);
-  hipLaunchKernelGGL((probe_chunks<KIND, 4>), dim3((unsigned)p.n_chunks), dim3(kWave), lds, s, p);
+  // CCJ_WALK_ROWS (tuning override): rows per lane walked concurrently.
+  static const int walk = [] {
+    const char *e = getenv("CCJ_WALK_ROWS");
+    return e ? atoi(e) : kWalkRows;
+  }();
+  const dim3 g((unsigned)p.n_chunks), b(kWave);
+  if (walk <= 2) hipLaunchKernelGGL((probe_chunks<KIND, 2>), g, b, 0, s, p);
+  else if (walk <= 4) hipLaunchKernelGGL((probe_chunks<KIND, 4>), g, b, 0, s, p);
+  else if (walk <= 6) hipLaunchKernelGGL((probe_chunks<KIND, 6>), g, b, 0, s, p);
+  else hipLaunchKernelGGL((probe_chunks<KIND, 8>), g, b, 0, s, p);
   return hipGetLastError();
 }
 
