@@ -43,9 +43,20 @@ class ProbeArgs(C.Structure):
                 ("out_rounds", C.c_void_p), ("out_round_counts", C.c_void_p), ("status", C.c_void_p)]
 
 
+class CompactArgs(C.Structure):
+    _fields_ = [("count", C.c_void_p), ("sel", C.c_void_p), ("payload", C.c_void_p), ("rounds", C.c_void_p),
+                ("round_counts", C.c_void_p), ("n_chunks", C.c_uint64), ("cap", C.c_uint64),
+                ("max_rounds", C.c_uint32), ("chunk", C.c_uint32), ("n_cols", C.c_uint32), ("reserved", C.c_uint32),
+                ("cols", C.c_void_p * 16), ("out_cols", C.c_void_p * 16), ("out_payload", C.c_void_p),
+                ("out_row", C.c_void_p), ("out_chunk_counts", C.c_void_p), ("out_cap_rows", C.c_uint64),
+                ("out_n_chunks", C.c_void_p), ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t),
+                ("status", C.c_void_p)]
+
+
 EXPORTS = ["ccj_last_error", "ccj_abi_version", "ccj_device_init", "ccj_table_build_reference",
            "ccj_table_build_from_host", "ccj_table_build_on_device", "ccj_table_get_info", "ccj_table_free",
-           "ccj_probe", "ccj_gen_uniform_keys", "ccj_probe_cost", "ccj_result_checksum"]
+           "ccj_probe", "ccj_gen_uniform_keys", "ccj_probe_cost", "ccj_result_checksum",
+           "ccj_compact_workspace_size", "ccj_compact"]
 
 
 def build(force: bool = False) -> str:
@@ -73,6 +84,9 @@ def lib():
         L.ccj_probe.argtypes = [vp, C.POINTER(ProbeArgs), vp]
         L.ccj_gen_uniform_keys.argtypes = [vp, u64, u64, u64, u64, vp]
         L.ccj_probe_cost.argtypes = [vp, vp, u64, vp, vp]
+        L.ccj_compact_workspace_size.restype = C.c_size_t
+        L.ccj_compact_workspace_size.argtypes = [u64, u64, C.c_uint32]
+        L.ccj_compact.argtypes = [C.POINTER(CompactArgs), vp]
         L.ccj_result_checksum.argtypes = [vp, vp, vp, u64, u64, C.c_uint32, u64, vp, vp]
         _lib = L
     return _lib
@@ -202,3 +216,47 @@ class Table:
                       status=_ptr(out["status"]).value)
         check(lib().ccj_probe(self._h, C.byref(a), _stream(stream)), "ccj_probe")
         return out
+
+
+def compact(probe_out, chunk: int, cols=(), payload: bool = True, rows: bool = True, stream=None):
+    """Device compaction of a probe output's Next results (include/ccj.h ccj_compact).
+
+    Returns dict(n_chunks (int), counts, cols [list], payload, row, status) — dense output chunks of
+    `chunk` rows in the (fixed) NaiveCompactor order.
+    """
+    import torch
+    dev = probe_out["count"].device
+    n_chunks, cap = probe_out["n_chunks"], probe_out["cap"]
+    if probe_out.get("round_counts") is None:
+        raise CCJError("compact needs the probe's per-round counts (alloc_outputs(rounds=True))")
+    out_rows = ((n_chunks * cap + chunk - 1) // chunk + 1) * chunk
+    ws_bytes = lib().ccj_compact_workspace_size(n_chunks, cap, chunk)
+    ws = torch.empty(max(ws_bytes, 8), dtype=torch.uint8, device=dev)
+    o = dict(
+        counts=torch.zeros(out_rows // chunk, dtype=torch.int32, device=dev),
+        cols=[torch.empty(out_rows, dtype=torch.int64, device=dev) for _ in cols],
+        payload=torch.empty(out_rows, dtype=torch.int64, device=dev) if payload else None,
+        row=torch.empty(out_rows, dtype=torch.int64, device=dev) if rows else None,
+        n=torch.zeros(1, dtype=torch.int64, device=dev),
+        status=torch.zeros(1, dtype=torch.int32, device=dev),
+        chunk=chunk,
+    )
+    a = CompactArgs()
+    a.count, a.sel = _ptr(probe_out["count"]).value, _ptr(probe_out["sel"]).value
+    a.payload = _ptr(probe_out["payload"]).value if probe_out.get("payload") is not None else None
+    a.rounds, a.round_counts = _ptr(probe_out["rounds"]).value, _ptr(probe_out["round_counts"]).value
+    a.n_chunks, a.cap, a.max_rounds, a.chunk = n_chunks, cap, probe_out["max_rounds"], chunk
+    a.n_cols = len(cols)
+    for i, col in enumerate(cols):
+        a.cols[i] = col.data_ptr()
+        a.out_cols[i] = o["cols"][i].data_ptr()
+    a.out_payload = o["payload"].data_ptr() if payload else None
+    a.out_row = o["row"].data_ptr() if rows else None
+    a.out_chunk_counts = o["counts"].data_ptr()
+    a.out_cap_rows = out_rows
+    a.out_n_chunks = o["n"].data_ptr()
+    a.workspace, a.workspace_bytes = ws.data_ptr(), ws_bytes
+    a.status = o["status"].data_ptr()
+    o["_ws"] = ws
+    check(lib().ccj_compact(C.byref(a), _stream(stream)), "ccj_compact")
+    return o

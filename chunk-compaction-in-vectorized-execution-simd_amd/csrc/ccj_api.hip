@@ -346,6 +346,31 @@ int ccj_probe(const ccj_table *t, const ccj_probe_args *a, ccj_stream stream) {
   return CCJ_OK;
 }
 
+size_t ccj_compact_workspace_size(uint64_t n_chunks, uint64_t cap, uint32_t chunk) {
+  if (chunk == 0) return 0;
+  return ccj::compact_workspace(n_chunks, cap, chunk);
+}
+
+int ccj_compact(const ccj_compact_args *a, ccj_stream stream) {
+  if (!a) return fail(CCJ_ERR_INVALID, "ccj_compact: null args");
+  if (a->chunk == 0 || a->chunk > ccj::kMaxChunk) return fail(CCJ_ERR_INVALID, "ccj_compact: chunk must be 1..2048");
+  if (a->n_cols > CCJ_MAX_COLS) return fail(CCJ_ERR_INVALID, "ccj_compact: too many columns");
+  if (a->out_cap_rows % a->chunk) return fail(CCJ_ERR_INVALID, "ccj_compact: out_cap_rows must be a multiple of chunk");
+  if (a->n_chunks == 0) {
+    if (a->out_n_chunks) HIP_TRY(hipMemsetAsync(a->out_n_chunks, 0, 8, (hipStream_t)stream), "memset");
+    return CCJ_OK;
+  }
+  if (!a->count || !a->sel || !a->rounds || !a->round_counts || !a->out_chunk_counts || !a->workspace)
+    return fail(CCJ_ERR_INVALID, "ccj_compact: missing buffer (round counts are required)");
+  if (a->out_payload && !a->payload) return fail(CCJ_ERR_INVALID, "ccj_compact: out_payload needs payload");
+  for (uint32_t q = 0; q < a->n_cols; ++q)
+    if (!a->cols[q] || !a->out_cols[q]) return fail(CCJ_ERR_INVALID, "ccj_compact: null column");
+  if (a->workspace_bytes < ccj::compact_workspace(a->n_chunks, a->cap, a->chunk))
+    return fail(CCJ_ERR_INVALID, "ccj_compact: workspace too small");
+  HIP_TRY(ccj::launch_compact(*a, (hipStream_t)stream), "compact launch");
+  return CCJ_OK;
+}
+
 int ccj_gen_uniform_keys(int64_t *d_out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t range,
                          ccj_stream stream) {
   if ((!d_out && n) || range == 0) return fail(CCJ_ERR_INVALID, "ccj_gen_uniform_keys: bad argument");

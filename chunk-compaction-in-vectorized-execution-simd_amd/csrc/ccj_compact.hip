@@ -1,0 +1,185 @@
+// ccj_compact.hip — device chunk compaction (NaiveCompactor::Compact/Flush, compactor.cpp:5-41,
+// with the fresh-temp-chunk fix of :36) over the Next results of a ccj_probe output.
+//
+// The reference compacts sequentially: a cache of up to `chunk` rows absorbs each Next result;
+// a full result bypasses the cache (:6); an overflowing result tops the cache up, the cache is
+// emitted, and the rest becomes the new cache (:22-35).  That order is a closed form of two
+// prefix sums, so it runs in parallel:
+//   P-stream  = rows of the non-full results, concatenated in pipeline order (t = position in it)
+//   F_s       = full results before result s;  E(t) = t == 0 ? 0 : ceil(t / chunk) - 1
+//   full result s           -> output chunk E(t_s) + F_s
+//   P-row u (chunk k = u/B)  -> output chunk k + #{full s : E(t_s) <= k}, row u % B
+// Kernels: per-chunk segment sums -> exclusive scans (hipCUB) -> full-result E list -> one wave
+// per probe chunk copies its rows (DataChunk::Append's gather, base.cpp:15-27) -> chunk counts.
+#include <hipcub/hipcub.hpp>
+
+#include "ccj_internal.h"
+
+namespace ccj {
+namespace {
+
+struct CompactParams {
+  ccj_compact_args a;
+  uint64_t *nonfull;  // [n_chunks] -> exclusive scan in place (t at chunk start)
+  uint64_t *full;     // [n_chunks] -> exclusive scan in place (F at chunk start)
+  uint64_t *totals;   // [2]: T_total, F_total
+  uint32_t *fullE;    // [max full results]
+  uint64_t max_full;
+};
+
+__global__ void seg_sums(CompactParams p) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= p.a.n_chunks) return;
+  const uint32_t rounds = p.a.rounds[c];
+  uint64_t nf = 0, f = 0;
+  for (uint32_t r = 0; r < rounds && r < p.a.max_rounds; ++r) {
+    const uint32_t rc = p.a.round_counts[c * p.a.max_rounds + r];
+    if (rc == p.a.chunk) ++f;
+    else nf += rc;
+  }
+  p.nonfull[c] = nf;
+  p.full[c] = f;
+}
+
+__global__ void seg_totals(CompactParams p, const uint64_t *nf_last, const uint64_t *f_last) {
+  // called after the exclusive scans: totals = scan[last] + value[last]
+  p.totals[0] = p.nonfull[p.a.n_chunks - 1] + nf_last[0];
+  p.totals[1] = p.full[p.a.n_chunks - 1] + f_last[0];
+  const uint64_t T = p.totals[0], F = p.totals[1], B = p.a.chunk;
+  const uint64_t n_out = F + (T + B - 1) / B;
+  if (p.a.out_n_chunks) *p.a.out_n_chunks = n_out;
+  if (n_out * B > p.a.out_cap_rows && p.a.status) atomicOr(p.a.status, CCJ_FLAG_CAP_OVERFLOW);
+  if (F > p.max_full && p.a.status) atomicOr(p.a.status, CCJ_FLAG_CAP_OVERFLOW);
+}
+
+__device__ __forceinline__ uint64_t e_of(uint64_t t, uint64_t B) { return t == 0 ? 0 : (t + B - 1) / B - 1; }
+
+__global__ void full_list(CompactParams p) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= p.a.n_chunks) return;
+  const uint32_t rounds = p.a.rounds[c];
+  uint64_t t = p.nonfull[c], f = p.full[c];
+  for (uint32_t r = 0; r < rounds && r < p.a.max_rounds; ++r) {
+    const uint32_t rc = p.a.round_counts[c * p.a.max_rounds + r];
+    if (rc == p.a.chunk) {
+      if (f < p.max_full) p.fullE[f] = (uint32_t)e_of(t, p.a.chunk);
+      ++f;
+    } else {
+      t += rc;
+    }
+  }
+}
+
+// #{full results s : E(t_s) <= k}: fullE is non-decreasing.
+__device__ __forceinline__ uint64_t full_before(const CompactParams &p, uint64_t F, uint64_t k) {
+  uint64_t lo = 0, hi = F;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (p.fullE[mid] <= k) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void copy_rows(CompactParams p) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t c = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= p.a.n_chunks) return;
+  const uint64_t B = p.a.chunk;
+  const uint64_t F = p.totals[1] < p.max_full ? p.totals[1] : p.max_full;
+  const uint64_t cap_rows = p.a.out_cap_rows;
+  uint64_t t = p.nonfull[c], f = p.full[c];
+  uint64_t src = c * p.a.cap;  // rows of this chunk's result, round-major
+  const uint32_t rounds = p.a.rounds[c];
+  const uint32_t total = p.a.count[c];
+  for (uint32_t r = 0; r < rounds && r < p.a.max_rounds; ++r) {
+    const uint32_t rc = p.a.round_counts[c * p.a.max_rounds + r];
+    const bool is_full = rc == B;
+    const uint64_t fbase = (e_of(t, B) + f) * B;
+    for (uint32_t j = lane; j < rc; j += 64) {
+      if (src + j >= c * p.a.cap + total) break;  // probe capped this chunk (flagged there)
+      uint64_t dest;
+      if (is_full) {
+        dest = fbase + j;
+      } else {
+        const uint64_t u = t + j;
+        const uint64_t k = u / B;
+        dest = (k + (F ? full_before(p, F, k) : 0)) * B + (u - k * B);
+      }
+      if (dest >= cap_rows) continue;
+      const uint32_t s = p.a.sel[src + j];
+      const uint64_t row = c * B + s;
+#pragma unroll 4
+      for (uint32_t q = 0; q < p.a.n_cols; ++q) p.a.out_cols[q][dest] = p.a.cols[q][row];
+      if (p.a.out_payload) p.a.out_payload[dest] = p.a.payload[src + j];
+      if (p.a.out_row) p.a.out_row[dest] = row;
+    }
+    src += rc;
+    if (is_full) ++f;
+    else t += rc;
+  }
+}
+
+__global__ void chunk_counts(CompactParams p) {
+  const uint64_t T = p.totals[0], F = p.totals[1], B = p.a.chunk;
+  const uint64_t n_out = F + (T + B - 1) / B;
+  const uint64_t lim = p.a.out_cap_rows / B;
+  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n_out && q < lim;
+       q += (uint64_t)gridDim.x * blockDim.x) {
+    // every output chunk is full except the last P-chunk, which is the last output chunk
+    uint32_t n = (uint32_t)B;
+    if (q == n_out - 1 && T > 0) n = (uint32_t)(T - ((T + B - 1) / B - 1) * B);
+    p.a.out_chunk_counts[q] = n;
+  }
+}
+
+size_t scan_temp_bytes(uint64_t n) {
+  size_t bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (uint64_t *)nullptr, (uint64_t *)nullptr, (int)n);
+  return (bytes + 255) & ~(size_t)255;
+}
+
+}  // namespace
+
+size_t compact_workspace(uint64_t n_chunks, uint64_t cap, uint32_t chunk) {
+  const uint64_t max_full = n_chunks * (cap / chunk + 1);
+  return 256 + 4 * ((n_chunks * 8 + 255) & ~255ull) + ((max_full * 4 + 255) & ~255ull) + scan_temp_bytes(n_chunks);
+}
+
+hipError_t launch_compact(const ccj_compact_args &a, hipStream_t s) {
+  CompactParams p{};
+  p.a = a;
+  char *w = (char *)a.workspace;
+  auto take = [&](size_t bytes) {
+    char *r = w;
+    w += (bytes + 255) & ~(size_t)255;
+    return r;
+  };
+  p.totals = (uint64_t *)take(256);
+  p.nonfull = (uint64_t *)take(a.n_chunks * 8);
+  p.full = (uint64_t *)take(a.n_chunks * 8);
+  uint64_t *nf_raw = (uint64_t *)take(a.n_chunks * 8);
+  uint64_t *f_raw = (uint64_t *)take(a.n_chunks * 8);
+  p.max_full = a.n_chunks * (a.cap / a.chunk + 1);
+  p.fullE = (uint32_t *)take(p.max_full * 4);
+  size_t tb = scan_temp_bytes(a.n_chunks);
+  void *tmp = take(tb);
+  const unsigned g = (unsigned)((a.n_chunks + 255) / 256);
+  CompactParams q = p;
+  q.nonfull = nf_raw;
+  q.full = f_raw;
+  hipLaunchKernelGGL(seg_sums, dim3(g), dim3(256), 0, s, q);
+  hipError_t e = hipGetLastError();
+  if (e) return e;
+  e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, nf_raw, p.nonfull, (int)a.n_chunks, s);
+  if (e) return e;
+  e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, f_raw, p.full, (int)a.n_chunks, s);
+  if (e) return e;
+  hipLaunchKernelGGL(seg_totals, dim3(1), dim3(1), 0, s, p, nf_raw + a.n_chunks - 1, f_raw + a.n_chunks - 1);
+  hipLaunchKernelGGL(full_list, dim3(g), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(copy_rows, dim3((unsigned)((a.n_chunks + 3) / 4)), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(chunk_counts, dim3(1024), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace ccj

@@ -68,4 +68,7 @@ hipError_t launch_result_checksum(const uint32_t *count, const uint32_t *sel, co
                                   uint64_t n_chunks, uint64_t cap, uint32_t chunk, uint64_t row_base,
                                   unsigned long long *acc, hipStream_t s);
 
+size_t compact_workspace(uint64_t n_chunks, uint64_t cap, uint32_t chunk);
+hipError_t launch_compact(const ccj_compact_args &a, hipStream_t s);
+
 }  // namespace ccj

@@ -127,6 +127,46 @@ typedef struct ccj_probe_args {
 
 int ccj_probe(const ccj_table *table, const ccj_probe_args *args, ccj_stream stream);
 
+/* ---- compaction ------------------------------------------------------------------------- */
+/* Replaces NaiveCompactor::Compact + Flush (compactor.cpp:5-41, compactor.h:23) applied to every
+ * Next result of a ccj_probe output, in pipeline order (chunk-major, round-major), with the
+ * reference's defect fixed (fresh temp chunk, the commented compactor.cpp:36):
+ *   - a Next result of exactly `chunk` rows passes through as its own output chunk (:6);
+ *   - other results are appended (DataChunk::Append, base.cpp:15-27: every column gathered
+ *     through the selection vector) into a cache that is emitted whenever the next result would
+ *     overflow it (:22-35); Flush emits the final partial chunk.
+ * Output: dense chunks of `chunk` rows: out_cols[k] = input column k at the matched row,
+ * out_payload = the probe payload (reference result column m+1; column m is never written by the
+ * reference and is not materialised), out_row = global probe row (c*chunk + sel).
+ * Needs out_round_counts from the probe (the Next boundaries). */
+#define CCJ_MAX_COLS 16
+typedef struct ccj_compact_args {
+  const uint32_t *count;        /* ccj_probe outputs (device) */
+  const uint32_t *sel;
+  const int64_t *payload;       /* or NULL */
+  const uint32_t *rounds;
+  const uint32_t *round_counts;
+  uint64_t n_chunks;
+  uint64_t cap;
+  uint32_t max_rounds;
+  uint32_t chunk;
+  uint32_t n_cols;              /* probe-side columns carried along, <= CCJ_MAX_COLS */
+  uint32_t reserved;
+  const int64_t *cols[CCJ_MAX_COLS];     /* device int64[n_chunks*chunk] each (chunk-major) */
+  int64_t *out_cols[CCJ_MAX_COLS];       /* device int64[out_cap_rows] each */
+  int64_t *out_payload;         /* device int64[out_cap_rows] or NULL */
+  uint64_t *out_row;            /* device uint64[out_cap_rows] or NULL */
+  uint32_t *out_chunk_counts;   /* device uint32[out_cap_rows / chunk] */
+  uint64_t out_cap_rows;        /* multiple of chunk */
+  uint64_t *out_n_chunks;       /* device word: output chunks written */
+  void *workspace;              /* device scratch of ccj_compact_workspace_size(n_chunks, ...) bytes */
+  size_t workspace_bytes;
+  uint32_t *status;             /* device word (ccj_flag bits) or NULL */
+} ccj_compact_args;
+
+size_t ccj_compact_workspace_size(uint64_t n_chunks, uint64_t cap, uint32_t chunk);
+int ccj_compact(const ccj_compact_args *args, ccj_stream stream);
+
 /* ---- workload + measurement helpers (not on the reference's path) ------------------------- */
 /* Synthetic probe column: d_out[i] = SplitMix64(seed) output (first_row + i) mod range — the
  * stream of oracle/ccj_gen.h ccj_uniform_key, so any row can be regenerated on the host.

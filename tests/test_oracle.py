@@ -136,3 +136,32 @@ def test_compact_plan_properties(B):
     for s in np.flatnonzero(segs == B):
         d = dest[start[s]:start[s] + B]
         assert d[0] % B == 0 and (np.diff(d.astype(np.int64)) == 1).all()
+
+
+def closed_form_compaction(segs, B):
+    """The prefix-sum form the device compactor uses (csrc/ccj_compact.hip header)."""
+    segs = np.asarray(segs, np.int64)
+    full = segs == B
+    t = np.concatenate([[0], np.cumsum(np.where(full, 0, segs))[:-1]])
+    F = np.concatenate([[0], np.cumsum(full)[:-1]])
+    E = np.where(t == 0, 0, (t + B - 1) // B - 1)
+    fullE = E[full]
+    dest = []
+    for s, c in enumerate(segs):
+        for j in range(c):
+            if full[s]:
+                dest.append((E[s] + F[s]) * B + j)
+            else:
+                u = t[s] + j
+                k = u // B
+                dest.append((k + np.searchsorted(fullE, k, side="right")) * B + u % B)
+    return np.array(dest, np.int64)
+
+
+@pytest.mark.parametrize("B,seed", [(4, 0), (4, 1), (8, 2), (16, 3), (5, 4)])
+def test_compaction_closed_form_equals_sequential(B, seed):
+    rng = np.random.default_rng(seed)
+    segs = rng.integers(0, B + 1, size=400)
+    segs[rng.random(400) < 0.2] = B
+    dest, _ = O.compact_plan(segs.astype(np.uint32), B)
+    assert np.array_equal(closed_form_compaction(segs, B), dest.astype(np.int64))
