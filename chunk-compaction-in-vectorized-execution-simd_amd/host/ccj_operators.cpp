@@ -1,0 +1,239 @@
+// ccj_operators.cpp — reference operator surface over the ccj C ABI (see ccj_operators.h).
+#include "ccj_operators.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <string>
+
+namespace simd_compaction_amd {
+
+namespace {
+
+void check(int rc, const char *what) {
+  if (rc != CCJ_OK) throw EngineError(std::string(what) + ": " + ccj_last_error());
+}
+
+void hip_check(hipError_t e, const char *what) {
+  if (e != hipSuccess) throw EngineError(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace
+
+void InitDevice(int device) { check(ccj_device_init(device), "ccj_device_init"); }
+
+// ---------------------------------------------------------------------------------------------
+DataChunk::DataChunk(const vector<AttributeType> &types)
+    : count_(0), types_(types), selection_vector_(kBlockSize) {
+  for (auto t : types) data_.emplace_back(t);
+  for (size_t i = 0; i < kBlockSize; ++i) selection_vector_[i] = (uint32_t)i;
+}
+
+void DataChunk::Append(DataChunk &chunk, size_t num, size_t offset) {
+  if (types_.size() != chunk.types_.size() || count_ + num > kBlockSize)
+    throw EngineError("DataChunk::Append: column mismatch or overflow");  // base.cpp:16-17 asserts
+  for (size_t c = 0; c < types_.size(); ++c) {
+    auto &dst = *data_[c].data_;
+    auto &src = *chunk.data_[c].data_;
+    for (size_t j = 0; j < num; ++j) dst[count_ + j] = src[chunk.selection_vector_[j + offset]];
+  }
+  count_ += num;
+}
+
+void DataChunk::AppendTuple(vector<Attribute> &tuple) {
+  for (size_t c = 0; c < types_.size(); ++c) data_[c].GetValue(count_) = tuple[c];
+  ++count_;
+}
+
+void DataChunk::Slice(DataChunk &other, vector<uint32_t> &sel, size_t count) {
+  count_ = count;
+  for (size_t c = 0; c < other.data_.size(); ++c) data_[c].Reference(other.data_[c]);
+  for (size_t i = 0; i < count; ++i) selection_vector_[i] = other.selection_vector_[sel[i]];
+}
+
+void DataChunk::Reset() {  // base.h:96-99
+  count_ = 0;
+  for (size_t i = 0; i < kBlockSize; ++i) selection_vector_[i] = (uint32_t)i;
+}
+
+// ---------------------------------------------------------------------------------------------
+// One ccj_table plus the device buffers of a single-chunk probe (the compatibility path: one
+// launch per Probe call; batched callers use ccj_probe directly).
+class DeviceTable {
+ public:
+  DeviceTable(int kind, size_t n, size_t cf) {
+    check(ccj_table_build_reference(kind, n, cf, CCJ_LAYOUT_REFERENCE, nullptr, &t_), "ccj_table_build_reference");
+    check(ccj_table_get_info(t_, &info_), "ccj_table_get_info");
+    hip_check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+  }
+  ~DeviceTable() {
+    Release();
+    ccj_table_free(t_);
+    (void)hipStreamDestroy(stream_);
+  }
+
+  // Probe + every Next round of one chunk: the whole ScanStructure lifetime in one launch.
+  ChunkProbeResult Run(Vector &join_key, size_t count, const vector<uint32_t> &sel) {
+    Ensure();
+    const size_t n = kBlockSize;
+    if (count > n || sel.size() < count) throw EngineError("Probe: count exceeds kBlockSize / sel");
+    const uint32_t cnt = (uint32_t)count;
+    hip_check(hipMemcpyAsync(d_keys_, join_key.Data(), n * sizeof(int64_t), hipMemcpyHostToDevice, stream_), "H2D");
+    if (count) hip_check(hipMemcpyAsync(d_sel_, sel.data(), count * 4, hipMemcpyHostToDevice, stream_), "H2D");
+    hip_check(hipMemcpyAsync(d_counts_, &cnt, 4, hipMemcpyHostToDevice, stream_), "H2D");
+    hip_check(hipMemsetAsync(d_status_, 0, 4, stream_), "memset");
+    ccj_probe_args a{};
+    a.keys = d_keys_;
+    a.sel = d_sel_;
+    a.counts = d_counts_;
+    a.n_rows = n;
+    a.chunk = (uint32_t)n;
+    a.max_rounds = max_rounds_;
+    a.cap = cap_;
+    a.out_count = d_count_;
+    a.out_sel = d_osel_;
+    a.out_payload = d_pay_;
+    a.out_rounds = d_rounds_;
+    a.out_round_counts = d_rc_;
+    a.status = d_status_;
+    check(ccj_probe(t_, &a, stream_), "ccj_probe");
+    uint32_t hdr[3];
+    hip_check(hipMemcpyAsync(&hdr[0], d_count_, 4, hipMemcpyDeviceToHost, stream_), "D2H");
+    hip_check(hipMemcpyAsync(&hdr[1], d_rounds_, 4, hipMemcpyDeviceToHost, stream_), "D2H");
+    hip_check(hipMemcpyAsync(&hdr[2], d_status_, 4, hipMemcpyDeviceToHost, stream_), "D2H");
+    hip_check(hipStreamSynchronize(stream_), "sync");
+    if (hdr[2]) throw EngineError("ccj_probe raised status flags " + std::to_string(hdr[2]));
+    ChunkProbeResult r;
+    r.round_counts.resize(hdr[1]);
+    r.sel.resize(hdr[0]);
+    r.payload.resize(hdr[0]);
+    if (hdr[1]) hip_check(hipMemcpyAsync(r.round_counts.data(), d_rc_, hdr[1] * 4, hipMemcpyDeviceToHost, stream_), "D2H");
+    if (hdr[0]) {
+      hip_check(hipMemcpyAsync(r.sel.data(), d_osel_, hdr[0] * 4, hipMemcpyDeviceToHost, stream_), "D2H");
+      hip_check(hipMemcpyAsync(r.payload.data(), d_pay_, hdr[0] * 8, hipMemcpyDeviceToHost, stream_), "D2H");
+    }
+    hip_check(hipStreamSynchronize(stream_), "sync");
+    return r;
+  }
+  const ccj_table *handle() const { return t_; }
+
+ private:
+  void Ensure() {
+    if (sized_for_ == kBlockSize) return;
+    Release();
+    const size_t n = kBlockSize;
+    cap_ = n * std::max<uint64_t>(1, info_.max_dup);
+    max_rounds_ = info_.max_rounds + 1;
+    hip_check(hipMalloc(&d_keys_, n * 8), "hipMalloc");
+    hip_check(hipMalloc(&d_sel_, n * 4), "hipMalloc");
+    hip_check(hipMalloc(&d_counts_, 4), "hipMalloc");
+    hip_check(hipMalloc(&d_count_, 4), "hipMalloc");
+    hip_check(hipMalloc(&d_rounds_, 4), "hipMalloc");
+    hip_check(hipMalloc(&d_status_, 4), "hipMalloc");
+    hip_check(hipMalloc(&d_osel_, cap_ * 4), "hipMalloc");
+    hip_check(hipMalloc(&d_pay_, cap_ * 8), "hipMalloc");
+    hip_check(hipMalloc(&d_rc_, max_rounds_ * 4), "hipMalloc");
+    sized_for_ = n;
+  }
+  void Release() {
+    for (void *p : {(void *)d_keys_, (void *)d_sel_, (void *)d_counts_, (void *)d_count_, (void *)d_rounds_,
+                    (void *)d_status_, (void *)d_osel_, (void *)d_pay_, (void *)d_rc_})
+      if (p) (void)hipFree(p);
+    d_keys_ = nullptr;
+    d_sel_ = d_counts_ = d_count_ = d_rounds_ = d_status_ = d_osel_ = d_rc_ = nullptr;
+    d_pay_ = nullptr;
+    sized_for_ = 0;
+  }
+
+  ccj_table *t_ = nullptr;
+  ccj_table_info info_{};
+  hipStream_t stream_{};
+  size_t sized_for_ = 0;
+  uint64_t cap_ = 0;
+  uint32_t max_rounds_ = 0;
+  int64_t *d_keys_ = nullptr, *d_pay_ = nullptr;
+  uint32_t *d_sel_ = nullptr, *d_counts_ = nullptr, *d_count_ = nullptr, *d_rounds_ = nullptr, *d_status_ = nullptr,
+           *d_osel_ = nullptr, *d_rc_ = nullptr;
+};
+
+// Fills `result` with one Next result: Slice (base.cpp:37-47) + payload column m+1 at the selected
+// physical rows (linear_probing_ht.cpp:85-94, chaining_ht.cpp:69-76).
+static void Materialise(const ChunkProbeResult &res, size_t pos, size_t rc, DataChunk &input, DataChunk &result) {
+  result.count_ = rc;
+  for (size_t c = 0; c < input.data_.size(); ++c) result.data_[c].Reference(input.data_[c]);
+  auto &pay = result.data_[input.data_.size() + 1];
+  for (size_t i = 0; i < rc; ++i) {
+    result.selection_vector_[i] = res.sel[pos + i];
+    pay.GetValue(res.sel[pos + i]) = res.payload[pos + i];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+LPHashTable::LPHashTable(size_t n, size_t cf) : t_(new DeviceTable(CCJ_TABLE_LP, n, cf)) {}
+LPHashTable::~LPHashTable() = default;
+const ccj_table *LPHashTable::handle() const { return t_->handle(); }
+
+LPScanStructure LPHashTable::Probe(Vector &join_key, size_t count, vector<uint32_t> &sel_vec) {
+  return LPScanStructure(t_->Run(join_key, count, sel_vec));
+}
+
+size_t LPScanStructure::Next(Vector &, DataChunk &input, DataChunk &result) {
+  result.Reset();
+  if (!HasNext()) return 0;
+  const size_t rc = res_.round_counts[round_++];
+  Materialise(res_, pos_, rc, input, result);  // LP Next slices even an empty result (:85)
+  pos_ += rc;
+  return rc;
+}
+
+HashTable::HashTable(size_t n, size_t cf) : t_(new DeviceTable(CCJ_TABLE_CHAIN, n, cf)) {}
+HashTable::~HashTable() = default;
+const ccj_table *HashTable::handle() const { return t_->handle(); }
+
+ScanStructure HashTable::Probe(Vector &join_key, size_t count, vector<uint32_t> &sel_vec) {
+  return ScanStructure(t_->Run(join_key, count, sel_vec));
+}
+
+size_t ScanStructure::EmitRound(DataChunk &input, DataChunk &result) {
+  const size_t rc = res_.round_counts[round_++];
+  if (rc > 0) Materialise(res_, pos_, rc, input, result);  // chaining slices only on a match (:67-76)
+  pos_ += rc;
+  return rc;
+}
+
+// chaining_ht.cpp:60-80 + ScanInnerJoin :82-107: repeat rounds until one matches or all ran out.
+size_t ScanStructure::Next(Vector &, DataChunk &input, DataChunk &result) {
+  result.Reset();
+  while (HasNext()) {
+    const size_t rc = EmitRound(input, result);
+    if (rc > 0) return rc;
+  }
+  return 0;
+}
+
+// chaining_ht.cpp:138-173: exactly one round per call.
+size_t ScanStructure::InOneNext(Vector &, DataChunk &input, DataChunk &result) {
+  result.Reset();
+  if (!HasNext()) return 0;
+  const size_t rc = EmitRound(input, result);
+  result.count_ = rc;
+  return rc;
+}
+
+// ---------------------------------------------------------------------------------------------
+void NaiveCompactor::Compact(unique_ptr<DataChunk> &chunk) {
+  if (chunk->count_ == kBlockSize) return;  // compactor.cpp:6
+  if (chunk->count_ <= kBlockSize - cached_chunk_->count_) {
+    cached_chunk_->Append(*chunk, chunk->count_);
+    chunk->Reset();
+    return;
+  }
+  const size_t n_move = kBlockSize - cached_chunk_->count_;
+  cached_chunk_->Append(*chunk, n_move);
+  temp_chunk_->Append(*chunk, chunk->count_ - n_move, n_move);
+  chunk.swap(cached_chunk_);
+  cached_chunk_.swap(temp_chunk_);
+  temp_chunk_ = std::make_unique<DataChunk>(types_);  // never recycle a chunk whose columns may be shared
+}
+
+}  // namespace simd_compaction_amd
