@@ -56,7 +56,8 @@ class CompactArgs(C.Structure):
 EXPORTS = ["ccj_last_error", "ccj_abi_version", "ccj_device_init", "ccj_table_build_reference",
            "ccj_table_build_from_host", "ccj_table_build_on_device", "ccj_table_get_info", "ccj_table_free",
            "ccj_probe", "ccj_gen_uniform_keys", "ccj_probe_cost", "ccj_result_checksum",
-           "ccj_compact_workspace_size", "ccj_compact"]
+           "ccj_compact_workspace_size", "ccj_compact", "ccj_partition_workspace_size", "ccj_partition_by_owner",
+           "ccj_result_checksum_mapped", "ccj_gen_reference_keys"]
 
 
 def build(force: bool = False) -> str:
@@ -83,10 +84,15 @@ def lib():
         L.ccj_table_free.argtypes = [vp]
         L.ccj_probe.argtypes = [vp, C.POINTER(ProbeArgs), vp]
         L.ccj_gen_uniform_keys.argtypes = [vp, u64, u64, u64, u64, vp]
+        L.ccj_gen_reference_keys.argtypes = [vp, u64, u64, u64, u64, vp]
         L.ccj_probe_cost.argtypes = [vp, vp, u64, vp, vp]
         L.ccj_compact_workspace_size.restype = C.c_size_t
         L.ccj_compact_workspace_size.argtypes = [u64, u64, C.c_uint32]
         L.ccj_compact.argtypes = [C.POINTER(CompactArgs), vp]
+        L.ccj_partition_workspace_size.restype = C.c_size_t
+        L.ccj_partition_workspace_size.argtypes = [u64, C.c_uint32]
+        L.ccj_partition_by_owner.argtypes = [vp, u64, C.c_uint32, u64, vp, vp, vp, vp, C.c_size_t, vp]
+        L.ccj_result_checksum_mapped.argtypes = [vp, vp, vp, u64, u64, C.c_uint32, vp, vp, vp]
         L.ccj_result_checksum.argtypes = [vp, vp, vp, u64, u64, C.c_uint32, u64, vp, vp]
         _lib = L
     return _lib
@@ -120,15 +126,30 @@ def gen_uniform_keys(n: int, seed: int, rng: int, first_row: int = 0, out=None, 
     return out
 
 
-def result_checksum(out, chunk: int, row_base: int = 0, stream=None):
-    """(matches, L2 checksum) of a probe output, computed on the device."""
+def result_checksum(out, chunk: int, row_base: int = 0, row_map=None, stream=None):
+    """(matches, L2 checksum) of a probe output, computed on the device.  row_map: optional device
+    uint64 column giving the global row of every probed position (shuffled inputs)."""
     import torch
     acc = torch.zeros(2, dtype=torch.int64, device=out["count"].device)
-    check(lib().ccj_result_checksum(_ptr(out["count"]), _ptr(out["sel"]), _ptr(out["payload"]), out["n_chunks"],
-                                    out["cap"], chunk, row_base, _ptr(acc), _stream(stream)), "ccj_result_checksum")
+    if row_map is None:
+        check(lib().ccj_result_checksum(_ptr(out["count"]), _ptr(out["sel"]), _ptr(out["payload"]), out["n_chunks"],
+                                        out["cap"], chunk, row_base, _ptr(acc), _stream(stream)), "ccj_result_checksum")
+    else:
+        check(lib().ccj_result_checksum_mapped(_ptr(out["count"]), _ptr(out["sel"]), _ptr(out["payload"]),
+                                               out["n_chunks"], out["cap"], chunk, _ptr(row_map), _ptr(acc),
+                                               _stream(stream)), "ccj_result_checksum_mapped")
     torch.cuda.synchronize()
     m, l2 = acc.cpu().tolist()
     return m, l2 & 0xFFFFFFFFFFFFFFFF
+
+
+def gen_reference_keys(first: int, n: int, n_total: int, cf: int = 1, out=None, stream=None):
+    """Device build-side keys first..first+n-1 of the reference generator (linear_probing_ht.cpp:14-25)."""
+    import torch
+    if out is None:
+        out = torch.empty(n, dtype=torch.int64, device=torch.device("cuda", torch.cuda.current_device()))
+    check(lib().ccj_gen_reference_keys(_ptr(out), first, n, n_total, cf, _stream(stream)), "ccj_gen_reference_keys")
+    return out
 
 
 class Table:
@@ -260,3 +281,24 @@ def compact(probe_out, chunk: int, cols=(), payload: bool = True, rows: bool = T
     o["_ws"] = ws
     check(lib().ccj_compact(C.byref(a), _stream(stream)), "ccj_compact")
     return o
+
+
+class OwnerPartitioner:
+    """Owner partitioning (include/ccj.h ccj_partition_by_owner) with reusable buffers."""
+
+    def __init__(self, n: int, parts: int, device=None):
+        import torch
+        dev = device or torch.device("cuda", torch.cuda.current_device())
+        self.n, self.parts = n, parts
+        self.ws_bytes = lib().ccj_partition_workspace_size(n, parts)
+        self.ws = torch.empty(max(self.ws_bytes, 8), dtype=torch.uint8, device=dev)
+        self.keys = torch.empty(n, dtype=torch.int64, device=dev)
+        self.rows = torch.empty(n, dtype=torch.int64, device=dev)
+        self.counts = torch.zeros(parts, dtype=torch.int64, device=dev)
+
+    def __call__(self, keys, row_base: int = 0, stream=None):
+        assert keys.numel() == self.n
+        check(lib().ccj_partition_by_owner(_ptr(keys), self.n, self.parts, row_base, _ptr(self.keys),
+                                           _ptr(self.rows), _ptr(self.counts), _ptr(self.ws), self.ws_bytes,
+                                           _stream(stream)), "ccj_partition_by_owner")
+        return self.keys, self.rows, self.counts

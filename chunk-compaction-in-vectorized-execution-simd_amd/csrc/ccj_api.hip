@@ -269,7 +269,7 @@ int ccj_table_build_reference(int kind, uint64_t n, uint64_t cf, int layout, ccj
   int64_t *d_keys = nullptr;
   if (hipMalloc(&d_keys, std::max<uint64_t>(n, 1) * sizeof(int64_t)) != hipSuccess)
     return fail(CCJ_ERR_OOM, "reference keys: hipMalloc failed");
-  hipError_t e = ccj::launch_gen_reference_keys(d_keys, n, cf, s);
+  hipError_t e = ccj::launch_gen_reference_keys(d_keys, 0, n, n, cf, s);
   if (e != hipSuccess) {
     (void)hipFree(d_keys);
     return hip_fail(e, "gen reference keys");
@@ -371,10 +371,37 @@ int ccj_compact(const ccj_compact_args *a, ccj_stream stream) {
   return CCJ_OK;
 }
 
+size_t ccj_partition_workspace_size(uint64_t n, uint32_t parts) {
+  return parts ? ccj::partition_workspace(n, parts) : 0;
+}
+
+int ccj_partition_by_owner(const int64_t *d_keys, uint64_t n, uint32_t parts, uint64_t row_base, int64_t *d_out_keys,
+                           uint64_t *d_out_rows, uint64_t *d_out_counts, void *d_workspace, size_t workspace_bytes,
+                           ccj_stream stream) {
+  if (parts == 0 || parts > ccj::kMaxParts || (parts & (parts - 1)))
+    return fail(CCJ_ERR_INVALID, "ccj_partition_by_owner: parts must be a power of two <= 64");
+  if (!d_out_counts || (n && (!d_keys || !d_out_keys || !d_out_rows || !d_workspace)))
+    return fail(CCJ_ERR_INVALID, "ccj_partition_by_owner: missing buffer");
+  if (workspace_bytes < ccj::partition_workspace(n, parts))
+    return fail(CCJ_ERR_INVALID, "ccj_partition_by_owner: workspace too small");
+  if (n >= (1ull << 31) * 4096) return fail(CCJ_ERR_LIMIT, "ccj_partition_by_owner: too many keys");
+  HIP_TRY(ccj::launch_partition(d_keys, n, parts, row_base, d_out_keys, d_out_rows, d_out_counts, d_workspace,
+                                (hipStream_t)stream),
+          "partition launch");
+  return CCJ_OK;
+}
+
 int ccj_gen_uniform_keys(int64_t *d_out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t range,
                          ccj_stream stream) {
   if ((!d_out && n) || range == 0) return fail(CCJ_ERR_INVALID, "ccj_gen_uniform_keys: bad argument");
   HIP_TRY(ccj::launch_gen_uniform(d_out, n, seed, first_row, range, (hipStream_t)stream), "gen uniform keys");
+  return CCJ_OK;
+}
+
+int ccj_gen_reference_keys(int64_t *d_out, uint64_t first, uint64_t n, uint64_t n_total, uint64_t cf,
+                           ccj_stream stream) {
+  if ((!d_out && n) || cf == 0 || first + n > n_total) return fail(CCJ_ERR_INVALID, "ccj_gen_reference_keys: bad argument");
+  HIP_TRY(ccj::launch_gen_reference_keys(d_out, first, n, n_total, cf, (hipStream_t)stream), "gen reference keys");
   return CCJ_OK;
 }
 
@@ -391,7 +418,19 @@ int ccj_result_checksum(const uint32_t *out_count, const uint32_t *out_sel, cons
                         ccj_stream stream) {
   if ((!out_count || !out_sel || !out_payload) && n_chunks) return fail(CCJ_ERR_INVALID, "ccj_result_checksum: null");
   if (!d_acc) return fail(CCJ_ERR_INVALID, "ccj_result_checksum: null acc");
-  HIP_TRY(ccj::launch_result_checksum(out_count, out_sel, out_payload, n_chunks, cap, chunk, row_base,
+  HIP_TRY(ccj::launch_result_checksum(out_count, out_sel, out_payload, n_chunks, cap, chunk, row_base, nullptr,
+                                      (unsigned long long *)d_acc, (hipStream_t)stream),
+          "result checksum");
+  return CCJ_OK;
+}
+
+int ccj_result_checksum_mapped(const uint32_t *out_count, const uint32_t *out_sel, const int64_t *out_payload,
+                               uint64_t n_chunks, uint64_t cap, uint32_t chunk, const uint64_t *row_map,
+                               uint64_t *d_acc, ccj_stream stream) {
+  if ((!out_count || !out_sel || !out_payload || !row_map) && n_chunks)
+    return fail(CCJ_ERR_INVALID, "ccj_result_checksum_mapped: null");
+  if (!d_acc) return fail(CCJ_ERR_INVALID, "ccj_result_checksum_mapped: null acc");
+  HIP_TRY(ccj::launch_result_checksum(out_count, out_sel, out_payload, n_chunks, cap, chunk, 0, row_map,
                                       (unsigned long long *)d_acc, (hipStream_t)stream),
           "result checksum");
   return CCJ_OK;

@@ -30,6 +30,7 @@ __host__ __device__ __forceinline__ uint64_t murmurhash64(uint64_t x) {
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr uint32_t kMaxChunk = 2048;
+constexpr uint32_t kMaxParts = 64;  // owner partitions (GPUs) per multisplit
 
 struct ProbeParams {
   const int64_t *table;
@@ -53,7 +54,8 @@ struct ProbeParams {
 
 // Launchers (ccj_kernels.hip).  Return hipError_t of the launch.
 hipError_t launch_probe(int kind, const ProbeParams &p, hipStream_t s);
-hipError_t launch_gen_reference_keys(int64_t *out, uint64_t n, uint64_t cf, hipStream_t s);
+hipError_t launch_gen_reference_keys(int64_t *out, uint64_t first, uint64_t n, uint64_t n_total, uint64_t cf,
+                                     hipStream_t s);
 hipError_t launch_fill(int64_t *p, uint64_t n, int64_t v, hipStream_t s);
 hipError_t launch_lp_insert(const int64_t *keys, uint64_t n, int64_t *slots, uint32_t mask, hipStream_t s);
 // Per-segment run statistics of an LP slot array (segment = 4096 slots): 4 x uint32 per segment:
@@ -66,9 +68,12 @@ hipError_t launch_probe_cost(int kind, const int64_t *table, const uint32_t *off
                              const int64_t *keys, uint64_t n, unsigned long long *acc, hipStream_t s);
 hipError_t launch_result_checksum(const uint32_t *count, const uint32_t *sel, const int64_t *payload,
                                   uint64_t n_chunks, uint64_t cap, uint32_t chunk, uint64_t row_base,
-                                  unsigned long long *acc, hipStream_t s);
+                                  const uint64_t *row_map, unsigned long long *acc, hipStream_t s);
 
 size_t compact_workspace(uint64_t n_chunks, uint64_t cap, uint32_t chunk);
 hipError_t launch_compact(const ccj_compact_args &a, hipStream_t s);
+size_t partition_workspace(uint64_t n, uint32_t parts);
+hipError_t launch_partition(const int64_t *keys, uint64_t n, uint32_t parts, uint64_t row_base, int64_t *out_keys,
+                            uint64_t *out_rows, uint64_t *out_counts, void *ws, hipStream_t s);
 
 }  // namespace ccj

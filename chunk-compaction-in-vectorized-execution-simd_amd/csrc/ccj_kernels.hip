@@ -385,9 +385,9 @@ hipError_t launch_kind(const ProbeParams &p, hipStream_t s) {
 }
 
 // linear_probing_ht.cpp:16-25: key t of the generator is (t / cf) * step.
-__global__ void gen_reference_keys(int64_t *out, uint64_t n, uint64_t cf, uint64_t step) {
+__global__ void gen_reference_keys(int64_t *out, uint64_t first, uint64_t n, uint64_t cf, uint64_t step) {
   for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x)
-    out[t] = (int64_t)((t / cf) * step);
+    out[t] = (int64_t)(((first + t) / cf) * step);
 }
 
 __global__ void fill_i64(int64_t *p, uint64_t n, int64_t v) {
@@ -513,14 +513,15 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t z) {
 __global__ __launch_bounds__(256) void result_checksum(const uint32_t *count, const uint32_t *sel,
                                                        const int64_t *payload, uint64_t n_chunks, uint64_t cap,
                                                        uint32_t chunk, uint64_t row_base,
-                                                       unsigned long long *acc) {
+                                                       const uint64_t *row_map, unsigned long long *acc) {
   const uint32_t lane = threadIdx.x & 63u;
   unsigned long long m = 0, l2 = 0;
   for (uint64_t c = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < n_chunks; c += (uint64_t)gridDim.x * 4) {
     const uint32_t n = count[c];
     m += n;
     for (uint32_t j = lane; j < n; j += 64) {
-      const uint64_t row = row_base + c * chunk + sel[c * cap + j];
+      const uint64_t local = c * chunk + sel[c * cap + j];
+      const uint64_t row = row_map ? row_map[local] : row_base + local;
       l2 += fmix64(row * 0x9e3779b97f4a7c15ULL + fmix64((uint64_t)payload[c * cap + j] + 1ULL));
     }
   }
@@ -545,11 +546,12 @@ hipError_t launch_probe(int kind, const ProbeParams &p, hipStream_t s) {
   return kind == CCJ_TABLE_LP ? launch_kind<CCJ_TABLE_LP>(p, s) : launch_kind<CCJ_TABLE_CHAIN>(p, s);
 }
 
-hipError_t launch_gen_reference_keys(int64_t *out, uint64_t n, uint64_t cf, hipStream_t s) {
+hipError_t launch_gen_reference_keys(int64_t *out, uint64_t first, uint64_t n, uint64_t n_total, uint64_t cf,
+                                     hipStream_t s) {
   if (n == 0) return hipSuccess;
-  const uint64_t num_unique = n / cf + (n % cf != 0);
-  const uint64_t step = n / num_unique;
-  hipLaunchKernelGGL(gen_reference_keys, dim3(grid_for(n, 256)), dim3(256), 0, s, out, n, cf, step);
+  const uint64_t num_unique = n_total / cf + (n_total % cf != 0);
+  const uint64_t step = n_total / num_unique;
+  hipLaunchKernelGGL(gen_reference_keys, dim3(grid_for(n, 256)), dim3(256), 0, s, out, first, n, cf, step);
   return hipGetLastError();
 }
 
@@ -582,10 +584,10 @@ hipError_t launch_probe_cost(int kind, const int64_t *table, const uint32_t *off
 
 hipError_t launch_result_checksum(const uint32_t *count, const uint32_t *sel, const int64_t *payload,
                                   uint64_t n_chunks, uint64_t cap, uint32_t chunk, uint64_t row_base,
-                                  unsigned long long *acc, hipStream_t s) {
+                                  const uint64_t *row_map, unsigned long long *acc, hipStream_t s) {
   if (n_chunks == 0) return hipSuccess;
   hipLaunchKernelGGL(result_checksum, dim3(grid_for(n_chunks, 4)), dim3(256), 0, s, count, sel, payload, n_chunks,
-                     cap, chunk, row_base, acc);
+                     cap, chunk, row_base, row_map, acc);
   return hipGetLastError();
 }
 

@@ -167,12 +167,28 @@ typedef struct ccj_compact_args {
 size_t ccj_compact_workspace_size(uint64_t n_chunks, uint64_t cap, uint32_t chunk);
 int ccj_compact(const ccj_compact_args *args, ccj_stream stream);
 
+/* ---- multi-GPU owner partitioning --------------------------------------------------------- */
+/* The exchange step of the radix-partitioned multi-GPU join: splits a key column
+ * into `parts` (a power of two, one per GPU) by owner(k) = murmurhash64(k) >> (64 - log2 parts),
+ * i.e. the top hash bits (the local tables use the low bits), keeping row order inside every
+ * destination.  Writes the keys and their global row ids (row_base + i) destination-major and
+ * the per-destination counts: the send buffers + split sizes of one all-to-all (RCCL, xGMI).
+ * No reference counterpart: the reference is single-threaded. */
+size_t ccj_partition_workspace_size(uint64_t n, uint32_t parts);
+int ccj_partition_by_owner(const int64_t *d_keys, uint64_t n, uint32_t parts, uint64_t row_base,
+                           int64_t *d_out_keys, uint64_t *d_out_rows, uint64_t *d_out_counts,
+                           void *d_workspace, size_t workspace_bytes, ccj_stream stream);
+
 /* ---- workload + measurement helpers (not on the reference's path) ------------------------- */
 /* Synthetic probe column: d_out[i] = SplitMix64(seed) output (first_row + i) mod range — the
  * stream of oracle/ccj_gen.h ccj_uniform_key, so any row can be regenerated on the host.
  * Replaces the reference's host-side source (main.cpp:41-55 + DataCollection::FetchChunk). */
 int ccj_gen_uniform_keys(int64_t *d_out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t range,
                          ccj_stream stream);
+/* Build-side keys first..first+n-1 of the reference generator for n_total tuples
+ * (linear_probing_ht.cpp:14-25: key t = (t / cf) * step), e.g. for sharding the build side. */
+int ccj_gen_reference_keys(int64_t *d_out, uint64_t first, uint64_t n, uint64_t n_total, uint64_t cf,
+                           ccj_stream stream);
 /* Work accounting for the roofline: d_acc[0] += table words examined (LP: slots read including
  * the terminating empty; chain: chain keys visited), d_acc[1] += matches, over n probe keys. */
 int ccj_probe_cost(const ccj_table *table, const int64_t *d_keys, uint64_t n, uint64_t *d_acc,
@@ -183,6 +199,11 @@ int ccj_probe_cost(const ccj_table *table, const int64_t *d_keys, uint64_t n, ui
 int ccj_result_checksum(const uint32_t *out_count, const uint32_t *out_sel, const int64_t *out_payload,
                         uint64_t n_chunks, uint64_t cap, uint32_t chunk, uint64_t row_base, uint64_t *d_acc,
                         ccj_stream stream);
+/* Same, with the probe rows mapped through row_map (row = row_map[c*chunk + sel]), for probes of
+ * shuffled columns whose original global rows travel beside the keys. */
+int ccj_result_checksum_mapped(const uint32_t *out_count, const uint32_t *out_sel, const int64_t *out_payload,
+                               uint64_t n_chunks, uint64_t cap, uint32_t chunk, const uint64_t *row_map,
+                               uint64_t *d_acc, ccj_stream stream);
 
 #ifdef __cplusplus
 }
