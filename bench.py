@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--layout", default="device", choices=["device", "reference"])
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-sample", type=int, default=1 << 26, help="probe keys in the multi-thread CPU sample")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 28, help="probe keys in the multi-thread CPU sample")
     ap.add_argument("--no-verify", action="store_true")
     return ap.parse_args()
 
@@ -77,8 +77,8 @@ def cpu_baseline(args):
     table = O.Table(O.LP, O.ref_build_keys(args.n_build, 1))
     build_s = time.perf_counter() - t0
     res = {}
-    for threads, n in ((1, min(args.cpu_sample // 8, 1 << 23)), (args.cpu_threads, args.cpu_sample)):
-        keys = O.uniform_keys(SEED, 0, n, args.n_build)
+    for threads, n in ((1, args.cpu_sample // 8), (args.cpu_threads, args.cpu_sample)):
+        keys = O.uniform_keys(SEED, 0, n, args.n_build, threads=args.cpu_threads)
         table.probe_totals(keys[: 1 << 16], args.chunk, threads=threads)  # warm
         t0 = time.perf_counter()
         m, l2 = table.probe_totals(keys, args.chunk, threads=threads)

@@ -219,6 +219,12 @@ uint64_t ccj_o_probe_totals(int kind, const int64_t *table, const uint64_t *buck
   return matches;
 }
 
+void ccj_o_gen_uniform(uint64_t seed, uint64_t row_begin, uint64_t n, uint64_t range, int64_t *out, int threads) {
+  if (threads <= 0) threads = omp_get_max_threads();
+#pragma omp parallel for num_threads(threads) schedule(static)
+  for (uint64_t i = 0; i < n; ++i) out[i] = ccj_uniform_key(seed, row_begin + i, range);
+}
+
 uint64_t ccj_o_count_uniform(uint64_t seed, uint64_t row_begin, uint64_t row_end, uint64_t range,
                              uint64_t n_build, uint64_t cf, uint64_t *l2_out, int threads) {
   uint64_t matches = 0, l2 = 0;

@@ -51,6 +51,9 @@ uint64_t ccj_o_probe_totals(int kind, const int64_t *table, const uint64_t *buck
                             const int64_t *keys, uint64_t n_rows, uint32_t chunk, uint64_t row_base,
                             uint64_t *l2_out, int threads);
 
+/* SplitMix64 probe keys rows [row_begin, row_begin + n) (ccj_gen.h ccj_uniform_key), threaded. */
+void ccj_o_gen_uniform(uint64_t seed, uint64_t row_begin, uint64_t n, uint64_t range, int64_t *out, int threads);
+
 /* Exact L1/L2 answer for a probe stream of SplitMix64 keys (ccj_gen.h) against the reference
  * generator's build side (n, cf), by membership. Returns matches; *l2 = checksum. */
 uint64_t ccj_o_count_uniform(uint64_t seed, uint64_t row_begin, uint64_t row_end, uint64_t range,

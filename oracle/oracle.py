@@ -49,6 +49,7 @@ def lib():
                                   C.c_uint32, u32p, u32p, i64p, u32p, u32p, C.c_int]
         L.ccj_o_probe_totals.restype = u64
         L.ccj_o_probe_totals.argtypes = [C.c_int, i64p, u64p, u64, i64p, u64, C.c_uint32, u64, u64p, C.c_int]
+        L.ccj_o_gen_uniform.argtypes = [u64, u64, u64, u64, i64p, C.c_int]
         L.ccj_o_count_uniform.restype = u64
         L.ccj_o_count_uniform.argtypes = [u64, u64, u64, u64, u64, u64, u64p, C.c_int]
         L.ccj_o_compact_plan.restype = u64
@@ -157,11 +158,11 @@ def fmix64(z):
         return z ^ (z >> np.uint64(31))
 
 
-def uniform_keys(seed, begin, end, rng):
-    i = np.arange(begin, end, dtype=np.uint64)
-    with np.errstate(over="ignore"):
-        s = np.uint64(seed) + (i + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
-    return (fmix64(s) % np.uint64(rng)).astype(np.int64)
+def uniform_keys(seed, begin, end, rng, threads=0):
+    """SplitMix64 probe keys of rows [begin, end) (ccj_gen.h ccj_uniform_key)."""
+    out = np.empty(end - begin, dtype=np.int64)
+    lib().ccj_o_gen_uniform(seed, begin, end - begin, rng, _p(out, C.c_int64), threads)
+    return out
 
 
 def l2_sum(rows, payload) -> int:
