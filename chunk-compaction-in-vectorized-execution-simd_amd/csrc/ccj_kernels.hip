@@ -22,18 +22,6 @@ __device__ __forceinline__ uint32_t lane_prefix(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// Emits one match: ordered by (round, j, lane) through the wave ballot `mb`.  The payload is the
-// matched table value, which equals the probe key: it is re-read from the key column (the chunk's
-// 16 KB were read moments earlier by the walk) instead of being held through the walk.
-__device__ __forceinline__ void emit_match(const ProbeParams &p, uint64_t obase, uint64_t total, uint64_t mb,
-                                           uint32_t r, uint64_t base) {
-  const uint64_t o = total + lane_prefix(mb);
-  if (o < p.cap) {
-    p.out_sel[obase + o] = r;
-    if (p.out_payload) p.out_payload[obase + o] = p.keys[base + r];
-  }
-}
-
 __device__ __forceinline__ uint32_t wave_or(uint32_t x) {
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) x |= (uint32_t)__shfl_xor((int)x, d);
@@ -69,8 +57,8 @@ __device__ __forceinline__ uint32_t phys_row(const ProbeParams &p, uint64_t base
 
 template <int KIND>
 __device__ void rounds_generic(const ProbeParams &p, uint64_t c, uint64_t base, uint32_t nj, uint32_t act,
-                               uint32_t &flags, uint64_t &total_out, uint32_t &rounds_out) {
-  const uint32_t lane = threadIdx.x;
+                               const int64_t *s_key, uint32_t &flags, uint64_t &total_out, uint32_t &rounds_out) {
+  const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint64_t obase = c * p.cap;
   uint64_t total = 0;
   uint32_t round = 0;
@@ -78,7 +66,7 @@ __device__ void rounds_generic(const ProbeParams &p, uint64_t c, uint64_t base, 
     uint32_t mat = 0;
     for (uint32_t j = 0; j < nj; ++j) {
       if ((act >> j) & 1u) {
-        const int64_t k = p.keys[base + phys_row(p, base, j * kWave + lane)];
+        const int64_t k = s_key[j * kWave + lane];
         const uint32_t h = (uint32_t)murmurhash64((uint64_t)k) & p.mask;
         if (KIND == CCJ_TABLE_LP) {
           const int64_t v = p.table[(h + round) & p.mask];
@@ -97,7 +85,13 @@ __device__ void rounds_generic(const ProbeParams &p, uint64_t c, uint64_t base, 
       const uint32_t j = (uint32_t)__builtin_ctz(any);
       const bool m = (mat >> j) & 1u;
       const uint64_t mb = __ballot(m);
-      if (m) emit_match(p, obase, total, mb, phys_row(p, base, j * kWave + lane), base);
+      if (m) {
+        const uint64_t o = total + lane_prefix(mb);
+        if (o < p.cap) {
+          p.out_sel[obase + o] = phys_row(p, base, j * kWave + lane);
+          if (p.out_payload) p.out_payload[obase + o] = s_key[j * kWave + lane];
+        }
+      }
       const uint32_t n = (uint32_t)__popcll(mb);
       total += n;
       rc += n;
@@ -112,31 +106,35 @@ __device__ void rounds_generic(const ProbeParams &p, uint64_t c, uint64_t base, 
 constexpr int kWin = 4;             // slots (LP) / chain keys per window load: 32 B, one aligned sector
 constexpr int kMaxFastRounds = 32;  // rounds recorded by the windowed path (bits of a u32)
 #ifndef CCJ_WALK_ROWS
-#define CCJ_WALK_ROWS 4
+#define CCJ_WALK_ROWS 2
 #endif
 constexpr int kWalkRows = CCJ_WALK_ROWS;  // rows per lane walked concurrently (loads in flight)
 
-constexpr int kEmitRows = 8;  // rows per lane whose key/sel loads are issued together in the emit
+constexpr int kEmitRows = 4;    // row groups per lane whose sel loads are issued together in the emit
+constexpr int kChunkWaves = 4;  // waves cooperating on one chunk
+constexpr int kBlock = kWave * kChunkWaves;
 
-// One wave per 64-thread workgroup = one chunk of up to 64*nj rows (row (j, lane) = j*64 + lane).
-// LDS (12 KB per wave): s_mm[nj*64] u32 — bit r set iff row (j, lane) matches in round r (Next
-// call r); s_off[kMaxFastRounds*32] u32 — matches of (round r, row group j), then its exclusive
-// prefix in round-major order: the output slot where that (r, j) group's ballot-pack starts.
+// One 256-thread workgroup (4 waves) per chunk of up to 64*nj rows; row (j, lane) = j*64 + lane is
+// owned by wave j % 4.  LDS (28 KB): s_key — the chunk's probe keys, staged once with coalesced
+// loads; s_mm[row] — bit r set iff the row matches in round r (Next call r); s_off[r*32 + j] —
+// matches of (round r, row group j), then their exclusive prefix in round-major order.
 //
 // Walk: every row's whole run (LP: home slot up to the first empty slot; chain: the bucket's CSR
-// range) is read once through aligned 32-byte windows, G rows per lane in flight.  A window is one
-// sector of a 64-byte line, so a continuation re-reads a line fetched moments earlier (L2-resident)
-// rather than one fetched a whole round of 2048 rows earlier — the reference's round-by-round
-// re-read (linear_probing_ht.cpp:72-80 then :100-110) loses L2 residency at GPU occupancy.
-// Count + scan: per (round, row group) match counts by ballot, exclusive scan across the wave.
-// Emit: row-group-major, but every match goes to offset s_off[r][j] + its ballot prefix, i.e.
-// exactly where the reference's round-major, idx-ascending result_vector order puts it (L3);
-// the payload/sel loads of kEmitRows row groups are then in flight together.
+// range) is read once through aligned 32-byte windows.  G cursors per lane each own every G-th row
+// of the lane and move on as soon as their run ends, so ~G window loads per lane stay in flight.
+// A continuation reads the line fetched moments earlier (L2-resident), not one fetched a whole
+// round of 2048 rows earlier — the reference's round-by-round re-read (linear_probing_ht.cpp:72-80,
+// :100-110) loses L2 residency at GPU occupancy.
+// Count + scan: per (round, row group) ballot counts, exclusive scan.  Emit: every match goes to
+// s_off[r][j] + its ballot prefix — the reference's round-major, idx-ascending result_vector
+// order (L3) — with the payload (== probe key) taken from LDS.
 template <int KIND, int G>
-__global__ __launch_bounds__(kWave) void probe_chunks(ProbeParams p) {
+__global__ __launch_bounds__(kBlock) void probe_chunks(ProbeParams p) {
+  __shared__ int64_t s_key[kMaxChunk];
   __shared__ uint32_t s_mm[kMaxChunk];
   __shared__ uint32_t s_off[kMaxFastRounds * 32];
-  const uint32_t lane = threadIdx.x;
+  __shared__ uint32_t s_red[3 * kChunkWaves];
+  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   const uint64_t c = blockIdx.x;
   const uint64_t base = c * p.chunk;
   const uint64_t rem = p.n_rows - base;
@@ -149,53 +147,53 @@ __global__ __launch_bounds__(kWave) void probe_chunks(ProbeParams p) {
     count = p.chunk;
   }
 
-  // Active rows: idx < count whose sel entry addresses a physical row of the chunk.
+  // Stage (Probe: linear_probing_ht.cpp:45-49 / chaining_ht.cpp:46-50): keys through sel -> LDS.
+  // Thread (wave, lane) stages rows j = 4q + wave, i.e. exactly the rows its lane owns: act bit q.
   uint32_t act = 0;
-  for (uint32_t j = 0; j < nj; ++j) {
-    const uint32_t i = j * kWave + lane;
+  for (uint32_t i = tid, q = 0; i < nj * kWave; i += kBlock, ++q) {
+    int64_t k = 0;
     if (i < count) {
-      if (phys_row(p, base, i) < phys) act |= 1u << j;
-      else flags |= CCJ_FLAG_BAD_INPUT;
+      const uint32_t r = phys_row(p, base, i);
+      if (r < phys) {
+        k = p.keys[base + r];
+        act |= 1u << q;
+      } else {
+        flags |= CCJ_FLAG_BAD_INPUT;
+      }
     }
+    s_key[i] = k;
+    s_mm[i] = 0u;
   }
-#pragma unroll
-  for (int q = 0; q < kMaxFastRounds * 32 / kWave; ++q) s_off[q * kWave + lane] = 0u;
-  for (uint32_t q = 0; q < nj; ++q) s_mm[q * kWave + lane] = 0u;
+  for (uint32_t q = tid; q < kMaxFastRounds * 32; q += kBlock) s_off[q] = 0u;
+  const uint32_t nq = nj > wave ? (nj - wave + kChunkWaves - 1) / kChunkWaves : 0;
 
-  // Walk.  G independent cursors per lane; cursor g owns rows j = g, g+G, ... of this lane and moves
-  // to its next active row as soon as the current run ends, so every iteration keeps ~G window loads
-  // per lane in flight instead of waiting for the slowest lane of a row group.  The next row's key
-  // is prefetched while the current row is walked.
+  // Walk.
   uint32_t lane_rounds = 0;
   bool long_run = false;
   {
-    uint32_t j[G], nj_next[G], cur[G], r0[G], lim[G], mm[G];
-    int64_t kj[G], nk[G];
-    uint32_t live = 0, start = 0, nk_ok = 0;  // bit g: cursor has a row / row needs its CSR range / nk loaded
-    auto next_active = [&](uint32_t from, int g) -> uint32_t {  // first active row >= from, == g mod G
-      for (uint32_t t = from; t < nj; t += G)
+    uint32_t q[G], cur[G], r0[G], lim[G], mm[G];
+    int64_t kj[G];
+    uint32_t live = 0, start = 0;  // bit g: cursor has a row / row still needs its CSR range
+    auto next_active = [&](uint32_t from) -> uint32_t {
+      for (uint32_t t = from; t < nq; t += G)
         if ((act >> t) & 1u) return t;
-      return nj;
+      return nq;
+    };
+    auto begin_row = [&](int g) {
+      kj[g] = s_key[(q[g] * kChunkWaves + wave) * kWave + lane];
+      const uint32_t h = (uint32_t)murmurhash64((uint64_t)kj[g]) & p.mask;
+      cur[g] = h;  // LP: home slot; chain: bucket until its CSR range is loaded
+      r0[g] = 0;
+      mm[g] = 0;
+      live |= 1u << g;
+      if (KIND == CCJ_TABLE_CHAIN) start |= 1u << g;
     };
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      j[g] = next_active(g, g);
-      nj_next[g] = j[g] < nj ? next_active(j[g] + G, g) : nj;
       cur[g] = r0[g] = lim[g] = mm[g] = 0;
-      kj[g] = nk[g] = 0;
-      if (j[g] < nj) kj[g] = p.keys[base + phys_row(p, base, j[g] * kWave + lane)];
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      if (j[g] < nj) {
-        live |= 1u << g;
-        const uint32_t h = (uint32_t)murmurhash64((uint64_t)kj[g]) & p.mask;
-        if (KIND == CCJ_TABLE_LP) cur[g] = h;
-        else {
-          cur[g] = h;  // bucket index until the CSR range is loaded
-          start |= 1u << g;
-        }
-      }
+      kj[g] = 0;
+      q[g] = next_active(g);
+      if (q[g] < nq) begin_row(g);
     }
     while (__ballot(live != 0u) != 0ull) {
       longlong2 v[G][kWin / 2];
@@ -209,11 +207,7 @@ __global__ __launch_bounds__(kWave) void probe_chunks(ProbeParams p) {
           } else {
             const longlong2 *w = reinterpret_cast<const longlong2 *>(p.table + (cur[g] & ~(uint32_t)(kWin - 1)));
 #pragma unroll
-            for (int q = 0; q < kWin / 2; ++q) v[g][q] = w[q];
-          }
-          if (!((nk_ok >> g) & 1u) && nj_next[g] < nj) {
-            nk[g] = p.keys[base + phys_row(p, base, nj_next[g] * kWave + lane)];
-            nk_ok |= 1u << g;
+            for (int t = 0; t < kWin / 2; ++t) v[g][t] = w[t];
           }
         }
       }
@@ -231,11 +225,11 @@ __global__ __launch_bounds__(kWave) void probe_chunks(ProbeParams p) {
             const uint32_t off = cur[g] - blk;
             bool go = true;
 #pragma unroll
-            for (int q = 0; q < kWin; ++q) {
-              const int64_t val = (q & 1) ? v[g][q >> 1].y : v[g][q >> 1].x;
-              if (go && (uint32_t)q >= off) {
-                const uint32_t r = r0[g] + (uint32_t)q - off;
-                const bool stop = KIND == CCJ_TABLE_LP ? (val == -1) : (blk + (uint32_t)q == lim[g]);
+            for (int t = 0; t < kWin; ++t) {
+              const int64_t val = (t & 1) ? v[g][t >> 1].y : v[g][t >> 1].x;
+              if (go && (uint32_t)t >= off) {
+                const uint32_t r = r0[g] + (uint32_t)t - off;
+                const bool stop = KIND == CCJ_TABLE_LP ? (val == -1) : (blk + (uint32_t)t == lim[g]);
                 if (stop) {
                   go = false;
                   lane_rounds = r > lane_rounds ? r : lane_rounds;
@@ -258,34 +252,46 @@ __global__ __launch_bounds__(kWave) void probe_chunks(ProbeParams p) {
             done = !go;
           }
           if (done) {
-            s_mm[j[g] * kWave + lane] = mm[g];
-            j[g] = nj_next[g];
-            if (j[g] < nj) {
-              nj_next[g] = next_active(j[g] + G, g);
-              kj[g] = nk[g];
-              nk_ok &= ~(1u << g);
-              mm[g] = 0;
-              r0[g] = 0;
-              const uint32_t h = (uint32_t)murmurhash64((uint64_t)kj[g]) & p.mask;
-              cur[g] = h;
-              if (KIND == CCJ_TABLE_CHAIN) start |= 1u << g;
-            } else {
-              live &= ~(1u << g);
-            }
+            s_mm[(q[g] * kChunkWaves + wave) * kWave + lane] = mm[g];
+            live &= ~(1u << g);
+            q[g] = next_active(q[g] + G);
+            if (q[g] < nq) begin_row(g);
           }
         }
       }
     }
   }
 
+  // Block-wide round count and long-run flag.
+  {
+    const uint32_t wr = wave_max(lane_rounds);
+    const bool wl = __ballot(long_run) != 0ull;
+    if (lane == 0) {
+      s_red[wave] = wr;
+      s_red[kChunkWaves + wave] = wl ? 1u : 0u;
+    }
+  }
+  __syncthreads();
+  uint32_t rounds = 0, any_long = 0;
+#pragma unroll
+  for (int w = 0; w < kChunkWaves; ++w) {
+    rounds = s_red[w] > rounds ? s_red[w] : rounds;
+    any_long |= s_red[kChunkWaves + w];
+  }
+
   uint64_t total = 0;
-  uint32_t rounds = 0;
-  if (__ballot(long_run) != 0ull) {
-    rounds_generic<KIND>(p, c, base, nj, act, flags, total, rounds);
+  if (any_long) {
+    if (wave == 0) {
+      uint32_t act_all = 0;
+      for (uint32_t j = 0; j < nj; ++j) {
+        const uint32_t i = j * kWave + lane;
+        if (i < count && phys_row(p, base, i) < phys) act_all |= 1u << j;
+      }
+      rounds_generic<KIND>(p, c, base, nj, act_all, s_key, flags, total, rounds);
+    }
   } else {
-    rounds = wave_max(lane_rounds);
-    // Count: matches per (round r, row group j).
-    for (uint32_t j = 0; j < nj; ++j) {
+    // Count: matches per (round r, row group j); wave w takes the row groups it owns.
+    for (uint32_t j = wave; j < nj; j += kChunkWaves) {
       const uint32_t m = s_mm[j * kWave + lane];
       for (uint32_t any = wave_or(m); any != 0u; any &= any - 1u) {
         const uint32_t r = (uint32_t)__builtin_ctz(any);
@@ -293,13 +299,14 @@ __global__ __launch_bounds__(kWave) void probe_chunks(ProbeParams p) {
         if (lane == 0) s_off[r * 32 + j] = n;
       }
     }
-    // Scan: exclusive prefix over (r, j) in round-major order, 16 entries per lane.
-    {
+    __syncthreads();
+    // Scan: exclusive prefix over (r, j) in round-major order, 16 entries per lane of wave 0.
+    if (wave == 0) {
       uint32_t loc[16], sum = 0;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        loc[q] = s_off[lane * 16 + q];
-        sum += loc[q];
+      for (int t = 0; t < 16; ++t) {
+        loc[t] = s_off[lane * 16 + t];
+        sum += loc[t];
       }
       uint32_t incl = sum;
 #pragma unroll
@@ -309,15 +316,17 @@ __global__ __launch_bounds__(kWave) void probe_chunks(ProbeParams p) {
       }
       uint32_t run = incl - sum;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        s_off[lane * 16 + q] = run;
-        run += loc[q];
+      for (int t = 0; t < 16; ++t) {
+        s_off[lane * 16 + t] = run;
+        run += loc[t];
       }
-      total = (uint64_t)(uint32_t)__shfl((int)incl, kWave - 1);
+      if (lane == kWave - 1) s_red[2 * kChunkWaves] = incl;
     }
+    __syncthreads();
+    total = s_red[2 * kChunkWaves];
     // Per-round counts (Next return values): differences of the round starts.
     if (p.out_round_counts) {
-      for (uint32_t r = lane; r < rounds; r += kWave) {
+      for (uint32_t r = tid; r < rounds; r += kBlock) {
         const uint32_t a = s_off[r * 32], b = r + 1 < rounds ? s_off[(r + 1) * 32] : (uint32_t)total;
         if (r < p.max_rounds) p.out_round_counts[c * p.max_rounds + r] = b - a;
       }
@@ -325,23 +334,17 @@ __global__ __launch_bounds__(kWave) void probe_chunks(ProbeParams p) {
     }
     // Emit.
     const uint64_t obase = c * p.cap;
-    for (uint32_t jb = 0; jb < nj; jb += kEmitRows) {
+    for (uint32_t jb = wave; jb < nj; jb += kChunkWaves * kEmitRows) {
       uint32_t m[kEmitRows], rr[kEmitRows];
-      int64_t pay[kEmitRows];
 #pragma unroll
       for (int g = 0; g < kEmitRows; ++g) {
-        const uint32_t j = jb + g;
+        const uint32_t j = jb + g * kChunkWaves;
         m[g] = j < nj ? s_mm[j * kWave + lane] : 0u;
-        rr[g] = 0;
-        pay[g] = 0;
-        if (m[g]) {
-          rr[g] = phys_row(p, base, j * kWave + lane);
-          if (p.out_payload) pay[g] = p.keys[base + rr[g]];  // matched table value == probe key
-        }
+        rr[g] = m[g] ? phys_row(p, base, j * kWave + lane) : 0u;
       }
 #pragma unroll
       for (int g = 0; g < kEmitRows; ++g) {
-        const uint32_t j = jb + g;
+        const uint32_t j = jb + g * kChunkWaves;
         for (uint32_t any = wave_or(m[g]); any != 0u; any &= any - 1u) {
           const uint32_t r = (uint32_t)__builtin_ctz(any);
           const bool bit = (m[g] >> r) & 1u;
@@ -350,7 +353,7 @@ __global__ __launch_bounds__(kWave) void probe_chunks(ProbeParams p) {
             const uint64_t o = (uint64_t)s_off[r * 32 + j] + lane_prefix(mb);
             if (o < p.cap) {
               p.out_sel[obase + o] = rr[g];
-              if (p.out_payload) p.out_payload[obase + o] = pay[g];
+              if (p.out_payload) p.out_payload[obase + o] = s_key[j * kWave + lane];  // == probe key
             }
           }
         }
@@ -359,7 +362,7 @@ __global__ __launch_bounds__(kWave) void probe_chunks(ProbeParams p) {
   }
 
   if (total > p.cap) flags |= CCJ_FLAG_CAP_OVERFLOW;
-  if (lane == 0) {
+  if (tid == 0) {
     p.out_count[c] = (uint32_t)(total < p.cap ? total : p.cap);
     if (p.out_rounds) p.out_rounds[c] = rounds;
   }
@@ -376,7 +379,7 @@ hipError_t launch_kind(const ProbeParams &p, hipStream_t s) {
     const char *e = getenv("CCJ_WALK_ROWS");
     return e ? atoi(e) : kWalkRows;
   }();
-  const dim3 g((unsigned)p.n_chunks), b(kWave);
+  const dim3 g((unsigned)p.n_chunks), b(kBlock);
   if (walk <= 2) hipLaunchKernelGGL((probe_chunks<KIND, 2>), g, b, 0, s, p);
   else if (walk <= 4) hipLaunchKernelGGL((probe_chunks<KIND, 4>), g, b, 0, s, p);
   else if (walk <= 6) hipLaunchKernelGGL((probe_chunks<KIND, 6>), g, b, 0, s, p);
