@@ -40,7 +40,9 @@ class ProbeArgs(C.Structure):
     _fields_ = [("keys", C.c_void_p), ("sel", C.c_void_p), ("counts", C.c_void_p), ("n_rows", C.c_uint64),
                 ("chunk", C.c_uint32), ("max_rounds", C.c_uint32), ("cap", C.c_uint64),
                 ("out_count", C.c_void_p), ("out_sel", C.c_void_p), ("out_payload", C.c_void_p),
-                ("out_rounds", C.c_void_p), ("out_round_counts", C.c_void_p), ("status", C.c_void_p)]
+                ("out_rounds", C.c_void_p), ("out_round_counts", C.c_void_p), ("status", C.c_void_p),
+                ("out_pos", C.c_void_p), ("n_payload_cols", C.c_uint32), ("reserved2", C.c_uint32),
+                ("out_payload_cols", C.c_void_p * 8)]
 
 
 class CompactArgs(C.Structure):
@@ -57,7 +59,7 @@ EXPORTS = ["ccj_last_error", "ccj_abi_version", "ccj_device_init", "ccj_table_bu
            "ccj_table_build_from_host", "ccj_table_build_on_device", "ccj_table_get_info", "ccj_table_free",
            "ccj_probe", "ccj_gen_uniform_keys", "ccj_probe_cost", "ccj_result_checksum",
            "ccj_compact_workspace_size", "ccj_compact", "ccj_partition_workspace_size", "ccj_partition_by_owner",
-           "ccj_result_checksum_mapped", "ccj_gen_reference_keys"]
+           "ccj_result_checksum_mapped", "ccj_gen_reference_keys", "ccj_table_set_payload"]
 
 
 def build(force: bool = False) -> str:
@@ -82,6 +84,7 @@ def lib():
         L.ccj_table_build_on_device.argtypes = [i32, vp, u64, vp, C.POINTER(vp)]
         L.ccj_table_get_info.argtypes = [vp, C.POINTER(TableInfo)]
         L.ccj_table_free.argtypes = [vp]
+        L.ccj_table_set_payload.argtypes = [vp, vp, C.c_uint32, vp]
         L.ccj_probe.argtypes = [vp, C.POINTER(ProbeArgs), vp]
         L.ccj_gen_uniform_keys.argtypes = [vp, u64, u64, u64, u64, vp]
         L.ccj_gen_reference_keys.argtypes = [vp, u64, u64, u64, u64, vp]
@@ -196,6 +199,11 @@ class Table:
         except Exception:
             pass
 
+    def set_payload(self, d_payload, n_cols: int, stream=None):
+        """Attach build payload columns: d_payload row-major int64 [n_keys, n_cols] in build order."""
+        check(lib().ccj_table_set_payload(self._h, _ptr(d_payload), n_cols, _stream(stream)), "ccj_table_set_payload")
+        self.n_payload_cols = n_cols
+
     def probe_cost(self, keys, stream=None):
         """(table words examined, matches) over a key column — roofline accounting."""
         import torch
@@ -206,7 +214,7 @@ class Table:
         return a[0], a[1]
 
     def alloc_outputs(self, n_rows: int, chunk: int, cap: int | None = None, rounds: bool = True,
-                      payload: bool = True, device=None):
+                      payload: bool = True, device=None, pos: bool = False, payload_cols: int = 0):
         import torch
         dev = device or torch.device("cuda", torch.cuda.current_device())
         n_chunks = (n_rows + chunk - 1) // chunk
@@ -220,6 +228,8 @@ class Table:
             rounds=torch.empty(n_chunks, dtype=torch.int32, device=dev) if rounds else None,
             round_counts=torch.zeros(n_chunks * mr, dtype=torch.int32, device=dev) if rounds else None,
             status=torch.zeros(1, dtype=torch.int32, device=dev),
+            pos=torch.empty(n_chunks * cap, dtype=torch.int32, device=dev) if pos else None,
+            payload_cols=[torch.empty(n_chunks * cap, dtype=torch.int64, device=dev) for _ in range(payload_cols)],
         )
         return o
 
@@ -235,6 +245,12 @@ class Table:
                       out_rounds=_ptr(out["rounds"]).value if out["rounds"] is not None else None,
                       out_round_counts=_ptr(out["round_counts"]).value if out["round_counts"] is not None else None,
                       status=_ptr(out["status"]).value)
+        if out.get("pos") is not None:
+            a.out_pos = out["pos"].data_ptr()
+        cols = out.get("payload_cols") or []
+        a.n_payload_cols = len(cols)
+        for i, col in enumerate(cols):
+            a.out_payload_cols[i] = col.data_ptr()
         check(lib().ccj_probe(self._h, C.byref(a), _stream(stream)), "ccj_probe")
         return out
 

@@ -107,11 +107,13 @@ int build_lp_host(const int64_t *keys, uint64_t n, ccj_table **out) {
   const uint64_t size = lp_num_slots(n);
   if (size > (1ull << 32)) return fail(CCJ_ERR_LIMIT, "LP table larger than 2^32 slots");
   std::vector<int64_t> slots(size, -1);
+  std::vector<uint32_t> rows(size < 4 ? 4 : size, ccj::kNoRow);
   const uint64_t mask = size - 1;
   for (uint64_t i = 0; i < n; ++i) {  // linear_probing_ht.cpp:28-36
     uint64_t s = ccj::murmurhash64((uint64_t)keys[i]) & mask;
     while (slots[s] != -1) s = (s + 1) & mask;
     slots[s] = keys[i];
+    if (keys[i] != -1) rows[s] = (uint32_t)i;
   }
   std::unique_ptr<ccj_table> t(new ccj_table());
   t->info.kind = CCJ_TABLE_LP;
@@ -125,6 +127,13 @@ int build_lp_host(const int64_t *keys, uint64_t n, ccj_table **out) {
   int rc = upload(&d, slots.data(), slots.size() * sizeof(int64_t), "LP slots");
   if (rc) return rc;
   t->d_table = (int64_t *)d;
+  t->positions = slots.size();
+  rc = upload(&d, rows.data(), rows.size() * sizeof(uint32_t), "LP slot rows");
+  if (rc) {
+    (void)hipFree(t->d_table);
+    return rc;
+  }
+  t->d_row = (uint32_t *)d;
   t->info.d_table = t->d_table;
   (void)hipGetDevice(&t->device);
   *out = t.release();
@@ -148,9 +157,14 @@ int build_chain_host(const int64_t *keys, uint64_t n, ccj_table **out) {
     off[b + 1] += off[b];
   }
   std::vector<int64_t> chain(n);
+  std::vector<uint32_t> rows;
   {
     std::vector<uint32_t> fill(off.begin(), off.end() - 1);
-    for (uint64_t i = 0; i < n; ++i) chain[fill[bucket[i]]++] = keys[i];
+    rows.assign(((n + 3) / 4) * 4 + (n == 0 ? 4 : 0), ccj::kNoRow);
+    for (uint64_t i = 0; i < n; ++i) {
+      rows[fill[bucket[i]]] = (uint32_t)i;
+      chain[fill[bucket[i]]++] = keys[i];
+    }
   }
   uint64_t dup = n ? 1 : 0;
   for (uint64_t b = 0; b < size; ++b) {
@@ -183,6 +197,14 @@ int build_chain_host(const int64_t *keys, uint64_t n, ccj_table **out) {
     return rc;
   }
   t->d_off = (uint32_t *)d;
+  t->positions = chain.size();
+  rc = upload(&d, rows.data(), rows.size() * sizeof(uint32_t), "chain rows");
+  if (rc) {
+    (void)hipFree(t->d_table);
+    (void)hipFree(t->d_off);
+    return rc;
+  }
+  t->d_row = (uint32_t *)d;
   t->info.d_table = t->d_table;
   t->info.d_bucket_off = t->d_off;
   (void)hipGetDevice(&t->device);
@@ -198,9 +220,19 @@ int build_lp_device(const int64_t *d_keys, uint64_t n, hipStream_t s, uint64_t k
   const uint64_t alloc = size < 4 ? 4 : size;  // aligned 4-slot windows
   if (hipMalloc(&d, alloc * sizeof(int64_t)) != hipSuccess) return fail(CCJ_ERR_OOM, "LP slots: hipMalloc failed");
   t->d_table = (int64_t *)d;
-  auto cleanup = [&]() { (void)hipFree(t->d_table); };
+  auto cleanup = [&]() {
+    (void)hipFree(t->d_table);
+    if (t->d_row) (void)hipFree(t->d_row);
+  };
+  t->positions = alloc;
+  if (hipMalloc(&d, alloc * sizeof(uint32_t)) != hipSuccess) {
+    cleanup();
+    return fail(CCJ_ERR_OOM, "LP slot rows: hipMalloc failed");
+  }
+  t->d_row = (uint32_t *)d;
   hipError_t e = ccj::launch_fill(t->d_table, alloc, -1, s);
-  if (e == hipSuccess) e = ccj::launch_lp_insert(d_keys, n, t->d_table, (uint32_t)(size - 1), s);
+  if (e == hipSuccess) e = hipMemsetAsync(t->d_row, 0xFF, alloc * sizeof(uint32_t), s);
+  if (e == hipSuccess) e = ccj::launch_lp_insert(d_keys, n, t->d_table, t->d_row, (uint32_t)(size - 1), s);
   const uint64_t n_seg = (size + ccj::kRunSegment - 1) / ccj::kRunSegment;
   uint32_t *d_stats = nullptr;
   if (e == hipSuccess) e = hipMalloc(&d_stats, n_seg * 4 * sizeof(uint32_t));
@@ -310,10 +342,32 @@ int ccj_table_get_info(const ccj_table *t, ccj_table_info *info) {
   return CCJ_OK;
 }
 
+int ccj_table_set_payload(ccj_table *t, const int64_t *d_payload, uint32_t n_cols, ccj_stream stream) {
+  if (!t || n_cols == 0 || n_cols > CCJ_MAX_PAYLOAD_COLS || (!d_payload && t->info.n_keys))
+    return fail(CCJ_ERR_INVALID, "ccj_table_set_payload: bad argument");
+  if (!t->d_row) return fail(CCJ_ERR_INVALID, "ccj_table_set_payload: table has no row map");
+  void *d = nullptr;
+  if (hipMalloc(&d, t->positions * n_cols * sizeof(int64_t)) != hipSuccess)
+    return fail(CCJ_ERR_OOM, "payload: hipMalloc failed");
+  hipError_t e = ccj::launch_scatter_payload(d_payload, n_cols, t->d_row, t->positions, (int64_t *)d,
+                                             (hipStream_t)stream);
+  if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+  if (e != hipSuccess) {
+    (void)hipFree(d);
+    return hip_fail(e, "payload scatter");
+  }
+  if (t->d_pay) (void)hipFree(t->d_pay);
+  t->d_pay = (int64_t *)d;
+  t->n_pay = n_cols;
+  return CCJ_OK;
+}
+
 int ccj_table_free(ccj_table *t) {
   if (!t) return CCJ_OK;
   if (t->d_table) (void)hipFree(t->d_table);
   if (t->d_off) (void)hipFree(t->d_off);
+  if (t->d_row) (void)hipFree(t->d_row);
+  if (t->d_pay) (void)hipFree(t->d_pay);
   delete t;
   return CCJ_OK;
 }
@@ -342,6 +396,15 @@ int ccj_probe(const ccj_table *t, const ccj_probe_args *a, ccj_stream stream) {
   p.out_rounds = a->out_rounds;
   p.out_round_counts = a->out_round_counts;
   p.status = a->status;
+  p.out_pos = a->out_pos;
+  if (a->n_payload_cols > t->n_pay) return fail(CCJ_ERR_INVALID, "ccj_probe: table has fewer payload columns");
+  p.pay = t->d_pay;
+  p.n_pay = a->n_payload_cols;
+  p.pay_stride = t->n_pay;
+  for (uint32_t c = 0; c < a->n_payload_cols; ++c) {
+    if (!a->out_payload_cols[c]) return fail(CCJ_ERR_INVALID, "ccj_probe: null payload column");
+    p.out_cols[c] = a->out_payload_cols[c];
+  }
   HIP_TRY(ccj::launch_probe(t->info.kind, p, (hipStream_t)stream), "probe launch");
   return CCJ_OK;
 }

@@ -12,6 +12,10 @@ struct ccj_table {
   ccj_table_info info;
   int64_t *d_table = nullptr;   // LP slots / chain keys
   uint32_t *d_off = nullptr;    // chain CSR offsets (size + 1)
+  uint32_t *d_row = nullptr;    // table position -> build tuple index (LP: kNoRow for empty slots)
+  uint64_t positions = 0;       // allocated positions (LP slots / chain keys, padded)
+  int64_t *d_pay = nullptr;     // position-major payload rows [positions][n_pay]
+  uint32_t n_pay = 0;
   int device = 0;
 };
 
@@ -50,14 +54,23 @@ struct ProbeParams {
   uint32_t *out_rounds;
   uint32_t *out_round_counts;
   uint32_t *status;
+  uint32_t *out_pos;
+  const int64_t *pay;  // position-major payload rows
+  uint32_t n_pay;      // payload columns gathered (<= CCJ_MAX_PAYLOAD_COLS)
+  uint32_t pay_stride; // payload columns stored per position
+  int64_t *out_cols[CCJ_MAX_PAYLOAD_COLS];
 };
+constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 
 // Launchers (ccj_kernels.hip).  Return hipError_t of the launch.
 hipError_t launch_probe(int kind, const ProbeParams &p, hipStream_t s);
 hipError_t launch_gen_reference_keys(int64_t *out, uint64_t first, uint64_t n, uint64_t n_total, uint64_t cf,
                                      hipStream_t s);
 hipError_t launch_fill(int64_t *p, uint64_t n, int64_t v, hipStream_t s);
-hipError_t launch_lp_insert(const int64_t *keys, uint64_t n, int64_t *slots, uint32_t mask, hipStream_t s);
+hipError_t launch_lp_insert(const int64_t *keys, uint64_t n, int64_t *slots, uint32_t *slot_row, uint32_t mask,
+                            hipStream_t s);
+hipError_t launch_scatter_payload(const int64_t *src, uint32_t n_cols, const uint32_t *row, uint64_t positions,
+                                  int64_t *dst, hipStream_t s);
 // Per-segment run statistics of an LP slot array (segment = 4096 slots): 4 x uint32 per segment:
 // {leading run, trailing run, longest run, all occupied}.
 hipError_t launch_lp_runs(const int64_t *slots, uint64_t n_slots, uint32_t *seg_stats, hipStream_t s);

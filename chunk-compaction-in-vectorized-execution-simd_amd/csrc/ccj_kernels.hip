@@ -22,6 +22,20 @@ __device__ __forceinline__ uint32_t lane_prefix(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// Table position of row key k's candidate in round r (LP: home + r; chain: chain start + r) and
+// the wide-payload gather (C5) for a match written at output slot o.
+template <int KIND>
+__device__ __forceinline__ void emit_extra(const ProbeParams &p, uint64_t obase, uint64_t o, int64_t k, uint32_t r) {
+  if (!p.out_pos && p.n_pay == 0) return;
+  const uint32_t h = (uint32_t)murmurhash64((uint64_t)k) & p.mask;
+  const uint32_t pos = KIND == CCJ_TABLE_LP ? ((h + r) & p.mask) : p.off[h] + r;
+  if (p.out_pos) p.out_pos[obase + o] = pos;
+  if (p.n_pay) {
+    const int64_t *row = p.pay + (uint64_t)pos * p.pay_stride;
+    for (uint32_t c = 0; c < p.n_pay; ++c) p.out_cols[c][obase + o] = row[c];
+  }
+}
+
 __device__ __forceinline__ uint32_t wave_or(uint32_t x) {
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) x |= (uint32_t)__shfl_xor((int)x, d);
@@ -90,6 +104,7 @@ __device__ void rounds_generic(const ProbeParams &p, uint64_t c, uint64_t base, 
         if (o < p.cap) {
           p.out_sel[obase + o] = phys_row(p, base, j * kWave + lane);
           if (p.out_payload) p.out_payload[obase + o] = s_key[j * kWave + lane];
+          emit_extra<KIND>(p, obase, o, s_key[j * kWave + lane], round);
         }
       }
       const uint32_t n = (uint32_t)__popcll(mb);
@@ -352,8 +367,10 @@ __global__ __launch_bounds__(kBlock) void probe_chunks(ProbeParams p) {
           if (bit) {
             const uint64_t o = (uint64_t)s_off[r * 32 + j] + lane_prefix(mb);
             if (o < p.cap) {
+              const int64_t k = s_key[j * kWave + lane];
               p.out_sel[obase + o] = rr[g];
-              if (p.out_payload) p.out_payload[obase + o] = s_key[j * kWave + lane];  // == probe key
+              if (p.out_payload) p.out_payload[obase + o] = k;  // matched table value == probe key
+              emit_extra<KIND>(p, obase, o, k, r);
             }
           }
         }
@@ -400,7 +417,7 @@ __global__ void fill_i64(int64_t *p, uint64_t n, int64_t v) {
 
 // Parallel linear-probing insert (CCJ_LAYOUT_DEVICE): CAS into the first empty slot at or after
 // h(k) & mask.  Occupied-slot set and per-cluster key sets equal the sequential build's.
-__global__ void lp_insert(const int64_t *keys, uint64_t n, int64_t *slots, uint32_t mask) {
+__global__ void lp_insert(const int64_t *keys, uint64_t n, int64_t *slots, uint32_t *slot_row, uint32_t mask) {
   for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
     const int64_t k = keys[t];
     if (k == -1) continue;  // the reference "stores" -1 into an empty slot: a no-op
@@ -411,6 +428,18 @@ __global__ void lp_insert(const int64_t *keys, uint64_t n, int64_t *slots, uint3
       if (old == ~0ull) break;
       s = (s + 1u) & mask;
     }
+    if (slot_row) slot_row[s] = (uint32_t)t;  // the slot now owned by build tuple t
+  }
+}
+
+// Re-lays build payload rows (build order) out by table position: dst[pos][c] = src[row(pos)][c].
+__global__ void scatter_payload(const int64_t *src, uint32_t n_cols, const uint32_t *row, uint64_t positions,
+                                int64_t *dst) {
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < positions * n_cols;
+       t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t pos = t / n_cols, c = t - pos * n_cols;
+    const uint32_t r = row[pos];
+    dst[t] = r == kNoRow ? 0 : src[(uint64_t)r * n_cols + c];
   }
 }
 
@@ -563,9 +592,18 @@ hipError_t launch_fill(int64_t *p, uint64_t n, int64_t v, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_lp_insert(const int64_t *keys, uint64_t n, int64_t *slots, uint32_t mask, hipStream_t s) {
+hipError_t launch_lp_insert(const int64_t *keys, uint64_t n, int64_t *slots, uint32_t *slot_row, uint32_t mask,
+                            hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(lp_insert, dim3(grid_for(n, 256)), dim3(256), 0, s, keys, n, slots, mask);
+  hipLaunchKernelGGL(lp_insert, dim3(grid_for(n, 256)), dim3(256), 0, s, keys, n, slots, slot_row, mask);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter_payload(const int64_t *src, uint32_t n_cols, const uint32_t *row, uint64_t positions,
+                                  int64_t *dst, hipStream_t s) {
+  if (positions == 0 || n_cols == 0) return hipSuccess;
+  hipLaunchKernelGGL(scatter_payload, dim3(grid_for(positions * n_cols, 256)), dim3(256), 0, s, src, n_cols, row,
+                     positions, dst);
   return hipGetLastError();
 }
 

@@ -59,6 +59,7 @@ enum ccj_layout {
 };
 
 typedef void *ccj_stream; /* hipStream_t; NULL = the default stream */
+#define CCJ_MAX_PAYLOAD_COLS 8
 typedef struct ccj_table ccj_table;
 
 typedef struct ccj_table_info {
@@ -93,6 +94,12 @@ int ccj_table_build_from_host(int kind, const int64_t *h_keys, uint64_t n, ccj_t
 int ccj_table_build_on_device(int kind, const int64_t *d_keys, uint64_t n, ccj_stream stream,
                               ccj_table **out);
 int ccj_table_get_info(const ccj_table *table, ccj_table_info *info);
+/* Attaches build-side payload columns (C5): d_payload is row-major int64
+ * [n_keys][n_cols] in build-tuple order (the order keys were given to the builder).  The table
+ * re-lays them out by table position (slot / chain index) so a match gathers one contiguous row.
+ * The reference discards its build payload (linear_probing_ht.cpp:20); this is the wide-payload
+ * extension the BASELINE config asks for. */
+int ccj_table_set_payload(ccj_table *table, const int64_t *d_payload, uint32_t n_cols, ccj_stream stream);
 int ccj_table_free(ccj_table *table);
 
 /* ---- probe -------------------------------------------------------------------------------- */
@@ -123,6 +130,14 @@ typedef struct ccj_probe_args {
   uint32_t *out_rounds;      /* device uint32[n_chunks] or NULL */
   uint32_t *out_round_counts;/* device uint32[n_chunks*max_rounds] or NULL */
   uint32_t *status;          /* device word, OR-ed with ccj_flag bits, or NULL */
+  /* Matched table position (LP slot / chain index), the reference's iterator at the match
+   * (GatherResult, chaining_ht.cpp:126-136; slot_ids_, linear_probing_ht.cpp:90-94). Or NULL. */
+  uint32_t *out_pos;
+  /* Wide payload (C5): the first n_payload_cols of the table's payload columns
+   * (ccj_table_set_payload) are gathered for every match: out_payload_cols[c][c*cap + j]. */
+  uint32_t n_payload_cols;
+  uint32_t reserved2;
+  int64_t *out_payload_cols[CCJ_MAX_PAYLOAD_COLS];
 } ccj_probe_args;
 
 int ccj_probe(const ccj_table *table, const ccj_probe_args *args, ccj_stream stream);

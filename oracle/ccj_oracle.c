@@ -55,12 +55,20 @@ uint64_t ccj_o_lp_num_slots(uint64_t n) {
 /* linear_probing_ht.cpp:7,28-36 — fill with -1, sequential insert at h(k) & mask, +1 with wrap.
  * Inserting -1 lands in an empty slot and leaves it empty, exactly as the reference does. */
 void ccj_o_lp_build(const int64_t *keys, uint64_t n, int64_t *slots, uint64_t n_slots) {
+  ccj_o_lp_build_rows(keys, n, slots, NULL, n_slots);
+}
+
+/* Same, also recording which build tuple owns each slot (rows[s], UINT32_MAX when empty). */
+void ccj_o_lp_build_rows(const int64_t *keys, uint64_t n, int64_t *slots, uint32_t *rows, uint64_t n_slots) {
   uint64_t mask = n_slots - 1;
   for (uint64_t i = 0; i < n_slots; ++i) slots[i] = -1;
+  if (rows)
+    for (uint64_t i = 0; i < n_slots; ++i) rows[i] = 0xFFFFFFFFu;
   for (uint64_t i = 0; i < n; ++i) {
     uint64_t s = ccj_o_murmurhash64((uint64_t)keys[i]) & mask;
     while (slots[s] != -1) s = (s + 1) & mask;
     slots[s] = keys[i];
+    if (rows && keys[i] != -1) rows[s] = (uint32_t)i;
   }
 }
 
@@ -75,13 +83,22 @@ uint64_t ccj_o_chain_num_buckets(uint64_t n) {
  * bucket; bucket b's chain is chain_keys[bucket_off[b] .. bucket_off[b+1]). */
 void ccj_o_chain_build(const int64_t *keys, uint64_t n, uint64_t n_buckets, uint64_t *bucket_off,
                        int64_t *chain_keys) {
+  ccj_o_chain_build_rows(keys, n, n_buckets, bucket_off, chain_keys, NULL);
+}
+
+void ccj_o_chain_build_rows(const int64_t *keys, uint64_t n, uint64_t n_buckets, uint64_t *bucket_off,
+                            int64_t *chain_keys, uint32_t *rows) {
   uint64_t mask = n_buckets - 1;
   memset(bucket_off, 0, (n_buckets + 1) * sizeof(uint64_t));
   for (uint64_t i = 0; i < n; ++i) bucket_off[(ccj_o_murmurhash64((uint64_t)keys[i]) & mask) + 1]++;
   for (uint64_t b = 0; b < n_buckets; ++b) bucket_off[b + 1] += bucket_off[b];
   uint64_t *fill = (uint64_t *)malloc(n_buckets * sizeof(uint64_t));
   memcpy(fill, bucket_off, n_buckets * sizeof(uint64_t));
-  for (uint64_t i = 0; i < n; ++i) chain_keys[fill[ccj_o_murmurhash64((uint64_t)keys[i]) & mask]++] = keys[i];
+  for (uint64_t i = 0; i < n; ++i) {
+    uint64_t q = fill[ccj_o_murmurhash64((uint64_t)keys[i]) & mask]++;
+    chain_keys[q] = keys[i];
+    if (rows) rows[q] = (uint32_t)i;
+  }
   free(fill);
 }
 
@@ -97,7 +114,7 @@ static int probe_chunk(int kind, const int64_t *table, const uint64_t *bucket_of
                        const int64_t *col, const uint32_t *sel, uint32_t count, uint64_t cap,
                        uint32_t max_rounds, uint64_t *pos, uint64_t *end, uint32_t *act,
                        uint32_t *o_sel, int64_t *o_pay, uint32_t *o_count, uint32_t *o_rounds,
-                       uint32_t *o_rc) {
+                       uint32_t *o_rc, uint32_t *o_pos) {
   uint64_t mask = size - 1;
   uint32_t n_act = 0;
   for (uint32_t i = 0; i < count; ++i) {
@@ -126,6 +143,7 @@ static int probe_chunk(int kind, const int64_t *table, const uint64_t *bucket_of
         if (total >= cap) return -1;
         o_sel[total] = r;
         o_pay[total] = cand;
+        if (o_pos) o_pos[total] = (uint32_t)pos[idx];
         ++total;
         ++rc;
       }
@@ -158,7 +176,7 @@ int ccj_o_probe(int kind, const int64_t *table, const uint64_t *bucket_off, uint
                 const int64_t *keys, const uint32_t *sel, const uint32_t *counts, uint64_t n_rows,
                 uint32_t chunk, uint64_t cap, uint32_t max_rounds, uint32_t *out_count,
                 uint32_t *out_sel, int64_t *out_payload, uint32_t *out_rounds,
-                uint32_t *out_round_counts, int threads) {
+                uint32_t *out_round_counts, int threads, uint32_t *out_pos) {
   uint64_t n_chunks = (n_rows + chunk - 1) / chunk;
   int err = 0;
   if (threads <= 0) threads = omp_get_max_threads();
@@ -175,7 +193,8 @@ int ccj_o_probe(int kind, const int64_t *table, const uint64_t *bucket_off, uint
       uint32_t rounds = 0;
       int e = probe_chunk(kind, table, bucket_off, size, keys + base, sel ? sel + base : NULL, count, cap,
                           max_rounds, pos, end, act, out_sel + c * cap, out_payload + c * cap, &out_count[c],
-                          &rounds, out_round_counts ? out_round_counts + c * (uint64_t)max_rounds : NULL);
+                          &rounds, out_round_counts ? out_round_counts + c * (uint64_t)max_rounds : NULL,
+                          out_pos ? out_pos + c * cap : NULL);
       if (out_rounds) out_rounds[c] = rounds;
       if (e) err = 1;
     }
@@ -205,7 +224,7 @@ uint64_t ccj_o_probe_totals(int kind, const int64_t *table, const uint64_t *buck
       uint32_t phys = (uint32_t)((n_rows - base) < chunk ? (n_rows - base) : chunk);
       uint32_t cnt = 0, rounds = 0;
       probe_chunk(kind, table, bucket_off, size, keys + base, NULL, phys, (uint64_t)chunk * 64, 0, pos, end,
-                  act, o_sel, o_pay, &cnt, &rounds, NULL);
+                  act, o_sel, o_pay, &cnt, &rounds, NULL, NULL);
       matches += cnt;
       for (uint32_t j = 0; j < cnt; ++j) l2 += ccj_l2_term(row_base + base + o_sel[j], o_pay[j]);
     }

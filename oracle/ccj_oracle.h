@@ -32,9 +32,12 @@ uint64_t ccj_o_ref_multiplicity(int64_t k, uint64_t n, uint64_t cf);
 
 uint64_t ccj_o_lp_num_slots(uint64_t n);
 void ccj_o_lp_build(const int64_t *keys, uint64_t n, int64_t *slots, uint64_t n_slots);
+void ccj_o_lp_build_rows(const int64_t *keys, uint64_t n, int64_t *slots, uint32_t *rows, uint64_t n_slots);
 uint64_t ccj_o_chain_num_buckets(uint64_t n);
 void ccj_o_chain_build(const int64_t *keys, uint64_t n, uint64_t n_buckets, uint64_t *bucket_off,
                        int64_t *chain_keys);
+void ccj_o_chain_build_rows(const int64_t *keys, uint64_t n, uint64_t n_buckets, uint64_t *bucket_off,
+                            int64_t *chain_keys, uint32_t *rows);
 
 /* kind 0 = linear probing (table = slots, size = n_slots), 1 = chaining (table = chain_keys,
  * bucket_off[n_buckets+1], size = n_buckets).  Returns 0, or -1 when an output bound
@@ -43,7 +46,7 @@ int ccj_o_probe(int kind, const int64_t *table, const uint64_t *bucket_off, uint
                 const int64_t *keys, const uint32_t *sel, const uint32_t *counts, uint64_t n_rows,
                 uint32_t chunk, uint64_t cap, uint32_t max_rounds, uint32_t *out_count,
                 uint32_t *out_sel, int64_t *out_payload, uint32_t *out_rounds,
-                uint32_t *out_round_counts, int threads);
+                uint32_t *out_round_counts, int threads, uint32_t *out_pos /* matched position or NULL */);
 
 /* Timed CPU baseline: probe n_rows keys chunk by chunk exactly as ccj_o_probe does, but keep only
  * the totals (matches, L2 checksum over global row ids).  Returns matches. */

@@ -41,12 +41,14 @@ def lib():
         L.ccj_o_lp_num_slots.restype = u64
         L.ccj_o_lp_num_slots.argtypes = [u64]
         L.ccj_o_lp_build.argtypes = [i64p, u64, i64p, u64]
+        L.ccj_o_lp_build_rows.argtypes = [i64p, u64, i64p, u32p, u64]
+        L.ccj_o_chain_build_rows.argtypes = [i64p, u64, u64, u64p, i64p, u32p]
         L.ccj_o_chain_num_buckets.restype = u64
         L.ccj_o_chain_num_buckets.argtypes = [u64]
         L.ccj_o_chain_build.argtypes = [i64p, u64, u64, u64p, i64p]
         L.ccj_o_probe.restype = C.c_int
         L.ccj_o_probe.argtypes = [C.c_int, i64p, u64p, u64, i64p, u32p, u32p, u64, C.c_uint32, u64,
-                                  C.c_uint32, u32p, u32p, i64p, u32p, u32p, C.c_int]
+                                  C.c_uint32, u32p, u32p, i64p, u32p, u32p, C.c_int, u32p]
         L.ccj_o_probe_totals.restype = u64
         L.ccj_o_probe_totals.argtypes = [C.c_int, i64p, u64p, u64, i64p, u64, C.c_uint32, u64, u64p, C.c_int]
         L.ccj_o_gen_uniform.argtypes = [u64, u64, u64, u64, i64p, C.c_int]
@@ -85,14 +87,17 @@ class Table:
         if kind == LP:
             self.size = L.ccj_o_lp_num_slots(len(keys))
             self.table = np.empty(self.size, dtype=np.int64)
-            L.ccj_o_lp_build(_p(keys, C.c_int64), len(keys), _p(self.table, C.c_int64), self.size)
+            self.rows = np.empty(self.size, dtype=np.uint32)  # slot -> build tuple (UINT32_MAX = empty)
+            L.ccj_o_lp_build_rows(_p(keys, C.c_int64), len(keys), _p(self.table, C.c_int64),
+                                  _p(self.rows, C.c_uint32), self.size)
             self.bucket_off = None
         else:
             self.size = L.ccj_o_chain_num_buckets(len(keys))
             self.bucket_off = np.empty(self.size + 1, dtype=np.uint64)
             self.table = np.empty(len(keys), dtype=np.int64)
-            L.ccj_o_chain_build(_p(keys, C.c_int64), len(keys), self.size, _p(self.bucket_off, C.c_uint64),
-                                _p(self.table, C.c_int64))
+            self.rows = np.empty(len(keys), dtype=np.uint32)  # chain index -> build tuple
+            L.ccj_o_chain_build_rows(_p(keys, C.c_int64), len(keys), self.size, _p(self.bucket_off, C.c_uint64),
+                                     _p(self.table, C.c_int64), _p(self.rows, C.c_uint32))
 
     def probe(self, keys, chunk, sel=None, counts=None, cap_factor=1, max_rounds=256, threads=0):
         """Returns dict(count, sel, payload, rounds, round_counts) per the ccj_oracle.h contract."""
@@ -106,6 +111,7 @@ class Table:
             payload=np.zeros(n_chunks * cap, np.int64),
             rounds=np.zeros(n_chunks, np.uint32),
             round_counts=np.zeros(n_chunks * max_rounds, np.uint32),
+            pos=np.zeros(n_chunks * cap, np.uint32),
         )
         if sel is not None:
             sel = np.ascontiguousarray(sel, dtype=np.uint32)
@@ -115,7 +121,7 @@ class Table:
                                _p(keys, C.c_int64), _p(sel, C.c_uint32), _p(counts, C.c_uint32), n_rows, chunk, cap,
                                max_rounds, _p(out["count"], C.c_uint32), _p(out["sel"], C.c_uint32),
                                _p(out["payload"], C.c_int64), _p(out["rounds"], C.c_uint32),
-                               _p(out["round_counts"], C.c_uint32), threads)
+                               _p(out["round_counts"], C.c_uint32), threads, _p(out["pos"], C.c_uint32))
         if rc != 0:
             raise RuntimeError("oracle probe: output bound exceeded (cap_factor / max_rounds too small)")
         out["cap"] = cap

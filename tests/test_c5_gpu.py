@@ -1,0 +1,83 @@
+"""C5: wide payload — 8 int64 build-side payload columns gathered on every match.
+
+Payload of build tuple r, column c: fmix64(r * 8 + c) (distinct per build tuple, so a gather from
+the wrong duplicate is caught).  Reference-order tables: every match's table position and payload
+row equal the oracle's (L3).  Device-built LP tables: every match's gathered row belongs to a
+build tuple with the probe's key, each build tuple at most once per probe row (L2)."""
+import numpy as np
+import pytest
+
+from helpers import ref_keys
+from oracle import oracle as O
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import ccj  # noqa: E402
+
+P = 8
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ccj.device_init(0)
+
+
+def payload_rows(n):
+    r = np.arange(n, dtype=np.uint64)[:, None] * np.uint64(P) + np.arange(P, dtype=np.uint64)[None, :]
+    return O.fmix64(r).view(np.int64)
+
+
+@pytest.mark.parametrize("kind", [ccj.LP, ccj.CHAIN])
+@pytest.mark.parametrize("cf", [1, 3])
+def test_c5_reference_layout(kind, cf):
+    n_build, n_probe, chunk = 1 << 18, 1 << 20, 2048
+    bkeys = ref_keys(n_build, cf)
+    pay = payload_rows(n_build)
+    table = ccj.Table.from_host(kind, bkeys)
+    table.set_payload(torch.from_numpy(pay.reshape(-1)).cuda(), P)
+    keys = O.uniform_keys(123 + cf, 0, n_probe, n_build + n_build // 4)
+    out = table.probe(torch.from_numpy(keys).cuda(), chunk, pos=True, payload_cols=P)
+    torch.cuda.synchronize()
+    assert int(out["status"].item()) == 0
+    otab = O.Table(kind, bkeys)
+    want = otab.probe(keys, chunk, cap_factor=cf, max_rounds=out["max_rounds"])
+    cnt = out["count"].cpu().numpy()
+    assert np.array_equal(cnt.view(np.uint32), want["count"])
+    cap = out["cap"]
+    valid = (np.arange(cap)[None, :] < cnt[:, None]).reshape(-1)
+    gpos = out["pos"].cpu().numpy().view(np.uint32)[valid]
+    assert np.array_equal(gpos, want["pos"][valid])
+    rows = otab.rows[gpos]
+    for c in range(P):
+        got = out["payload_cols"][c].cpu().numpy()[valid]
+        assert np.array_equal(got, pay[rows, c]), f"payload column {c}"
+
+
+def test_c5_device_built_lp():
+    n_build, n_probe, chunk, cf = 1 << 18, 1 << 20, 2048, 2
+    bkeys = ref_keys(n_build, cf)
+    pay = payload_rows(n_build)
+    table = ccj.Table.on_device(ccj.LP, torch.from_numpy(bkeys).cuda())
+    table.set_payload(torch.from_numpy(pay.reshape(-1)).cuda(), P)
+    keys = O.uniform_keys(9, 0, n_probe, n_build)
+    out = table.probe(torch.from_numpy(keys).cuda(), chunk, pos=True, payload_cols=P)
+    torch.cuda.synchronize()
+    cnt = out["count"].cpu().numpy().astype(np.int64)
+    cap = out["cap"]
+    valid = (np.arange(cap)[None, :] < cnt[:, None]).reshape(-1)
+    sel = out["sel"].cpu().numpy().view(np.uint32)[valid].astype(np.int64)
+    chunk_of = np.repeat(np.arange(len(cnt)), cnt)
+    prow = chunk_of * chunk + sel
+    col0 = out["payload_cols"][0].cpu().numpy()[valid]
+    inv = {int(v): r for r, v in enumerate(pay[:, 0])}
+    brow = np.array([inv[int(v)] for v in col0], np.int64)
+    assert np.array_equal(bkeys[brow], keys[prow])  # the gathered build tuple has the probe's key
+    for c in range(1, P):
+        assert np.array_equal(out["payload_cols"][c].cpu().numpy()[valid], pay[brow, c])
+    pairs = prow * n_build + brow
+    assert len(np.unique(pairs)) == len(pairs)  # each build duplicate gathered once per probe row
+    m, _ = O.count_uniform(9, 0, n_probe, n_build, n_build, cf)
+    assert len(brow) == m
