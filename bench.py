@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--n-probe", type=int, default=1 << 30, help="probe keys per GPU")
     ap.add_argument("--chunk", type=int, default=2048)
     ap.add_argument("--layout", default="device", choices=["device", "reference"])
+    ap.add_argument("--path", default="partitioned", choices=["partitioned", "chunk"],
+                    help="partitioned: slot-range partition + L2-resident probe (L1/L2 parity); "
+                         "chunk: reference-order chunk probe (L3 parity)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-sample", type=int, default=1 << 28, help="probe keys in the multi-thread CPU sample")
@@ -126,12 +129,16 @@ def main():
         table = ccj.Table.reference(ccj.LP, n_build, 1, layout, stream=stream)
         keys = ccj.gen_uniform_keys(n_probe, SEED, n_build, first_row=rank * n_probe, stream=stream)
         out = table.alloc_outputs(n_probe, chunk, rounds=True)
+        part = table.alloc_partitioned(n_probe) if args.path == "partitioned" else None
     stream.synchronize()
     log(f"[setup] table {table.size} slots, max_rounds {table.max_rounds}, keys {n_probe}: "
         f"{time.perf_counter() - t0:.1f} s")
 
-    def step():
-        table.probe(keys, chunk, out=out, stream=stream)
+    def step(path=args.path):
+        if path == "partitioned":
+            table.probe_partitioned(keys, chunk, out=out, part=part, stream=stream)
+        else:
+            table.probe(keys, chunk, out=out, stream=stream)
 
     for _ in range(args.warmup):
         step()
@@ -161,7 +168,25 @@ def main():
 
     # ---- verification + work accounting (untimed) ----
     status = int(out["status"].item())
-    matches, l2 = ccj.result_checksum(out, chunk, row_base=rank * n_probe, stream=stream)
+    if args.path == "partitioned":
+        rm = part["row_map"][:n_probe].to(torch.int64) + rank * n_probe
+        matches, l2 = ccj.result_checksum(out, chunk, row_map=rm, stream=stream)
+        del rm
+    else:
+        matches, l2 = ccj.result_checksum(out, chunk, row_base=rank * n_probe, stream=stream)
+    # the other path, timed the same way (reported beside the headline)
+    other = "chunk" if args.path == "partitioned" else "partitioned"
+    if other == "partitioned":
+        part = table.alloc_partitioned(n_probe)
+    step(other)
+    stream.synchronize()
+    ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
+    for a, b in ev2:
+        a.record(stream)
+        step(other)
+        b.record(stream)
+    stream.synchronize()
+    other_ms = sum(a.elapsed_time(b) for a, b in ev2) / len(ev2)
     examined, cost_matches = table.probe_cost(keys, stream=stream)
     parity = {"status_flags": status, "matches": matches, "l2": hex(l2)}
     if not args.no_verify:
@@ -200,10 +225,16 @@ def main():
             "hbm_gbs_algorithmic": achieved,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "probe_chunks<LP,32>", "kernel_ms": kern_ms,
+                         "kernel": ("ccj_probe_partitioned (2 slot-partition passes + probe_chunks)"
+                                    if args.path == "partitioned" else "probe_chunks<LP,2>"),
+                         "kernel_ms": kern_ms,
                          "alg_bytes_per_tuple": alg_bytes_per_tuple, "s_bar": s_bar, "m_bar": m_bar},
             "cpu_baseline": cpu,
             "parity": parity,
+            "path": args.path,
+            "other_path": {"path": other, "ms_per_step": other_ms, "value": n_probe / (other_ms * 1e-3),
+                           "frac": alg_bytes / (other_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                           "parity": "L3 (reference order)" if other == "chunk" else "L1/L2"},
         }
         print(json.dumps(line), flush=True)
     if dist:

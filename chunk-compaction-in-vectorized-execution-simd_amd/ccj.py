@@ -59,7 +59,8 @@ EXPORTS = ["ccj_last_error", "ccj_abi_version", "ccj_device_init", "ccj_table_bu
            "ccj_table_build_from_host", "ccj_table_build_on_device", "ccj_table_get_info", "ccj_table_free",
            "ccj_probe", "ccj_gen_uniform_keys", "ccj_probe_cost", "ccj_result_checksum",
            "ccj_compact_workspace_size", "ccj_compact", "ccj_partition_workspace_size", "ccj_partition_by_owner",
-           "ccj_result_checksum_mapped", "ccj_gen_reference_keys", "ccj_table_set_payload"]
+           "ccj_result_checksum_mapped", "ccj_gen_reference_keys", "ccj_table_set_payload",
+           "ccj_probe_partitioned_workspace_size", "ccj_probe_partitioned"]
 
 
 def build(force: bool = False) -> str:
@@ -85,6 +86,9 @@ def lib():
         L.ccj_table_get_info.argtypes = [vp, C.POINTER(TableInfo)]
         L.ccj_table_free.argtypes = [vp]
         L.ccj_table_set_payload.argtypes = [vp, vp, C.c_uint32, vp]
+        L.ccj_probe_partitioned_workspace_size.restype = C.c_size_t
+        L.ccj_probe_partitioned_workspace_size.argtypes = [vp, u64]
+        L.ccj_probe_partitioned.argtypes = [vp, C.POINTER(ProbeArgs), vp, vp, C.c_size_t, vp]
         L.ccj_probe.argtypes = [vp, C.POINTER(ProbeArgs), vp]
         L.ccj_gen_uniform_keys.argtypes = [vp, u64, u64, u64, u64, vp]
         L.ccj_gen_reference_keys.argtypes = [vp, u64, u64, u64, u64, vp]
@@ -107,9 +111,15 @@ def check(rc: int, what: str):
 
 
 def _stream(stream):
+    """HIP stream handle for a library call.  Work queued on the caller's current stream (tensor
+    allocations, copies) is ordered before the call when `stream` is a different stream."""
     import torch
-    s = stream if stream is not None else torch.cuda.current_stream()
-    return C.c_void_p(s.cuda_stream)
+    cur = torch.cuda.current_stream()
+    if stream is None:
+        return C.c_void_p(cur.cuda_stream)
+    if stream != cur:
+        stream.wait_stream(cur)
+    return C.c_void_p(stream.cuda_stream)
 
 
 def _ptr(t):
@@ -233,10 +243,28 @@ class Table:
         )
         return o
 
-    def probe(self, keys, chunk: int, sel=None, counts=None, out=None, stream=None, **alloc_kw):
-        """Batched Probe + Next loop (include/ccj.h ccj_probe).  Returns the output dict."""
+    def alloc_partitioned(self, n_rows: int, device=None):
+        """Workspace + row map for probe_partitioned."""
+        import torch
+        dev = device or torch.device("cuda", torch.cuda.current_device())
+        ws_bytes = lib().ccj_probe_partitioned_workspace_size(self._h, n_rows)
+        return dict(ws=torch.empty(max(ws_bytes, 8), dtype=torch.uint8, device=dev), ws_bytes=ws_bytes,
+                    row_map=torch.empty(max(n_rows, 1), dtype=torch.int32, device=dev))
+
+    def probe_partitioned(self, keys, chunk: int, out=None, part=None, stream=None, **alloc_kw):
+        """Slot-range-partitioned probe (ccj_probe_partitioned): L1/L2 results of probe(); out_sel
+        indexes the partitioned column and part["row_map"] maps it back to original rows."""
         if out is None:
             out = self.alloc_outputs(keys.numel(), chunk, **alloc_kw)
+        if part is None:
+            part = self.alloc_partitioned(keys.numel())
+        a = self._args(keys, chunk, None, None, out)
+        check(lib().ccj_probe_partitioned(self._h, C.byref(a), _ptr(part["row_map"]), _ptr(part["ws"]),
+                                          part["ws_bytes"], _stream(stream)), "ccj_probe_partitioned")
+        out["row_map"] = part["row_map"]
+        return out
+
+    def _args(self, keys, chunk, sel, counts, out):
         a = ProbeArgs(keys=_ptr(keys).value, sel=_ptr(sel).value if sel is not None else None,
                       counts=_ptr(counts).value if counts is not None else None, n_rows=keys.numel(), chunk=chunk,
                       max_rounds=out["max_rounds"], cap=out["cap"], out_count=_ptr(out["count"]).value,
@@ -251,8 +279,16 @@ class Table:
         a.n_payload_cols = len(cols)
         for i, col in enumerate(cols):
             a.out_payload_cols[i] = col.data_ptr()
+        return a
+
+    def probe(self, keys, chunk: int, sel=None, counts=None, out=None, stream=None, **alloc_kw):
+        """Batched Probe + Next loop (include/ccj.h ccj_probe).  Returns the output dict."""
+        if out is None:
+            out = self.alloc_outputs(keys.numel(), chunk, **alloc_kw)
+        a = self._args(keys, chunk, sel, counts, out)
         check(lib().ccj_probe(self._h, C.byref(a), _stream(stream)), "ccj_probe")
         return out
+
 
 
 def compact(probe_out, chunk: int, cols=(), payload: bool = True, rows: bool = True, stream=None):

@@ -372,13 +372,14 @@ int ccj_table_free(ccj_table *t) {
   return CCJ_OK;
 }
 
-int ccj_probe(const ccj_table *t, const ccj_probe_args *a, ccj_stream stream) {
+namespace {
+int fill_probe_params(const ccj_table *t, const ccj_probe_args *a, ccj::ProbeParams &p) {
   if (!t || !a) return fail(CCJ_ERR_INVALID, "ccj_probe: null table/args");
   if (a->chunk == 0 || a->chunk > ccj::kMaxChunk) return fail(CCJ_ERR_INVALID, "ccj_probe: chunk must be 1..2048");
-  if (a->n_rows == 0) return CCJ_OK;  // no chunks: nothing to launch
-  if (!a->out_count || !a->out_sel || !a->keys) return fail(CCJ_ERR_INVALID, "ccj_probe: missing buffer");
   if (a->out_round_counts && a->max_rounds == 0) return fail(CCJ_ERR_INVALID, "ccj_probe: max_rounds == 0");
-  ccj::ProbeParams p{};
+  if (a->n_rows && (!a->out_count || !a->out_sel || !a->keys))
+    return fail(CCJ_ERR_INVALID, "ccj_probe: missing buffer");
+  p = ccj::ProbeParams{};
   p.table = t->d_table;
   p.off = t->d_off;
   p.mask = (uint32_t)(t->info.size - 1);
@@ -405,6 +406,45 @@ int ccj_probe(const ccj_table *t, const ccj_probe_args *a, ccj_stream stream) {
     if (!a->out_payload_cols[c]) return fail(CCJ_ERR_INVALID, "ccj_probe: null payload column");
     p.out_cols[c] = a->out_payload_cols[c];
   }
+  return CCJ_OK;
+}
+}  // namespace
+
+size_t ccj_probe_partitioned_workspace_size(const ccj_table *t, uint64_t n_rows) {
+  if (!t) return 0;
+  return ((n_rows * 8 + 255) & ~255ull) + ccj::slot_partition_workspace(n_rows, ccj::slot_plan(t->info.size));
+}
+
+int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t *out_row_map, void *ws,
+                          size_t ws_bytes, ccj_stream stream) {
+  ccj::ProbeParams p;
+  if (int rc = fill_probe_params(t, a, p)) return rc;
+  if (t->info.kind != CCJ_TABLE_LP) return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: LP tables only");
+  if (a->sel || a->counts) return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: sel/counts must be NULL");
+  if (a->n_rows >= (1ull << 32)) return fail(CCJ_ERR_LIMIT, "ccj_probe_partitioned: n_rows must be < 2^32");
+  if (a->n_rows == 0) return CCJ_OK;
+  if (!out_row_map || !ws || ws_bytes < ccj_probe_partitioned_workspace_size(t, a->n_rows))
+    return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: missing row map or workspace too small");
+  const ccj::SlotPlan pl = ccj::slot_plan(t->info.size);
+  hipStream_t s = (hipStream_t)stream;
+  int64_t *pkeys = (int64_t *)ws;
+  void *rest = (char *)ws + ((a->n_rows * 8 + 255) & ~255ull);
+  if (pl.lo_bits == 0) {  // the whole table is one window: identity order
+    HIP_TRY(hipMemcpyAsync(pkeys, a->keys, a->n_rows * 8, hipMemcpyDeviceToDevice, s), "copy");
+    HIP_TRY(ccj::launch_iota_u32(out_row_map, a->n_rows, s), "iota");
+  } else {
+    HIP_TRY(ccj::launch_slot_partition(a->keys, a->n_rows, pl, pkeys, out_row_map, rest, s), "slot partition");
+  }
+  p.keys = pkeys;
+  p.xcd_swizzle = 1;
+  HIP_TRY(ccj::launch_probe(t->info.kind, p, s), "probe launch");
+  return CCJ_OK;
+}
+
+int ccj_probe(const ccj_table *t, const ccj_probe_args *a, ccj_stream stream) {
+  ccj::ProbeParams p;
+  if (int rc = fill_probe_params(t, a, p)) return rc;
+  if (a->n_rows == 0) return CCJ_OK;  // no chunks: nothing to launch
   HIP_TRY(ccj::launch_probe(t->info.kind, p, (hipStream_t)stream), "probe launch");
   return CCJ_OK;
 }

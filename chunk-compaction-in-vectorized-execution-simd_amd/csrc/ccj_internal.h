@@ -59,6 +59,7 @@ struct ProbeParams {
   uint32_t n_pay;      // payload columns gathered (<= CCJ_MAX_PAYLOAD_COLS)
   uint32_t pay_stride; // payload columns stored per position
   int64_t *out_cols[CCJ_MAX_PAYLOAD_COLS];
+  uint32_t xcd_swizzle;  // 1: consecutive chunks go to the same XCD (L2 reuse of partitioned input)
 };
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 
@@ -67,6 +68,7 @@ hipError_t launch_probe(int kind, const ProbeParams &p, hipStream_t s);
 hipError_t launch_gen_reference_keys(int64_t *out, uint64_t first, uint64_t n, uint64_t n_total, uint64_t cf,
                                      hipStream_t s);
 hipError_t launch_fill(int64_t *p, uint64_t n, int64_t v, hipStream_t s);
+hipError_t launch_iota_u32(uint32_t *p, uint64_t n, hipStream_t s);
 hipError_t launch_lp_insert(const int64_t *keys, uint64_t n, int64_t *slots, uint32_t *slot_row, uint32_t mask,
                             hipStream_t s);
 hipError_t launch_scatter_payload(const int64_t *src, uint32_t n_cols, const uint32_t *row, uint64_t positions,
@@ -86,6 +88,16 @@ hipError_t launch_result_checksum(const uint32_t *count, const uint32_t *sel, co
 size_t compact_workspace(uint64_t n_chunks, uint64_t cap, uint32_t chunk);
 hipError_t launch_compact(const ccj_compact_args &a, hipStream_t s);
 size_t partition_workspace(uint64_t n, uint32_t parts);
+// Slot-range partitioning for the L2-resident probe: partition p = slot >> window_bits, with the
+// partition bits split into a low digit (first LSD pass) and a high digit (second pass).
+constexpr uint32_t kWindowBits = 17;  // 2^17 slots = 1 MiB table window per partition
+struct SlotPlan {
+  uint32_t window_bits, lo_bits, hi_bits;
+};
+SlotPlan slot_plan(uint64_t table_size);
+size_t slot_partition_workspace(uint64_t n, const SlotPlan &pl);
+hipError_t launch_slot_partition(const int64_t *keys, uint64_t n, const SlotPlan &pl, int64_t *out_keys,
+                                 uint32_t *out_rows, void *ws, hipStream_t s);
 hipError_t launch_partition(const int64_t *keys, uint64_t n, uint32_t parts, uint64_t row_base, int64_t *out_keys,
                             uint64_t *out_rows, uint64_t *out_counts, void *ws, hipStream_t s);
 

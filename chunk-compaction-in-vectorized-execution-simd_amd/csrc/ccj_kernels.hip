@@ -150,7 +150,14 @@ __global__ __launch_bounds__(kBlock) void probe_chunks(ProbeParams p) {
   __shared__ uint32_t s_off[kMaxFastRounds * 32];
   __shared__ uint32_t s_red[3 * kChunkWaves];
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
-  const uint64_t c = blockIdx.x;
+  // Optional XCD-aware order (perf only): workgroups are dealt round-robin to the 8 XCDs, so block
+  // b takes chunk (b % 8) * (n8 / 8) + b / 8 and each XCD walks a contiguous range of chunks —
+  // with slot-partitioned input, the table window those chunks share stays in that XCD's L2.
+  uint64_t c = blockIdx.x;
+  if (p.xcd_swizzle) {
+    const uint64_t n8 = p.n_chunks & ~7ull;
+    if (c < n8) c = (c & 7) * (n8 >> 3) + (c >> 3);
+  }
   const uint64_t base = c * p.chunk;
   const uint64_t rem = p.n_rows - base;
   const uint32_t phys = rem < p.chunk ? (uint32_t)rem : p.chunk;
@@ -584,6 +591,16 @@ hipError_t launch_gen_reference_keys(int64_t *out, uint64_t first, uint64_t n, u
   const uint64_t num_unique = n_total / cf + (n_total % cf != 0);
   const uint64_t step = n_total / num_unique;
   hipLaunchKernelGGL(gen_reference_keys, dim3(grid_for(n, 256)), dim3(256), 0, s, out, first, n, cf, step);
+  return hipGetLastError();
+}
+
+__global__ void iota_u32(uint32_t *p, uint64_t n) {
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x)
+    p[t] = (uint32_t)t;
+}
+
+hipError_t launch_iota_u32(uint32_t *p, uint64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(iota_u32, dim3(grid_for(n, 256)), dim3(256), 0, s, p, n);
   return hipGetLastError();
 }
 

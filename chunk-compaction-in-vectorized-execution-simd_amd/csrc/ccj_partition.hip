@@ -1,11 +1,14 @@
-// ccj_partition.hip — owner partitioning of a probe (or build) key column for the multi-GPU join
-// (SURVEY §8e): owner(k) = murmurhash64(k) >> (64 - log2 P), the TOP hash bits, disjoint from the
-// low bits every GPU's local table uses for its slot/bucket, so shard tables stay evenly loaded.
+// ccj_partition.hip — stable multisplits of a key column by a digit of its murmurhash64 value.
 //
-// Stable multisplit in two passes: (1) per-tile destination counts, written destination-major;
+//  - owner partitioning for the multi-GPU join: digit = h >> (64 - log2 P), the TOP
+//    hash bits, disjoint from the low bits every GPU's local table uses, so shards stay balanced;
+//  - slot-range partitioning for the L2-resident probe (ccj_probe_partitioned): digits of the
+//    slot index h & (n_slots - 1) above the window bits, two LSD passes (low digit, then high).
+//
+// Each pass is a stable multisplit in two kernels: (1) per-tile digit counts, written digit-major;
 // (2) after an exclusive scan of those counts, every tile re-reads its keys and scatters them in
-// row order (ballot + mbcnt ranks inside a wave, LDS-scanned across the tile's waves), so each
-// destination segment keeps the source row order: deterministic send buffers.
+// row order (ballot + mbcnt ranks inside a wave, LDS-scanned across the tile's waves).  Stability
+// makes the outputs deterministic and lets two LSD passes compose into a sort by (hi, lo).
 #include <hipcub/hipcub.hpp>
 
 #include "ccj_internal.h"
@@ -17,28 +20,33 @@ constexpr int kTileThreads = 256;
 constexpr int kTileIters = 32;
 constexpr uint64_t kTile = (uint64_t)kTileThreads * kTileIters;  // 8192 keys per tile
 
-__device__ __forceinline__ uint32_t owner_of(int64_t k, uint32_t shift) {
-  return shift >= 64 ? 0u : (uint32_t)(murmurhash64((uint64_t)k) >> shift);
-}
+struct Digit {
+  uint32_t shift;  // >= 64: every key to digit 0
+  uint32_t mask;   // parts - 1
+  __device__ __forceinline__ uint32_t operator()(int64_t k) const {
+    return shift >= 64 ? 0u : (uint32_t)(murmurhash64((uint64_t)k) >> shift) & mask;
+  }
+};
 
-__global__ __launch_bounds__(kTileThreads) void part_count(const int64_t *keys, uint64_t n, uint32_t parts,
-                                                           uint32_t shift, uint64_t n_tiles, uint64_t *cnt) {
+__global__ __launch_bounds__(kTileThreads) void part_count(const int64_t *keys, uint64_t n, uint32_t parts, Digit dg,
+                                                           uint64_t n_tiles, uint64_t *cnt) {
   __shared__ uint32_t s_cnt[kMaxParts];
   const uint64_t tile = blockIdx.x;
   if (threadIdx.x < kMaxParts) s_cnt[threadIdx.x] = 0;
   __syncthreads();
   for (int it = 0; it < kTileIters; ++it) {
     const uint64_t i = tile * kTile + (uint64_t)it * kTileThreads + threadIdx.x;
-    if (i < n) atomicAdd(&s_cnt[owner_of(keys[i], shift)], 1u);
+    if (i < n) atomicAdd(&s_cnt[dg(keys[i])], 1u);
   }
   __syncthreads();
   if (threadIdx.x < parts) cnt[(uint64_t)threadIdx.x * n_tiles + tile] = s_cnt[threadIdx.x];
 }
 
-__global__ __launch_bounds__(kTileThreads) void part_scatter(const int64_t *keys, uint64_t n, uint32_t parts,
-                                                             uint32_t shift, uint64_t n_tiles, const uint64_t *off,
-                                                             uint64_t row_base, int64_t *out_keys,
-                                                             uint64_t *out_rows) {
+template <typename RowT>
+__global__ __launch_bounds__(kTileThreads) void part_scatter(const int64_t *keys, const RowT *in_rows, uint64_t n,
+                                                             uint32_t parts, Digit dg, uint64_t n_tiles,
+                                                             const uint64_t *off, uint64_t row_base,
+                                                             int64_t *out_keys, RowT *out_rows) {
   __shared__ uint64_t s_base[kMaxParts];
   __shared__ uint32_t s_wave[kTileThreads / 64][kMaxParts];
   const uint64_t tile = blockIdx.x;
@@ -49,7 +57,7 @@ __global__ __launch_bounds__(kTileThreads) void part_scatter(const int64_t *keys
     const uint64_t i = tile * kTile + (uint64_t)it * kTileThreads + threadIdx.x;
     const bool valid = i < n;
     const int64_t k = valid ? keys[i] : 0;
-    const uint32_t d = valid ? owner_of(k, shift) : 0xFFFFFFFFu;
+    const uint32_t d = valid ? dg(k) : 0xFFFFFFFFu;
     uint32_t rank = 0;
     for (uint32_t p = 0; p < parts; ++p) {
       const uint64_t m = __ballot(d == p);
@@ -61,7 +69,7 @@ __global__ __launch_bounds__(kTileThreads) void part_scatter(const int64_t *keys
       uint64_t pos = s_base[d] + rank;
       for (uint32_t w = 0; w < wave; ++w) pos += s_wave[w][d];
       out_keys[pos] = k;
-      out_rows[pos] = row_base + i;
+      out_rows[pos] = in_rows ? in_rows[i] : (RowT)(row_base + i);
     }
     __syncthreads();
     if (threadIdx.x < parts) {
@@ -89,37 +97,90 @@ size_t scan_bytes(uint64_t n) {
   return (b + 255) & ~(size_t)255;
 }
 
-}  // namespace
-
-size_t partition_workspace(uint64_t n, uint32_t parts) {
+size_t pass_workspace(uint64_t n, uint32_t parts) {
   const uint64_t n_tiles = (n + kTile - 1) / kTile;
   const uint64_t m = n_tiles * parts;
   return 2 * ((m * 8 + 255) & ~255ull) + scan_bytes(m ? m : 1);
 }
 
-hipError_t launch_partition(const int64_t *keys, uint64_t n, uint32_t parts, uint64_t row_base, int64_t *out_keys,
-                            uint64_t *out_rows, uint64_t *out_counts, void *ws, hipStream_t s) {
-  uint32_t log2p = 0;
-  while ((1u << log2p) < parts) ++log2p;
-  const uint32_t shift = 64 - log2p;  // 64 -> every key to part 0
+// One stable multisplit pass.  out_counts (digit totals) may be NULL.
+template <typename RowT>
+hipError_t split_pass(const int64_t *keys, const RowT *in_rows, uint64_t n, uint32_t parts, Digit dg,
+                      uint64_t row_base, int64_t *out_keys, RowT *out_rows, uint64_t *out_counts, void *ws,
+                      hipStream_t s) {
   const uint64_t n_tiles = (n + kTile - 1) / kTile;
   const uint64_t m = n_tiles * parts;
-  if (n == 0) return hipMemsetAsync(out_counts, 0, parts * 8, s);
+  if (n == 0) return out_counts ? hipMemsetAsync(out_counts, 0, parts * 8, s) : hipSuccess;
   char *w = (char *)ws;
   uint64_t *cnt = (uint64_t *)w;
   w += (m * 8 + 255) & ~255ull;
   uint64_t *off = (uint64_t *)w;
   w += (m * 8 + 255) & ~255ull;
   size_t tb = scan_bytes(m);
-  hipLaunchKernelGGL(part_count, dim3((unsigned)n_tiles), dim3(kTileThreads), 0, s, keys, n, parts, shift, n_tiles, cnt);
+  hipLaunchKernelGGL(part_count, dim3((unsigned)n_tiles), dim3(kTileThreads), 0, s, keys, n, parts, dg, n_tiles, cnt);
   hipError_t e = hipGetLastError();
   if (e) return e;
   e = hipcub::DeviceScan::ExclusiveSum(w, tb, cnt, off, (int)m, s);
   if (e) return e;
-  hipLaunchKernelGGL(part_scatter, dim3((unsigned)n_tiles), dim3(kTileThreads), 0, s, keys, n, parts, shift, n_tiles,
-                     off, row_base, out_keys, out_rows);
-  hipLaunchKernelGGL(part_totals, dim3(1), dim3(64), 0, s, cnt, off, parts, n_tiles, out_counts);
+  hipLaunchKernelGGL((part_scatter<RowT>), dim3((unsigned)n_tiles), dim3(kTileThreads), 0, s, keys, in_rows, n, parts,
+                     dg, n_tiles, off, row_base, out_keys, out_rows);
+  if (out_counts) hipLaunchKernelGGL(part_totals, dim3(1), dim3(64), 0, s, cnt, off, parts, n_tiles, out_counts);
   return hipGetLastError();
+}
+
+uint32_t log2u(uint64_t x) {
+  uint32_t l = 0;
+  while ((1ull << l) < x) ++l;
+  return l;
+}
+
+}  // namespace
+
+size_t partition_workspace(uint64_t n, uint32_t parts) { return pass_workspace(n, parts); }
+
+hipError_t launch_partition(const int64_t *keys, uint64_t n, uint32_t parts, uint64_t row_base, int64_t *out_keys,
+                            uint64_t *out_rows, uint64_t *out_counts, void *ws, hipStream_t s) {
+  const uint32_t lp = log2u(parts);
+  const Digit dg{lp == 0 ? 64u : 64u - lp, parts - 1};
+  return split_pass<uint64_t>(keys, nullptr, n, parts, dg, row_base, out_keys, out_rows, out_counts, ws, s);
+}
+
+// ---- slot-range partitioning for the L2-resident probe ------------------------------------------
+SlotPlan slot_plan(uint64_t table_size) {
+  SlotPlan pl{};
+  const uint32_t sbits = log2u(table_size);  // table_size is a power of two
+  pl.window_bits = kWindowBits < sbits ? kWindowBits : sbits;
+  if (sbits - pl.window_bits > 12) pl.window_bits = sbits - 12;  // two passes of <= 64 digits
+  const uint32_t dbits = sbits - pl.window_bits;
+  pl.lo_bits = dbits < 6 ? dbits : 6;
+  pl.hi_bits = dbits - pl.lo_bits;
+  return pl;
+}
+
+size_t slot_partition_workspace(uint64_t n, const SlotPlan &pl) {
+  if (pl.lo_bits == 0) return 256;
+  // pass buffers (keys + u32 rows) + the larger of the two passes' count/scan scratch
+  const size_t buf = ((n * 8 + 255) & ~255ull) + ((n * 4 + 255) & ~255ull);
+  const size_t a = pass_workspace(n, 1u << pl.lo_bits);
+  const size_t b = pl.hi_bits ? pass_workspace(n, 1u << pl.hi_bits) : 0;
+  return buf + (a > b ? a : b);
+}
+
+hipError_t launch_slot_partition(const int64_t *keys, uint64_t n, const SlotPlan &pl, int64_t *out_keys,
+                                 uint32_t *out_rows, void *ws, hipStream_t s) {
+  if (pl.lo_bits == 0) return hipSuccess;
+  char *w = (char *)ws;
+  int64_t *tk = (int64_t *)w;
+  w += (n * 8 + 255) & ~255ull;
+  uint32_t *tr = (uint32_t *)w;
+  w += (n * 4 + 255) & ~255ull;
+  const Digit lo{pl.window_bits, (1u << pl.lo_bits) - 1};
+  if (pl.hi_bits == 0)
+    return split_pass<uint32_t>(keys, nullptr, n, 1u << pl.lo_bits, lo, 0, out_keys, out_rows, nullptr, w, s);
+  const Digit hi{pl.window_bits + pl.lo_bits, (1u << pl.hi_bits) - 1};
+  hipError_t e = split_pass<uint32_t>(keys, nullptr, n, 1u << pl.lo_bits, lo, 0, tk, tr, nullptr, w, s);
+  if (e) return e;
+  return split_pass<uint32_t>(tk, tr, n, 1u << pl.hi_bits, hi, 0, out_keys, out_rows, nullptr, w, s);
 }
 
 }  // namespace ccj

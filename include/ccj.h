@@ -142,6 +142,18 @@ typedef struct ccj_probe_args {
 
 int ccj_probe(const ccj_table *table, const ccj_probe_args *args, ccj_stream stream);
 
+/* Slot-range-partitioned probe (the throughput path; L1/L2 parity, not L3 order).
+ * LP tables only.  The probe column (args->keys, n_rows; sel and counts must be NULL) is first
+ * split by its home slot's partition (slot >> 17: 1 MiB of table per partition, two stable LSD
+ * passes), then probed chunk by chunk like ccj_probe with consecutive chunks kept on one XCD, so
+ * each partition's table window is read from L2 instead of as random HBM lines.  Outputs are
+ * ccj_probe's, over the partitioned column: out_sel indexes partitioned positions, and
+ * out_row_map[pos] gives the original row of partitioned position pos.  Same matches, payloads
+ * and per-row multiplicities as ccj_probe (L1 + L2). */
+size_t ccj_probe_partitioned_workspace_size(const ccj_table *table, uint64_t n_rows);
+int ccj_probe_partitioned(const ccj_table *table, const ccj_probe_args *args, uint32_t *out_row_map,
+                          void *workspace, size_t workspace_bytes, ccj_stream stream);
+
 /* ---- compaction ------------------------------------------------------------------------- */
 /* Replaces NaiveCompactor::Compact + Flush (compactor.cpp:5-41, compactor.h:23) applied to every
  * Next result of a ccj_probe output, in pipeline order (chunk-major, round-major), with the

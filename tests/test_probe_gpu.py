@@ -158,3 +158,33 @@ def test_l1_l2_large_membership(kind):
     # L2 checksum computed on the device side of the test with torch integer ops
     rows, pay = matches_of(host(out), 2048)
     assert O.l2_sum(rows, pay) == l2
+
+
+@pytest.mark.parametrize("n_build,cf,n_probe,rng", [(1 << 20, 1, 1 << 22, 1 << 20), (1 << 22, 2, 1 << 23, 3 << 21),
+                                                    (1 << 16, 1, 100000, 1 << 17), (1000, 1, 5000, 2000),
+                                                    (1 << 24, 1, (1 << 24) + 77, 1 << 24)])
+def test_partitioned_probe_l1_l2(n_build, cf, n_probe, rng):
+    table = ccj.Table.reference(ccj.LP, n_build, cf, ccj.LAYOUT_DEVICE)
+    keys = ccj.gen_uniform_keys(n_probe, 31, rng)
+    out = table.probe_partitioned(keys, 2048)
+    torch.cuda.synchronize()
+    assert int(out["status"].item()) == 0
+    m, l2 = ccj.result_checksum(out, 2048, row_map=out["row_map"][:n_probe].to(torch.int64))
+    assert (m, l2) == O.count_uniform(31, 0, n_probe, rng, n_build, cf)
+    # the row map is a permutation of the probe rows, grouped by table window (slot >> 17)
+    rm = out["row_map"][:n_probe].cpu().numpy().view(np.uint32)
+    assert np.array_equal(np.sort(rm), np.arange(n_probe, dtype=np.uint32))
+
+
+def test_partitioned_probe_same_rows_as_chunk_probe():
+    n_build, n_probe = 1 << 20, 1 << 21
+    table = ccj.Table.reference(ccj.LP, n_build, 3, ccj.LAYOUT_REFERENCE)
+    keys = ccj.gen_uniform_keys(n_probe, 5, n_build)
+    a = host(table.probe(keys, 2048))
+    b = host(table.probe_partitioned(keys, 2048))
+    ra, pa = matches_of(a, 2048)
+    rb_local, pb = matches_of(b, 2048)
+    rb = b["row_map"].view(np.uint32)[rb_local.astype(np.int64)].astype(np.uint64)
+    oa = np.lexsort((pa, ra))
+    ob = np.lexsort((pb, rb))
+    assert np.array_equal(ra[oa], rb[ob]) and np.array_equal(pa[oa], pb[ob])
