@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--n-probe", type=int, default=1 << 30, help="probe keys per GPU")
     ap.add_argument("--chunk", type=int, default=2048)
     ap.add_argument("--layout", default="device", choices=["device", "reference"])
-    ap.add_argument("--path", default="partitioned", choices=["partitioned", "chunk"],
+    ap.add_argument("--path", default="chunk", choices=["partitioned", "chunk"],
                     help="partitioned: slot-range partition + L2-resident probe (L1/L2 parity); "
                          "chunk: reference-order chunk probe (L3 parity)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")

@@ -255,10 +255,12 @@ class Table:
         """Slot-range-partitioned probe (ccj_probe_partitioned): L1/L2 results of probe(); out_sel
         indexes the partitioned column and part["row_map"] maps it back to original rows."""
         if out is None:
+            alloc_kw.setdefault("rounds", False)
             out = self.alloc_outputs(keys.numel(), chunk, **alloc_kw)
         if part is None:
             part = self.alloc_partitioned(keys.numel())
         a = self._args(keys, chunk, None, None, out)
+        a.out_round_counts = None  # no Next boundaries in partition order
         check(lib().ccj_probe_partitioned(self._h, C.byref(a), _ptr(part["row_map"]), _ptr(part["ws"]),
                                           part["ws_bytes"], _stream(stream)), "ccj_probe_partitioned")
         out["row_map"] = part["row_map"]

@@ -5,6 +5,7 @@
 // insertion order (CCJ_LAYOUT_REFERENCE), which is inherently serial and untimed in the
 // reference too (main.cpp:62-68 builds tables before the timed loop at :92-94).
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -421,6 +422,8 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   if (int rc = fill_probe_params(t, a, p)) return rc;
   if (t->info.kind != CCJ_TABLE_LP) return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: LP tables only");
   if (a->sel || a->counts) return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: sel/counts must be NULL");
+  if (a->out_pos || a->n_payload_cols || a->out_round_counts)
+    return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: out_pos/payload columns/round counts not supported");
   if (a->n_rows >= (1ull << 32)) return fail(CCJ_ERR_LIMIT, "ccj_probe_partitioned: n_rows must be < 2^32");
   if (a->n_rows == 0) return CCJ_OK;
   if (!out_row_map || !ws || ws_bytes < ccj_probe_partitioned_workspace_size(t, a->n_rows))
@@ -436,8 +439,9 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
     HIP_TRY(ccj::launch_slot_partition(a->keys, a->n_rows, pl, pkeys, out_row_map, rest, s), "slot partition");
   }
   p.keys = pkeys;
-  p.xcd_swizzle = 1;
-  HIP_TRY(ccj::launch_probe(t->info.kind, p, s), "probe launch");
+  p.xcd_swizzle = getenv("CCJ_NO_SWIZZLE") ? 0 : 1;
+  if (const char *ab = getenv("CCJ_ABLATE")) p.ablate = (uint32_t)atoi(ab);
+  HIP_TRY(ccj::launch_probe_flat(t->info.kind, p, s), "probe launch");
   return CCJ_OK;
 }
 

@@ -60,11 +60,13 @@ struct ProbeParams {
   uint32_t pay_stride; // payload columns stored per position
   int64_t *out_cols[CCJ_MAX_PAYLOAD_COLS];
   uint32_t xcd_swizzle;  // 1: consecutive chunks go to the same XCD (L2 reuse of partitioned input)
+  uint32_t ablate;       // timing-only ablations (CCJ_ABLATE env, never set in product calls)
 };
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 
 // Launchers (ccj_kernels.hip).  Return hipError_t of the launch.
 hipError_t launch_probe(int kind, const ProbeParams &p, hipStream_t s);
+hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s);
 hipError_t launch_gen_reference_keys(int64_t *out, uint64_t first, uint64_t n, uint64_t n_total, uint64_t cf,
                                      hipStream_t s);
 hipError_t launch_fill(int64_t *p, uint64_t n, int64_t v, hipStream_t s);

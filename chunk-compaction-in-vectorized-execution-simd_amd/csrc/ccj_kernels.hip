@@ -396,6 +396,169 @@ __global__ __launch_bounds__(kBlock) void probe_chunks(ProbeParams p) {
   }
 }
 
+// Flat probe for slot-partitioned input (ccj_probe_partitioned): the output order inside a chunk
+// is free (L1/L2 parity), so every row walks its run and writes its matches as soon as they are
+// found — one phase, no per-round bookkeeping.  256 threads per 2048-row chunk, row i = k*256 +
+// tid (coalesced key loads), all of a lane's rows walked concurrently through aligned 32-byte
+// windows that the slot partitioning keeps L2-resident.  Matches are placed with one LDS atomic
+// per wave and step (wave prefix sum of the lanes' match counts).
+constexpr int kFlatThreads = 256;
+constexpr int kFlatRows = kMaxChunk / kFlatThreads;  // 8
+constexpr uint32_t kFlatStage = kMaxChunk;          // matches staged in LDS per chunk
+
+template <int KIND, int W>
+__global__ __launch_bounds__(kFlatThreads) void probe_flat(ProbeParams p) {
+  __shared__ uint32_t s_cnt, s_rounds;
+  __shared__ uint32_t s_sel[kFlatStage];
+  __shared__ int64_t s_pay[kFlatStage];
+  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1);
+  uint64_t c = blockIdx.x;
+  if (p.xcd_swizzle) {
+    const uint64_t n8 = p.n_chunks & ~7ull;
+    if (c < n8) c = (c & 7) * (n8 >> 3) + (c >> 3);
+  }
+  const uint64_t base = c * p.chunk;
+  const uint64_t rem = p.n_rows - base;
+  const uint32_t phys = rem < p.chunk ? (uint32_t)rem : p.chunk;
+  const uint64_t obase = c * p.cap;
+  if (tid == 0) {
+    s_cnt = 0;
+    s_rounds = 0;
+  }
+  __syncthreads();
+  int64_t key[kFlatRows];
+  uint32_t cur[kFlatRows], r0[kFlatRows], lim[kFlatRows];
+  uint32_t need = 0, lane_rounds = 0;
+#pragma unroll
+  for (int k = 0; k < kFlatRows; ++k) {
+    const uint32_t i = k * kFlatThreads + tid;
+    key[k] = 0;
+    cur[k] = r0[k] = lim[k] = 0;
+    if (i < phys) {
+      key[k] = p.keys[base + i];
+      const uint32_t h = (uint32_t)murmurhash64((uint64_t)key[k]) & p.mask;
+      if (KIND == CCJ_TABLE_LP) {
+        cur[k] = h;
+        need |= 1u << k;
+      } else {
+        cur[k] = p.off[h];
+        lim[k] = p.off[h + 1];
+        if (cur[k] != lim[k]) need |= 1u << k;
+      }
+    }
+  }
+  uint32_t overflow = 0;
+  while (__ballot(need != 0u) != 0ull) {
+    int64_t v[kFlatRows][W];
+#pragma unroll
+    for (int k = 0; k < kFlatRows; ++k) {
+      if ((need >> k) & 1u) {
+        const int64_t *w = p.table + (cur[k] & ~(uint32_t)(W - 1));
+        if (p.ablate & 2u) {  // timing only: no table reads
+#pragma unroll
+          for (int t = 0; t < W; ++t) v[k][t] = t ? -1 : key[k];
+        } else if (W == 2) {
+          const longlong2 x = *reinterpret_cast<const longlong2 *>(w);
+          v[k][0] = x.x;
+          v[k][W - 1] = x.y;
+        } else {
+#pragma unroll
+          for (int t = 0; t < W; t += 2) {
+            const longlong2 x = reinterpret_cast<const longlong2 *>(w)[t / 2];
+            v[k][t] = x.x;
+            v[k][t + 1] = x.y;
+          }
+        }
+      }
+    }
+    uint32_t hits[kFlatRows];  // bit t: window position t matched
+    uint32_t n_hits = 0;
+#pragma unroll
+    for (int k = 0; k < kFlatRows; ++k) {
+      hits[k] = 0;
+      if ((need >> k) & 1u) {
+        const uint32_t blk = cur[k] & ~(uint32_t)(W - 1);
+        const uint32_t off = cur[k] - blk;
+        bool go = true;
+#pragma unroll
+        for (int t = 0; t < W; ++t) {
+          if (go && (uint32_t)t >= off) {
+            const int64_t val = v[k][t];
+            const bool stop = KIND == CCJ_TABLE_LP ? (val == -1) : (blk + (uint32_t)t == lim[k]);
+            if (stop) {
+              go = false;
+              const uint32_t r = r0[k] + (uint32_t)t - off;
+              lane_rounds = r > lane_rounds ? r : lane_rounds;
+            } else if (val == key[k]) {
+              hits[k] |= 1u << t;
+            }
+          }
+        }
+        n_hits += (uint32_t)__builtin_popcount(hits[k]);
+        if (go) {
+          r0[k] += (uint32_t)W - off;
+          cur[k] = KIND == CCJ_TABLE_LP ? ((blk + W) & p.mask) : blk + W;
+          if (KIND == CCJ_TABLE_CHAIN && cur[k] == lim[k]) {
+            lane_rounds = r0[k] > lane_rounds ? r0[k] : lane_rounds;
+            go = false;
+          }
+        }
+        if (!go) need &= ~(1u << k);
+      }
+    }
+    // place this step's matches: wave prefix of n_hits, one LDS atomic per wave
+    uint32_t incl = n_hits;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
+      if (lane >= (uint32_t)d) incl += o;
+    }
+    const uint32_t wave_total = (uint32_t)__shfl((int)incl, kWave - 1);
+    uint32_t wbase = 0;
+    if (wave_total) {
+      if (lane == 0) wbase = atomicAdd(&s_cnt, wave_total);
+      wbase = (uint32_t)__shfl((int)wbase, 0);
+    }
+    if (n_hits) {
+      uint32_t o = wbase + incl - n_hits;
+#pragma unroll
+      for (int k = 0; k < kFlatRows; ++k) {
+        for (uint32_t hm = hits[k]; hm; hm &= hm - 1u, ++o) {
+          if (p.ablate & 1u) continue;  // timing only: no output stores
+          const uint32_t i = k * kFlatThreads + tid;
+          if (o < kFlatStage) {  // staged in LDS, written out coalesced below
+            s_sel[o] = i;
+            s_pay[o] = key[k];  // matched table value == probe key
+          } else if (o < p.cap) {
+            p.out_sel[obase + o] = i;
+            if (p.out_payload) p.out_payload[obase + o] = key[k];
+          } else {
+            overflow = 1;
+          }
+        }
+      }
+    }
+  }
+  {
+    const uint32_t wr = wave_max(lane_rounds);
+    if (lane == 0) atomicMax(&s_rounds, wr);
+  }
+  __syncthreads();
+  const uint32_t total = s_cnt;
+  const uint32_t staged = total < kFlatStage ? total : kFlatStage;
+  if (!(p.ablate & 1u)) {
+    for (uint32_t q = tid; q < staged && q < p.cap; q += kFlatThreads) {
+      p.out_sel[obase + q] = s_sel[q];
+      if (p.out_payload) p.out_payload[obase + q] = s_pay[q];
+    }
+  }
+  if (tid == 0) {
+    p.out_count[c] = total < p.cap ? total : (uint32_t)p.cap;
+    if (p.out_rounds) p.out_rounds[c] = s_rounds;  // rounds the reference would run on this chunk
+  }
+  if (p.status && (overflow || total > p.cap)) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
+}
+
 template <int KIND>
 hipError_t launch_kind(const ProbeParams &p, hipStream_t s) {
   // CCJ_WALK_ROWS (tuning override): rows per lane walked concurrently.
@@ -579,6 +742,23 @@ unsigned grid_for(uint64_t n, unsigned block) {
 }
 
 }  // namespace
+
+hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
+  if (p.n_chunks == 0) return hipSuccess;
+  const dim3 g((unsigned)p.n_chunks), b(kFlatThreads);
+  static const int win = [] {
+    const char *e = getenv("CCJ_FLAT_WIN");
+    return e ? atoi(e) : 2;
+  }();
+  if (kind == CCJ_TABLE_LP) {
+    if (win == 4) hipLaunchKernelGGL((probe_flat<CCJ_TABLE_LP, 4>), g, b, 0, s, p);
+    else hipLaunchKernelGGL((probe_flat<CCJ_TABLE_LP, 2>), g, b, 0, s, p);
+  } else {
+    if (win == 4) hipLaunchKernelGGL((probe_flat<CCJ_TABLE_CHAIN, 4>), g, b, 0, s, p);
+    else hipLaunchKernelGGL((probe_flat<CCJ_TABLE_CHAIN, 2>), g, b, 0, s, p);
+  }
+  return hipGetLastError();
+}
 
 hipError_t launch_probe(int kind, const ProbeParams &p, hipStream_t s) {
   if (p.n_chunks == 0) return hipSuccess;

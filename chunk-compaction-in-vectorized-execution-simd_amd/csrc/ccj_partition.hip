@@ -5,10 +5,12 @@
 //  - slot-range partitioning for the L2-resident probe (ccj_probe_partitioned): digits of the
 //    slot index h & (n_slots - 1) above the window bits, two LSD passes (low digit, then high).
 //
-// Each pass is a stable multisplit in two kernels: (1) per-tile digit counts, written digit-major;
-// (2) after an exclusive scan of those counts, every tile re-reads its keys and scatters them in
-// row order (ballot + mbcnt ranks inside a wave, LDS-scanned across the tile's waves).  Stability
-// makes the outputs deterministic and lets two LSD passes compose into a sort by (hi, lo).
+// Each pass is a multisplit in two kernels: (1) per-tile digit counts, written digit-major;
+// (2) after an exclusive scan of those counts, every tile re-reads its keys, builds an LDS image
+// of itself grouped by digit, and writes each digit segment whole.  The owner split ranks keys
+// stably (ballot + mbcnt), so the send buffers are deterministic; the slot split ranks them with
+// LDS atomics (grouping exact, order inside a tile's segment not), which is all the probe needs:
+// the second LSD pass still leaves every partition contiguous and its table window shared.
 #include <hipcub/hipcub.hpp>
 
 #include "ccj_internal.h"
@@ -17,8 +19,8 @@ namespace ccj {
 namespace {
 
 constexpr int kTileThreads = 256;
-constexpr int kTileIters = 32;
-constexpr uint64_t kTile = (uint64_t)kTileThreads * kTileIters;  // 8192 keys per tile
+constexpr int kTileIters = 16;
+constexpr uint64_t kTile = (uint64_t)kTileThreads * kTileIters;  // 4096 keys per tile
 
 struct Digit {
   uint32_t shift;  // >= 64: every key to digit 0
@@ -42,42 +44,88 @@ __global__ __launch_bounds__(kTileThreads) void part_count(const int64_t *keys, 
   if (threadIdx.x < parts) cnt[(uint64_t)threadIdx.x * n_tiles + tile] = s_cnt[threadIdx.x];
 }
 
-template <typename RowT>
+// Scatter of one tile: keys are ranked stably per digit (ballot + mbcnt inside a wave, LDS scan
+// across the tile's waves and iterations) into an LDS image of the tile sorted by digit, which is
+// then written out digit segment by digit segment: consecutive threads write consecutive
+// addresses of one segment, so every destination line is written whole (a direct scatter of
+// 8-byte stores to up to 64 destinations leaves partial lines in L2 and measured 2-3x slower).
+template <typename RowT, bool STABLE>
 __global__ __launch_bounds__(kTileThreads) void part_scatter(const int64_t *keys, const RowT *in_rows, uint64_t n,
                                                              uint32_t parts, Digit dg, uint64_t n_tiles,
-                                                             const uint64_t *off, uint64_t row_base,
-                                                             int64_t *out_keys, RowT *out_rows) {
-  __shared__ uint64_t s_base[kMaxParts];
+                                                             const uint64_t *cnt, const uint64_t *off,
+                                                             uint64_t row_base, int64_t *out_keys, RowT *out_rows) {
+  __shared__ int64_t s_k[kTile];
+  __shared__ RowT s_r[kTile];
+  __shared__ uint64_t s_glob[kMaxParts];
+  __shared__ uint32_t s_loc[kMaxParts], s_run[kMaxParts];
   __shared__ uint32_t s_wave[kTileThreads / 64][kMaxParts];
   const uint64_t tile = blockIdx.x;
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  if (threadIdx.x < parts) s_base[threadIdx.x] = off[(uint64_t)threadIdx.x * n_tiles + tile];
+  const uint64_t t0 = tile * kTile;
+  const uint32_t tn = (uint32_t)(n - t0 < kTile ? n - t0 : kTile);
+  if (threadIdx.x < parts) {
+    s_glob[threadIdx.x] = off[(uint64_t)threadIdx.x * n_tiles + tile];
+    s_run[threadIdx.x] = (uint32_t)cnt[(uint64_t)threadIdx.x * n_tiles + tile];
+  }
   __syncthreads();
-  for (int it = 0; it < kTileIters; ++it) {
-    const uint64_t i = tile * kTile + (uint64_t)it * kTileThreads + threadIdx.x;
-    const bool valid = i < n;
-    const int64_t k = valid ? keys[i] : 0;
-    const uint32_t d = valid ? dg(k) : 0xFFFFFFFFu;
-    uint32_t rank = 0;
-    for (uint32_t p = 0; p < parts; ++p) {
-      const uint64_t m = __ballot(d == p);
-      if (d == p) rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      if (lane == 0) s_wave[wave][p] = (uint32_t)__popcll(m);
+  if (threadIdx.x == 0) {  // local exclusive offsets of the digit segments inside the tile image
+    uint32_t acc = 0;
+    for (uint32_t d = 0; d < parts; ++d) {
+      s_loc[d] = acc;
+      acc += s_run[d];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < parts) s_run[threadIdx.x] = s_loc[threadIdx.x];
+  __syncthreads();
+  if (STABLE) {
+    for (int it = 0; it < kTileIters; ++it) {
+      const uint32_t li = (uint32_t)it * kTileThreads + threadIdx.x;
+      const bool valid = li < tn;
+      const int64_t k = valid ? keys[t0 + li] : 0;
+      const uint32_t d = valid ? dg(k) : 0xFFFFFFFFu;
+      uint32_t rank = 0;
+      for (uint32_t q = 0; q < parts; ++q) {
+        const uint64_t m = __ballot(d == q);
+        if (d == q) rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (lane == 0) s_wave[wave][q] = (uint32_t)__popcll(m);
+      }
+      __syncthreads();
+      if (valid) {
+        uint32_t pos = s_run[d] + rank;
+        for (uint32_t w = 0; w < wave; ++w) pos += s_wave[w][d];
+        s_k[pos] = k;
+        s_r[pos] = in_rows ? in_rows[t0 + li] : (RowT)(row_base + t0 + li);
+      }
+      __syncthreads();
+      if (threadIdx.x < parts) {
+        uint32_t t = 0;
+        for (uint32_t w = 0; w < kTileThreads / 64; ++w) t += s_wave[w][threadIdx.x];
+        s_run[threadIdx.x] += t;
+      }
+      __syncthreads();
+    }
+  } else {
+    // Unstable: the position inside a digit segment comes from an LDS atomic (one per key).
+    // Grouping is exact; the order inside a (tile, digit) segment is not reproducible.
+#pragma unroll 4
+    for (int it = 0; it < kTileIters; ++it) {
+      const uint32_t li = (uint32_t)it * kTileThreads + threadIdx.x;
+      if (li < tn) {
+        const int64_t k = keys[t0 + li];
+        const uint32_t pos = atomicAdd(&s_run[dg(k)], 1u);
+        s_k[pos] = k;
+        s_r[pos] = in_rows ? in_rows[t0 + li] : (RowT)(row_base + t0 + li);
+      }
     }
     __syncthreads();
-    if (valid) {
-      uint64_t pos = s_base[d] + rank;
-      for (uint32_t w = 0; w < wave; ++w) pos += s_wave[w][d];
-      out_keys[pos] = k;
-      out_rows[pos] = in_rows ? in_rows[i] : (RowT)(row_base + i);
-    }
-    __syncthreads();
-    if (threadIdx.x < parts) {
-      uint32_t t = 0;
-      for (uint32_t w = 0; w < kTileThreads / 64; ++w) t += s_wave[w][threadIdx.x];
-      s_base[threadIdx.x] += t;
-    }
-    __syncthreads();
+  }
+  for (uint32_t q = threadIdx.x; q < tn; q += kTileThreads) {
+    const int64_t k = s_k[q];
+    const uint32_t d = dg(k);
+    const uint64_t dest = s_glob[d] + (q - s_loc[d]);
+    out_keys[dest] = k;
+    out_rows[dest] = s_r[q];
   }
 }
 
@@ -104,7 +152,7 @@ size_t pass_workspace(uint64_t n, uint32_t parts) {
 }
 
 // One stable multisplit pass.  out_counts (digit totals) may be NULL.
-template <typename RowT>
+template <typename RowT, bool STABLE>
 hipError_t split_pass(const int64_t *keys, const RowT *in_rows, uint64_t n, uint32_t parts, Digit dg,
                       uint64_t row_base, int64_t *out_keys, RowT *out_rows, uint64_t *out_counts, void *ws,
                       hipStream_t s) {
@@ -122,8 +170,8 @@ hipError_t split_pass(const int64_t *keys, const RowT *in_rows, uint64_t n, uint
   if (e) return e;
   e = hipcub::DeviceScan::ExclusiveSum(w, tb, cnt, off, (int)m, s);
   if (e) return e;
-  hipLaunchKernelGGL((part_scatter<RowT>), dim3((unsigned)n_tiles), dim3(kTileThreads), 0, s, keys, in_rows, n, parts,
-                     dg, n_tiles, off, row_base, out_keys, out_rows);
+  hipLaunchKernelGGL((part_scatter<RowT, STABLE>), dim3((unsigned)n_tiles), dim3(kTileThreads), 0, s, keys, in_rows, n, parts,
+                     dg, n_tiles, cnt, off, row_base, out_keys, out_rows);
   if (out_counts) hipLaunchKernelGGL(part_totals, dim3(1), dim3(64), 0, s, cnt, off, parts, n_tiles, out_counts);
   return hipGetLastError();
 }
@@ -142,7 +190,7 @@ hipError_t launch_partition(const int64_t *keys, uint64_t n, uint32_t parts, uin
                             uint64_t *out_rows, uint64_t *out_counts, void *ws, hipStream_t s) {
   const uint32_t lp = log2u(parts);
   const Digit dg{lp == 0 ? 64u : 64u - lp, parts - 1};
-  return split_pass<uint64_t>(keys, nullptr, n, parts, dg, row_base, out_keys, out_rows, out_counts, ws, s);
+  return split_pass<uint64_t, true>(keys, nullptr, n, parts, dg, row_base, out_keys, out_rows, out_counts, ws, s);
 }
 
 // ---- slot-range partitioning for the L2-resident probe ------------------------------------------
@@ -176,11 +224,11 @@ hipError_t launch_slot_partition(const int64_t *keys, uint64_t n, const SlotPlan
   w += (n * 4 + 255) & ~255ull;
   const Digit lo{pl.window_bits, (1u << pl.lo_bits) - 1};
   if (pl.hi_bits == 0)
-    return split_pass<uint32_t>(keys, nullptr, n, 1u << pl.lo_bits, lo, 0, out_keys, out_rows, nullptr, w, s);
+    return split_pass<uint32_t, false>(keys, nullptr, n, 1u << pl.lo_bits, lo, 0, out_keys, out_rows, nullptr, w, s);
   const Digit hi{pl.window_bits + pl.lo_bits, (1u << pl.hi_bits) - 1};
-  hipError_t e = split_pass<uint32_t>(keys, nullptr, n, 1u << pl.lo_bits, lo, 0, tk, tr, nullptr, w, s);
+  hipError_t e = split_pass<uint32_t, false>(keys, nullptr, n, 1u << pl.lo_bits, lo, 0, tk, tr, nullptr, w, s);
   if (e) return e;
-  return split_pass<uint32_t>(tk, tr, n, 1u << pl.hi_bits, hi, 0, out_keys, out_rows, nullptr, w, s);
+  return split_pass<uint32_t, false>(tk, tr, n, 1u << pl.hi_bits, hi, 0, out_keys, out_rows, nullptr, w, s);
 }
 
 }  // namespace ccj

@@ -149,7 +149,8 @@ int ccj_probe(const ccj_table *table, const ccj_probe_args *args, ccj_stream str
  * each partition's table window is read from L2 instead of as random HBM lines.  Outputs are
  * ccj_probe's, over the partitioned column: out_sel indexes partitioned positions, and
  * out_row_map[pos] gives the original row of partitioned position pos.  Same matches, payloads
- * and per-row multiplicities as ccj_probe (L1 + L2). */
+ * and per-row multiplicities as ccj_probe (L1 + L2); within a chunk the order is unspecified, so
+ * out_round_counts, out_pos and payload columns are not produced (must be NULL / 0). */
 size_t ccj_probe_partitioned_workspace_size(const ccj_table *table, uint64_t n_rows);
 int ccj_probe_partitioned(const ccj_table *table, const ccj_probe_args *args, uint32_t *out_row_map,
                           void *workspace, size_t workspace_bytes, ccj_stream stream);
