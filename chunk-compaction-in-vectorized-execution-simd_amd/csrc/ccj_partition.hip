@@ -108,14 +108,22 @@ __global__ __launch_bounds__(kTileThreads) void part_scatter(const int64_t *keys
   } else {
     // Unstable: the position inside a digit segment comes from an LDS atomic (one per key).
     // Grouping is exact; the order inside a (tile, digit) segment is not reproducible.
-#pragma unroll 4
+    // All of the tile's loads are issued before the first LDS atomic (latency hidden once).
+    int64_t kk[kTileIters];
+    RowT rr[kTileIters];
+#pragma unroll
+    for (int it = 0; it < kTileIters; ++it) {
+      const uint32_t li = (uint32_t)it * kTileThreads + threadIdx.x;
+      kk[it] = li < tn ? __builtin_nontemporal_load(keys + t0 + li) : 0;
+      rr[it] = li < tn ? (in_rows ? __builtin_nontemporal_load(in_rows + t0 + li) : (RowT)(row_base + t0 + li)) : 0;
+    }
+#pragma unroll
     for (int it = 0; it < kTileIters; ++it) {
       const uint32_t li = (uint32_t)it * kTileThreads + threadIdx.x;
       if (li < tn) {
-        const int64_t k = keys[t0 + li];
-        const uint32_t pos = atomicAdd(&s_run[dg(k)], 1u);
-        s_k[pos] = k;
-        s_r[pos] = in_rows ? in_rows[t0 + li] : (RowT)(row_base + t0 + li);
+        const uint32_t pos = atomicAdd(&s_run[dg(kk[it])], 1u);
+        s_k[pos] = kk[it];
+        s_r[pos] = rr[it];
       }
     }
     __syncthreads();
