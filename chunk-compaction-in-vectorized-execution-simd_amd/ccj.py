@@ -60,7 +60,17 @@ EXPORTS = ["ccj_last_error", "ccj_abi_version", "ccj_device_init", "ccj_table_bu
            "ccj_probe", "ccj_gen_uniform_keys", "ccj_probe_cost", "ccj_result_checksum",
            "ccj_compact_workspace_size", "ccj_compact", "ccj_partition_workspace_size", "ccj_partition_by_owner",
            "ccj_result_checksum_mapped", "ccj_gen_reference_keys", "ccj_table_set_payload",
-           "ccj_probe_partitioned_workspace_size", "ccj_probe_partitioned"]
+           "ccj_probe_partitioned_workspace_size", "ccj_probe_partitioned", "ccj_pipeline_create",
+           "ccj_pipeline_run", "ccj_pipeline_free", "ccj_pipeline_checksum"]
+
+MAX_JOINS = 8
+COMPACT_NONE, COMPACT_FULL = 0, 1
+
+
+class PipelineResult(C.Structure):
+    _fields_ = [("n_out", C.c_uint64), ("cols", C.c_void_p * MAX_JOINS), ("payload", C.c_void_p * MAX_JOINS),
+                ("chunks_in", C.c_uint64 * MAX_JOINS), ("rows_in", C.c_uint64 * MAX_JOINS),
+                ("rows_out", C.c_uint64 * MAX_JOINS)]
 
 
 def build(force: bool = False) -> str:
@@ -101,6 +111,10 @@ def lib():
         L.ccj_partition_by_owner.argtypes = [vp, u64, C.c_uint32, u64, vp, vp, vp, vp, C.c_size_t, vp]
         L.ccj_result_checksum_mapped.argtypes = [vp, vp, vp, u64, u64, C.c_uint32, vp, vp, vp]
         L.ccj_result_checksum.argtypes = [vp, vp, vp, u64, u64, C.c_uint32, u64, vp, vp]
+        L.ccj_pipeline_create.argtypes = [C.POINTER(vp), C.c_uint32, C.c_uint32, i32, C.POINTER(vp)]
+        L.ccj_pipeline_run.argtypes = [vp, C.POINTER(vp), u64, vp, C.POINTER(PipelineResult)]
+        L.ccj_pipeline_free.argtypes = [vp]
+        L.ccj_pipeline_checksum.argtypes = [C.POINTER(PipelineResult), C.c_uint32, vp, vp]
         _lib = L
     return _lib
 
@@ -356,3 +370,78 @@ class OwnerPartitioner:
                                            _ptr(self.rows), _ptr(self.counts), _ptr(self.ws), self.ws_bytes,
                                            _stream(stream)), "ccj_partition_by_owner")
         return self.keys, self.rows, self.counts
+
+
+_HIP = None
+
+
+def _d2h_i64(ptr, n):
+    """Copy n int64 from a raw device pointer the library owns (hipMemcpy; caller synchronised)."""
+    import numpy as np
+    global _HIP
+    out = np.empty(n, np.int64)
+    if n == 0:
+        return out
+    if _HIP is None:
+        _HIP = C.CDLL("libamdhip64.so")
+        _HIP.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    rc = _HIP.hipMemcpy(out.ctypes.data_as(C.c_void_p), C.c_void_p(ptr), n * 8, 2)  # hipMemcpyDeviceToHost
+    if rc != 0:
+        raise CCJError(f"hipMemcpy failed ({rc})")
+    return out
+
+
+class Pipeline:
+    """main.cpp's ExecutePipeline / FlushPipelineCache (main.cpp:119-191) over `tables`, join l
+    probing column l, with no compaction or the (fixed) NaiveCompactor between joins
+    (ccj_pipeline_run, include/ccj.h).  run() returns the result table as device columns."""
+
+    def __init__(self, tables, chunk: int, compact: bool):
+        self.tables = list(tables)  # keep the tables alive as long as the pipeline
+        self.joins = len(self.tables)
+        arr = (C.c_void_p * self.joins)(*[t._h.value for t in self.tables])
+        h = C.c_void_p()
+        check(lib().ccj_pipeline_create(arr, self.joins, chunk, COMPACT_FULL if compact else COMPACT_NONE,
+                                        C.byref(h)), "ccj_pipeline_create")
+        self.h = h
+        self.res = PipelineResult()
+
+    def run(self, cols, stream=None):
+        """cols: `joins` device int64 columns of equal length (the probe side, column-major)."""
+        assert len(cols) == self.joins
+        n = cols[0].numel()
+        arr = (C.c_void_p * self.joins)(*[c.data_ptr() for c in cols])
+        self._cols = cols
+        check(lib().ccj_pipeline_run(self.h, arr, n, _stream(stream), C.byref(self.res)), "ccj_pipeline_run")
+        return self.res
+
+    def stats(self):
+        r = self.res
+        return [dict(chunks_in=r.chunks_in[l], rows_in=r.rows_in[l], rows_out=r.rows_out[l])
+                for l in range(self.joins)]
+
+    def result_columns(self):
+        """The result table as numpy int64 columns in the sink's column order: the probe columns,
+        then per join a zero column (result column m, never written) and its payload."""
+        import numpy as np
+        import torch
+        torch.cuda.synchronize()
+        n = self.res.n_out
+        out = [_d2h_i64(self.res.cols[j], n) for j in range(self.joins)]
+        for l in range(self.joins):
+            out.append(np.zeros(n, np.int64))
+            out.append(_d2h_i64(self.res.payload[l], n))
+        return out
+
+    def checksum(self, stream=None):
+        import torch
+        acc = torch.zeros(2, dtype=torch.int64, device="cuda")
+        check(lib().ccj_pipeline_checksum(C.byref(self.res), self.joins, _ptr(acc), _stream(stream)),
+              "ccj_pipeline_checksum")
+        a = acc.cpu().tolist()
+        return a[0], a[1] & 0xFFFFFFFFFFFFFFFF
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.ccj_pipeline_free(self.h)
+            self.h = None

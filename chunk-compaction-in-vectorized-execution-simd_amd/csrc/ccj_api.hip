@@ -46,6 +46,15 @@ int check_device() {
   return CCJ_OK;
 }
 
+}  // namespace
+
+namespace ccj {
+int api_fail(int code, const std::string &msg) { return fail(code, msg); }
+int api_check_device() { return check_device(); }
+}  // namespace ccj
+
+namespace {
+
 uint64_t lp_num_slots(uint64_t n) {  // linear_probing_ht.cpp:5-6
   uint64_t s = 1;
   while (s < (n << 2)) s <<= 1;

@@ -59,6 +59,10 @@ struct ProbeParams {
   uint32_t n_pay;      // payload columns gathered (<= CCJ_MAX_PAYLOAD_COLS)
   uint32_t pay_stride; // payload columns stored per position
   int64_t *out_cols[CCJ_MAX_PAYLOAD_COLS];
+  // Pipeline input (ccj_pipeline, no-compaction mode): chunk c's rows start at chunk_base[c] of
+  // `keys` (sel must be NULL, counts required) and its outputs at out_base[c]; NULL = c*chunk, c*cap.
+  const uint64_t *chunk_base;
+  const uint64_t *out_base;
   uint32_t xcd_swizzle;  // 1: consecutive chunks go to the same XCD (L2 reuse of partitioned input)
   uint32_t ablate;       // timing-only ablations (CCJ_ABLATE env, never set in product calls)
 };
@@ -86,6 +90,10 @@ hipError_t launch_probe_cost(int kind, const int64_t *table, const uint32_t *off
 hipError_t launch_result_checksum(const uint32_t *count, const uint32_t *sel, const int64_t *payload,
                                   uint64_t n_chunks, uint64_t cap, uint32_t chunk, uint64_t row_base,
                                   const uint64_t *row_map, unsigned long long *acc, hipStream_t s);
+
+// Error reporting of the C ABI (ccj_api.hip): sets ccj_last_error() and returns code.
+int api_fail(int code, const std::string &msg);
+int api_check_device();
 
 size_t compact_workspace(uint64_t n_chunks, uint64_t cap, uint32_t chunk);
 hipError_t launch_compact(const ccj_compact_args &a, hipStream_t s);

@@ -73,7 +73,7 @@ template <int KIND>
 __device__ void rounds_generic(const ProbeParams &p, uint64_t c, uint64_t base, uint32_t nj, uint32_t act,
                                const int64_t *s_key, uint32_t &flags, uint64_t &total_out, uint32_t &rounds_out) {
   const uint32_t lane = threadIdx.x & (kWave - 1);
-  const uint64_t obase = c * p.cap;
+  const uint64_t obase = p.out_base ? p.out_base[c] : c * p.cap;
   uint64_t total = 0;
   uint32_t round = 0;
   while (true) {
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(kBlock) void probe_chunks(ProbeParams p) {
     const uint64_t n8 = p.n_chunks & ~7ull;
     if (c < n8) c = (c & 7) * (n8 >> 3) + (c >> 3);
   }
-  const uint64_t base = c * p.chunk;
+  const uint64_t base = p.chunk_base ? p.chunk_base[c] : c * p.chunk;
   const uint64_t rem = p.n_rows - base;
   const uint32_t phys = rem < p.chunk ? (uint32_t)rem : p.chunk;
   const uint32_t nj = (p.chunk + kWave - 1) / kWave;
@@ -355,7 +355,7 @@ __global__ __launch_bounds__(kBlock) void probe_chunks(ProbeParams p) {
       if (rounds > p.max_rounds) flags |= CCJ_FLAG_ROUND_OVERFLOW;
     }
     // Emit.
-    const uint64_t obase = c * p.cap;
+    const uint64_t obase = p.out_base ? p.out_base[c] : c * p.cap;
     for (uint32_t jb = wave; jb < nj; jb += kChunkWaves * kEmitRows) {
       uint32_t m[kEmitRows], rr[kEmitRows];
 #pragma unroll

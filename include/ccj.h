@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CCJ_ABI_VERSION 1
+#define CCJ_ABI_VERSION 2
 
 enum ccj_status {
   CCJ_OK = 0,
@@ -194,6 +194,45 @@ typedef struct ccj_compact_args {
 
 size_t ccj_compact_workspace_size(uint64_t n_chunks, uint64_t cap, uint32_t chunk);
 int ccj_compact(const ccj_compact_args *args, ccj_stream stream);
+
+/* ---- multi-join pipeline ------------------------------------------------------------------ */
+/* Replaces main.cpp's ExecutePipeline / FlushPipelineCache (main.cpp:119-191): a chain of joins,
+ * join l probing column l of its input with tables[l], and between joins either
+ *   CCJ_COMPACT_NONE: every Next result goes on to the next join as its own chunk (main.cpp
+ *                     :149-159 with no compactor; LP's empty Next results produce nothing), or
+ *   CCJ_COMPACT_FULL: the Next results pass through the NaiveCompactor first (compactor.cpp:5-41
+ *                     with the :36 fix, `Compactor` in setting.h), flushed at the end (:172-191).
+ * The device runs it join by join: join l probes ALL of its input chunks in one launch, in the
+ * order the reference's depth-first recursion would hand them to it, and its output is then
+ * concatenated (NONE) or compacted (FULL) into join l+1's chunks.  Both modes materialise the
+ * carried columns (DataChunk::Append, base.cpp:15-27); they differ in how rows are chunked, which
+ * is what the reference's compaction changes.  The result (the ResultCollector's table,
+ * main.cpp:125-128) is, per tuple in the reference's append order: the n_joins probe columns,
+ * then per join a zero column (result column m, never written by the reference) and its payload.
+ * Synchronises `stream` once per join (output sizes), so it is not graph-capturable. */
+#define CCJ_MAX_JOINS 8
+enum ccj_compact_mode { CCJ_COMPACT_NONE = 0, CCJ_COMPACT_FULL = 1 };
+typedef struct ccj_pipeline ccj_pipeline;
+typedef struct ccj_pipeline_result {
+  uint64_t n_out;                        /* result tuples */
+  const int64_t *cols[CCJ_MAX_JOINS];    /* device int64[n_out]: probe column j of each tuple */
+  const int64_t *payload[CCJ_MAX_JOINS]; /* device int64[n_out]: join l's payload (result column n_joins+2l+1) */
+  uint64_t chunks_in[CCJ_MAX_JOINS];     /* chunks probed by join l (probe workgroups) */
+  uint64_t rows_in[CCJ_MAX_JOINS];       /* tuples probed by join l */
+  uint64_t rows_out[CCJ_MAX_JOINS];      /* tuples produced by join l */
+} ccj_pipeline_result;
+/* tables[l] must outlive the pipeline; chunk = kBlockSize (1..2048). */
+int ccj_pipeline_create(const ccj_table *const *tables, uint32_t n_joins, uint32_t chunk, int compact_mode,
+                        ccj_pipeline **out);
+/* d_cols[j] = device int64[n_rows], the probe side (main.cpp:47-55's table, column-major).  Result
+ * buffers belong to the pipeline and stay valid until the next run or ccj_pipeline_free. */
+int ccj_pipeline_run(ccj_pipeline *pl, const int64_t *const *d_cols, uint64_t n_rows, ccj_stream stream,
+                     ccj_pipeline_result *res);
+int ccj_pipeline_free(ccj_pipeline *pl);
+/* Result verification: d_acc[0] += tuples, d_acc[1] += sum over tuples of fmix64(t), where
+ * t = 0x51ED27 folded over the tuple's columns k in order as t = fmix64(t ^ v_k) + k (the
+ * order-insensitive checksum host/pipeline_main.cpp and oracle/ref_driver.cpp print). */
+int ccj_pipeline_checksum(const ccj_pipeline_result *res, uint32_t n_joins, uint64_t *d_acc, ccj_stream stream);
 
 /* ---- multi-GPU owner partitioning --------------------------------------------------------- */
 /* The exchange step of the radix-partitioned multi-GPU join: splits a key column

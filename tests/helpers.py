@@ -78,3 +78,54 @@ def assert_trace_equal(got, want):
 def ref_keys(n, cf):
     from oracle import oracle as O
     return O.ref_build_keys(n, cf)
+
+
+def oracle_pipeline(tables, cols, B, compact, cap_factor, max_rounds=256):
+    """main.cpp's ExecutePipeline / FlushPipelineCache (main.cpp:119-191) restated join by join on
+    the oracle (TEST INFRASTRUCTURE): join l probes column l of every input chunk with the
+    oracle's L3 probe (round-major Next order), then the Next results, in pipeline order, either
+    become the next join's chunks one by one (no compaction) or are re-chunked by the oracle's
+    literal NaiveCompactor simulation (compact_plan, compactor.cpp:5-41 with the :36 fix).
+    Returns the result table's carried columns (probe columns, then one payload per join) in the
+    ResultCollector's append order."""
+    from oracle import oracle as O
+
+    carried = [np.asarray(c, np.int64) for c in cols]
+    counts = None  # chunk c = rows [c*B, c*B + counts[c]) of the carried arrays
+    for l, t in enumerate(tables):
+        out = t.probe(carried[l], B, counts=counts, cap_factor=cap_factor, max_rounds=max_rounds)
+        cap, R = out["cap"], out["max_rounds"]
+        seg_rows, seg_pay, seg_counts = [], [], []
+        for c in range(len(out["count"])):
+            src = c * cap
+            for r in range(int(out["rounds"][c])):
+                rc = int(out["round_counts"][c * R + r])
+                seg_rows.append(c * B + out["sel"][src:src + rc].astype(np.int64))
+                seg_pay.append(out["payload"][src:src + rc])
+                seg_counts.append(rc)
+                src += rc
+        rows = np.concatenate(seg_rows) if seg_rows else np.zeros(0, np.int64)
+        pay = np.concatenate(seg_pay) if seg_pay else np.zeros(0, np.int64)
+        stream = [c[rows] for c in carried] + [pay]
+        if compact:
+            dest, occ = O.compact_plan(np.array(seg_counts, np.uint32), B)
+            nxt = []
+            for col in stream:
+                a = np.zeros(len(occ) * B, np.int64)
+                a[dest.astype(np.int64)] = col
+                nxt.append(a)
+            carried, counts = nxt, occ.astype(np.uint32)
+        else:
+            keep = [k for k, n in enumerate(seg_counts) if n]
+            starts = np.concatenate([[0], np.cumsum(seg_counts)])
+            nxt = [np.zeros(len(keep) * B, np.int64) for _ in stream]
+            for i, k in enumerate(keep):
+                a, n = starts[k], seg_counts[k]
+                for q, col in enumerate(stream):
+                    nxt[q][i * B:i * B + n] = col[a:a + n]
+            carried, counts = nxt, np.array([seg_counts[k] for k in keep], np.uint32)
+        if counts.size == 0:
+            return [np.zeros(0, np.int64) for _ in range(len(cols) + len(tables))]
+    # result table in append order: chunk by chunk, its first counts[c] rows
+    idx = np.concatenate([np.arange(c * B, c * B + int(n)) for c, n in enumerate(counts)])
+    return [col[idx] for col in carried]

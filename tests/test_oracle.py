@@ -165,3 +165,27 @@ def test_compaction_closed_form_equals_sequential(B, seed):
     segs[rng.random(400) < 0.2] = B
     dest, _ = O.compact_plan(segs.astype(np.uint32), B)
     assert np.array_equal(closed_form_compaction(segs, B), dest.astype(np.int64))
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+@pytest.mark.parametrize("joins,n,rhs,cf,B", [(3, 3000, 500, 3, 128), (2, 2000, 300, 1, 2048), (1, 500, 40, 4, 64)])
+def test_oracle_pipeline_is_the_join(kind, joins, n, rhs, cf, B):
+    """The oracle's join-by-join pipeline (helpers.oracle_pipeline) yields exactly the multi-way
+    join: every LHS row appears prod_l multiplicity(col_l) times with payload_l = col_l, with or
+    without compaction (the two modes differ only in order)."""
+    from helpers import oracle_pipeline
+    cols = [O.uniform_keys(7 + j, 0, n, rhs + 1) for j in range(joins)]
+    tables = [O.Table(kind, O.ref_build_keys(rhs, cf)) for _ in range(joins)]
+    mult = np.ones(n, np.int64)
+    for c in cols:
+        mult *= np.array([O.ref_multiplicity(int(k), rhs, cf) for k in c])
+    res = {}
+    for compact in (False, True):
+        out = oracle_pipeline(tables, cols, B, compact, cap_factor=cf)
+        assert len(out[0]) == int(mult.sum())
+        for l in range(joins):
+            np.testing.assert_array_equal(out[joins + l], out[l])
+        res[compact] = sorted(zip(*[o.tolist() for o in out]))
+    assert res[False] == res[True]
+    want = sorted(tuple(int(c[i]) for c in cols) for i in range(n) for _ in range(int(mult[i])))
+    assert [r[:joins] for r in res[False]] == want

@@ -1,0 +1,124 @@
+"""The device multi-join pipeline (ccj_pipeline_run, include/ccj.h) against
+(1) the oracle's join-by-join restatement of main.cpp's ExecutePipeline (tests/helpers.py
+oracle_pipeline) — the whole result table, in order (L3), with and without compaction — and
+(2) the reference's own pipeline answers (tests/golden/known_answers.json pipe_cases) through the
+C++ driver's batched engine (host/pipeline_main.cpp --engine batched): count, order-insensitive
+checksum over every column, first result rows; plus the batched engine's full result order vs
+the per-chunk facade running the reference's recursion (--dump)."""
+import filecmp
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from helpers import known_answers, oracle_pipeline
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "chunk-compaction-in-vectorized-execution-simd_amd", "host", "ccj_pipeline")
+KA = known_answers()["pipe_cases"]
+CASES = [k for k in sorted(KA) if "naive_compact" not in k and "16M" not in k]
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    import torch
+    import ccj
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ccj.device_init(0)
+    return torch.device("cuda", 0)
+
+
+def _inputs(joins, n, rhs, seed):
+    from oracle import oracle as O
+    return [O.uniform_keys(seed + j, 0, n, rhs + 1) for j in range(joins)]
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+@pytest.mark.parametrize("compact", [False, True])
+@pytest.mark.parametrize("joins,n,rhs,cf,B", [(3, 20000, 4000, 3, 256), (2, 5000, 1000, 1, 2048),
+                                              (3, 3000, 200, 5, 64), (1, 777, 50, 2, 100), (4, 4096, 1500, 2, 512)])
+def test_pipeline_l3_vs_oracle(kind, compact, joins, n, rhs, cf, B):
+    import torch
+    import ccj
+    from oracle import oracle as O
+    dev = _dev()
+    cols = _inputs(joins, n, rhs, 11)
+    dt = [ccj.Table.reference(kind, rhs, cf, ccj.LAYOUT_REFERENCE) for _ in range(joins)]
+    ot = [O.Table(kind, O.ref_build_keys(rhs, cf)) for _ in range(joins)]
+    want = oracle_pipeline(ot, cols, B, compact, cap_factor=cf)
+    pl = ccj.Pipeline(dt, B, compact)
+    pl.run([torch.from_numpy(c).to(dev) for c in cols])
+    got = pl.result_columns()
+    got = got[:joins] + [got[joins + 2 * l + 1] for l in range(joins)]
+    assert pl.res.n_out == len(want[0])
+    for g, w in zip(got, want):
+        np.testing.assert_array_equal(g, w)
+    st = pl.stats()
+    assert st[0]["rows_in"] == n and st[-1]["rows_out"] == len(want[0])
+    # the multiset does not depend on compaction; compaction never adds chunks
+    n_chk, l2 = pl.checksum()
+    other = ccj.Pipeline(dt, B, not compact)
+    other.run([torch.from_numpy(c).to(dev) for c in cols])
+    assert other.checksum() == (n_chk, l2)
+    full, none = (pl, other) if compact else (other, pl)
+    assert all(f["chunks_in"] <= g["chunks_in"] for f, g in zip(full.stats(), none.stats()))
+
+
+def test_pipeline_empty_and_no_match():
+    import torch
+    import ccj
+    dev = _dev()
+    t = [ccj.Table.reference(1, 100, 1, ccj.LAYOUT_REFERENCE) for _ in range(2)]
+    for compact in (False, True):
+        pl = ccj.Pipeline(t, 256, compact)
+        pl.run([torch.zeros(0, dtype=torch.int64, device=dev)] * 2)
+        assert pl.res.n_out == 0
+        pl.run([torch.full((1000,), 10**9, dtype=torch.int64, device=dev)] * 2)  # no key matches
+        assert pl.res.n_out == 0 and pl.stats()[0]["rows_out"] == 0
+        assert pl.checksum() == (0, 0)
+
+
+def run_bin(spec, engine, dump=None):
+    args = [BIN, "--join-num", spec["joins"], "--chunk-factor", spec["cf"], "--lhs-size", spec["lhs"],
+            "--rhs-size", spec["rhs"], "--table", spec["kind"], "--compact", "full" if spec["compact"] else "none",
+            "--block-size", spec["B"], "--engine", engine]
+    if dump:
+        args += ["--dump", dump]
+    return subprocess.run([str(a) for a in args], capture_output=True, text=True, timeout=600)
+
+
+def parse(out):
+    res, head = {}, []
+    for line in out.splitlines():
+        t = line.split()
+        if t and t[0] == "PIPE":
+            res = {t[i]: int(t[i + 1]) for i in range(1, len(t), 2)}
+        elif t and t[0] == "ROW":
+            head.append([int(x) for x in t[1:]])
+    return res, head
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_batched_engine_matches_reference(name):
+    want = KA[name]
+    p = run_bin(want["spec"], "batched")
+    assert p.returncode == 0, p.stderr
+    res, head = parse(p.stdout)
+    assert res["n_out"] == want["n_out"]
+    assert res["l2"] == want["l2"]
+    assert head == want["head"]
+
+
+@pytest.mark.parametrize("name", [k for k in CASES if "200k" in k or "300k" in k])
+def test_batched_engine_order_equals_facade(name, tmp_path):
+    spec = KA[name]["spec"]
+    a, b = str(tmp_path / "facade.bin"), str(tmp_path / "batched.bin")
+    p = run_bin(spec, "facade", a)
+    assert p.returncode == 0, p.stderr
+    q = run_bin(spec, "batched", b)
+    assert q.returncode == 0, q.stderr
+    assert os.path.getsize(a) == KA[name]["n_out"] * 8 * 3 * spec["joins"]
+    assert filecmp.cmp(a, b, shallow=False)
