@@ -1,13 +1,16 @@
 #!/usr/bin/env python3
 """bench.py — probe throughput of the MI355X hash-join hot path (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c5] [--no-cpu]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|pipeline] [--no-cpu]
   N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 Step = one pass of the hot path over one batch:
   c2 (default; BASELINE configs[1]): LP table of 2^26 reference-generator keys (2 GiB, alpha 1/4),
       2^30 uniform probe keys in [0, 2^26) resident in HBM, chunk 2048 -> one ccj_probe launch
       (hash, probe rounds, ballot packs, payload) writing row ids + payloads + per-round counts.
+  pipeline: main.cpp's default 3-join pipeline (2e7 LHS rows, 2e6-key chaining tables, cf 1,
+      B 256, main.cpp's own mt19937(2) data) on the device (ccj_pipeline_run, host/ccj_pipeline
+      --engine batched) with the compactor between joins, no-compaction timed beside it.
   N > 1 (C4 shape, weak scaling): every rank owns the build keys with owner = h(k) >> (64-log2 N)
       and 2^30 probe keys of its own; a step = owner partition + RCCL all-to-all (xGMI) + local
       probe.
@@ -45,7 +48,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=["c2"])
+    ap.add_argument("--workload", default="c2", choices=["c2", "pipeline"])
+    ap.add_argument("--pipe-lhs", type=int, default=20000000)
+    ap.add_argument("--pipe-rhs", type=int, default=2000000)
+    ap.add_argument("--pipe-joins", type=int, default=3)
+    ap.add_argument("--pipe-block", type=int, default=256)
+    ap.add_argument("--pipe-table", default="chain", choices=["chain", "lp"])
     ap.add_argument("--n-build", type=int, default=1 << 26)
     ap.add_argument("--n-probe", type=int, default=1 << 30, help="probe keys per GPU")
     ap.add_argument("--chunk", type=int, default=2048)
@@ -70,11 +78,40 @@ def cpu_model():
     return platform.processor()
 
 
+REF_DRIVER = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
+
+
+def has_avx512():
+    try:
+        return "avx512f" in open("/proc/cpuinfo").read()
+    except OSError:
+        return False
+
+
+def reference_cpu(args, n):
+    """The reference's own LP Probe + Next loop (linear_probing_ht.cpp, compiled from its sources
+    into oracle/_ref/ref_driver by oracle/Makefile), single thread, on the first n keys of the
+    same probe stream; returns (tuples/s, seconds, matches, wall incl. build) or None."""
+    import subprocess
+    if not (os.path.exists(REF_DRIVER) and has_avx512()):
+        return None
+    t0 = time.perf_counter()
+    p = subprocess.run([REF_DRIVER, "bench", "lp", "next", str(args.chunk), str(args.n_build), "1", str(n),
+                        str(args.n_build), str(SEED)], capture_output=True, text=True, timeout=600)
+    if p.returncode != 0:
+        log(f"[cpu] reference driver failed: {p.stderr[-300:]}")
+        return None
+    t = p.stdout.split()
+    i = t.index("BENCH")
+    m, secs = int(t[i + 2]), float(t[i + 4])
+    return n / secs, secs, m, time.perf_counter() - t0
+
+
 def cpu_baseline(args):
-    """Our scalar C restatement of main.cpp's no-compact LP probe path (oracle/, 'port'), timed on
-    this box's host cores on a bounded sample of the same workload."""
+    """The reference's scalar CPU path timed on this box's host cores, on a bounded sample of the
+    same workload: the reference's own code (oracle/_ref, kind "reference", 1 core — it is
+    single-threaded) when it is present, plus our C restatement (oracle/, "port") multi-threaded."""
     from oracle import oracle as O
-    import numpy as np
 
     t0 = time.perf_counter()
     table = O.Table(O.LP, O.ref_build_keys(args.n_build, 1))
@@ -87,23 +124,108 @@ def cpu_baseline(args):
         m, l2 = table.probe_totals(keys, args.chunk, threads=threads)
         dt = time.perf_counter() - t0
         res[threads] = (n / dt, n, dt, m)
+    del table
     thr = args.cpu_threads
     v, n, dt, m = res[thr]
     v1, n1, dt1, _ = res[1]
-    return {
+    port = {
         "value": v, "unit": "probe tuples/s", "cores": thr, "kind": "port",
         "sample": (f"first {n} of the same 2^30-key uniform probe stream (seed {SEED}) against the same "
                    f"{args.n_build}-key LP table built on the host, chunk {args.chunk}, {thr} threads "
                    f"(one per contiguous chunk range), {dt:.2f} s; 1 thread on {n1} keys: "
                    f"{v1 / 1e6:.1f} M tuples/s ({dt1:.2f} s); table build {build_s:.1f} s untimed"),
         "single_thread_value": v1,
+    }
+    n_ref = args.cpu_sample // 2
+    ref = reference_cpu(args, n_ref)
+    if ref is None:
+        port.update(cpu_model=cpu_model(), nproc=os.cpu_count())
+        return port
+    rv, rs, rm, rwall = ref
+    return {
+        "value": rv, "unit": "probe tuples/s", "cores": 1, "kind": "reference",
+        "sample": (f"the reference's LPHashTable(2^26, 1) + Probe/Next loop (its sources compiled by "
+                   f"oracle/Makefile, -O3 AVX-512), one thread, on the first {n_ref} keys of the same "
+                   f"probe stream (seed {SEED}), chunk {args.chunk}: {rs:.2f} s timed, {rm} matches "
+                   f"(expected {n_ref}); table build + key generation untimed ({rwall - rs:.1f} s)"),
+        "matches_ok": rm == n_ref,
+        "port_multithread": port,
         "cpu_model": cpu_model(),
         "nproc": os.cpu_count(),
     }
 
 
+def bench_pipeline(args):
+    """main.cpp's pipeline on the device (host/ccj_pipeline --engine batched -> ccj_pipeline_run)
+    with and without compaction, and the reference's own pipeline on the host CPU, same data."""
+    import subprocess
+    binp = os.path.join(PKG, "host", "ccj_pipeline")
+    reps = args.warmup + args.steps
+    spec = [str(x) for x in ("--join-num", args.pipe_joins, "--chunk-factor", 1, "--lhs-size", args.pipe_lhs,
+                             "--rhs-size", args.pipe_rhs, "--table", args.pipe_table,
+                             "--block-size", args.pipe_block, "--engine", "batched", "--repeat", reps)]
+    runs = {}
+    for mode in ("full", "none"):
+        p = subprocess.run([binp] + spec + ["--compact", mode], capture_output=True, text=True, timeout=900)
+        if p.returncode != 0:
+            raise RuntimeError(f"ccj_pipeline failed: {p.stderr[-500:]}")
+        out = {}
+        for line in (p.stdout + p.stderr).splitlines():
+            t = line.split()
+            if t and t[0] == "PIPE":
+                out["n_out"], out["l2"] = int(t[2]), int(t[4])
+            elif t and t[0] == "TIMES":
+                out["times"] = [float(x) for x in t[1:]]
+            elif t and t[0] == "[join":
+                out.setdefault("joins", []).append({t[i]: int(t[i + 1]) for i in range(2, len(t), 2)})
+        tt = out["times"][args.warmup:]
+        out["s_per_step"] = sum(tt) / len(tt)
+        runs[mode] = out
+        log(f"[pipeline] {mode}: {out['s_per_step'] * 1e3:.2f} ms/step, n_out {out['n_out']}")
+    cpu, parity = None, {"n_out": runs["full"]["n_out"], "l2": hex(runs["full"]["l2"]),
+                         "modes_agree": runs["full"]["n_out"] == runs["none"]["n_out"]
+                         and runs["full"]["l2"] == runs["none"]["l2"]}
+    if not args.no_cpu and os.path.exists(REF_DRIVER) and has_avx512():
+        base = [REF_DRIVER, "pipeline", args.pipe_table, str(args.pipe_block), str(args.pipe_joins), "1",
+                str(args.pipe_lhs), str(args.pipe_rhs)]
+        ref = {}
+        for compact, count_only in ((0, 0), (0, 1), (2, 1)):
+            p = subprocess.run(base + [str(compact), str(count_only)], capture_output=True, text=True, timeout=900)
+            t = p.stdout.split()
+            ref[(compact, count_only)] = (int(t[t.index("n_out") + 1]), int(t[t.index("l2") + 1]),
+                                          float(t[t.index("seconds") + 1]))
+        n_ref, l2_ref, _ = ref[(0, 0)]
+        parity.update(expected_n_out=n_ref, l1_ok=n_ref == runs["full"]["n_out"], l2_ok=l2_ref == runs["full"]["l2"])
+        secs = ref[(2, 1)][2]
+        cpu = {"value": args.pipe_lhs / secs, "unit": "LHS tuples/s", "cores": 1, "kind": "reference",
+               "sample": (f"the whole workload: the reference's ExecutePipeline/FlushPipelineCache over its "
+                          f"own classes (compiled from its sources, oracle/_ref/ref_driver), one thread, "
+                          f"fixed compactor: {secs:.2f} s; no compaction: {ref[(0, 1)][2]:.2f} s "
+                          f"(main.cpp's timed region, result collection off)"),
+               "no_compact_value": args.pipe_lhs / ref[(0, 1)][2], "cpu_model": cpu_model()}
+    full, none = runs["full"], runs["none"]
+    line = {
+        "metric": "pipeline LHS tuples/s (main.cpp multi-join pipeline with chunk compaction)",
+        "value": args.pipe_lhs / full["s_per_step"], "unit": "LHS tuples/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": full["s_per_step"] * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic: main.cpp's own generator (mt19937(2), uniform_int_distribution<int>(0, rhs))",
+        "config": {"workload": (f"main.cpp pipeline: {args.pipe_joins} {args.pipe_table} joins, "
+                                f"{args.pipe_lhs} LHS / {args.pipe_rhs} RHS, cf 1, B {args.pipe_block}"),
+                   "compaction": "NaiveCompactor (fixed) between joins", "parallelism": "dp1"},
+        "no_compaction": {"ms_per_step": none["s_per_step"] * 1e3, "value": args.pipe_lhs / none["s_per_step"],
+                          "joins": none.get("joins")},
+        "joins": full.get("joins"),
+        "cpu_baseline": cpu,
+        "parity": parity,
+    }
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
+    if args.workload == "pipeline":  # runs the C++ driver in child processes
+        return bench_pipeline(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

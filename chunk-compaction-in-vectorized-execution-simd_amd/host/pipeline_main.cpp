@@ -130,13 +130,16 @@ double RunBatched(PipelineState &st, const vector<vector<Attribute>> &table, siz
            "ccj_pipeline_create");
   ccj_pipeline_result res{};
   double latency = 0;
+  fprintf(stderr, "TIMES");
   for (size_t r = 0; r < std::max<size_t>(repeat, 1); ++r) {
     HipCheck(hipDeviceSynchronize(), "sync");
     auto t0 = std::chrono::steady_clock::now();
     CcjCheck(ccj_pipeline_run(pl, (const int64_t *const *)d_cols.data(), n, nullptr, &res), "ccj_pipeline_run");
     HipCheck(hipDeviceSynchronize(), "sync");
     latency = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    fprintf(stderr, " %.6f", latency);
   }
+  fprintf(stderr, "\n");
   for (size_t l = 0; l < joins; ++l)
     fprintf(stderr, "[join %zu] chunks_in %llu rows_in %llu rows_out %llu\n", l, (unsigned long long)res.chunks_in[l],
             (unsigned long long)res.rows_in[l], (unsigned long long)res.rows_out[l]);

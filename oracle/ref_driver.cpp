@@ -10,6 +10,7 @@
 //   pipeline        main.cpp:41-55 (data gen), :62-68 (tables), :79-102 (chunk loop),
 //                   :119-170 ExecutePipeline, :172-191 FlushPipelineCache
 // and prints per-Next traces / counts / checksums that tests/golden/make_golden.py stores.
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -155,9 +156,14 @@ struct Pipe {
   std::vector<std::unique_ptr<FixedCompactor>> fixed;
   uint64_t n_out = 0, l2 = 0;
   size_t ncols_out = 0;
+  bool count_only = false;  // timing runs: main.cpp's ResultCollector without flag_collect_tuples
   std::vector<std::vector<int64_t>> head;
 
   void Sink(DataChunk &c) {
+    if (count_only) {
+      n_out += c.count_;
+      return;
+    }
     for (size_t i = 0; i < c.count_; ++i) {
       uint32_t s = c.selection_vector_[i];
       // order-insensitive tuple checksum over every column of the final result
@@ -217,7 +223,7 @@ struct Pipe {
   }
 };
 
-int RunPipeline(size_t joins, size_t cf, size_t lhs, size_t rhs, int compact, bool use_lp) {
+int RunPipeline(size_t joins, size_t cf, size_t lhs, size_t rhs, int compact, bool use_lp, bool count_only) {
   kJoins = joins;
   ccj_mt19937 gen;
   ccj_mt19937_seed(&gen, 2);  // main.cpp:43 std::mt19937 gen(2)
@@ -230,6 +236,7 @@ int RunPipeline(size_t joins, size_t cf, size_t lhs, size_t rhs, int compact, bo
     table.AppendTuple(tuple);
   }
   Pipe p;
+  p.count_only = count_only;
   p.compact = compact;
   p.use_lp = use_lp;
   p.inter.resize(joins);
@@ -243,14 +250,20 @@ int RunPipeline(size_t joins, size_t cf, size_t lhs, size_t rhs, int compact, bo
     p.fixed.push_back(std::make_unique<FixedCompactor>(types));
   }
   size_t start = 0, end;
+  double secs = 0;  // main.cpp:92-101: only ExecutePipeline and the final flush are timed
   do {
     end = std::min(start + kBlockSize, lhs);
     DataChunk chunk = table.FetchChunk(start, end);
     start = end;
+    auto t0 = std::chrono::steady_clock::now();
     p.Exec(chunk, 0);
+    secs += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   } while (end < lhs);
+  auto t0 = std::chrono::steady_clock::now();
   if (compact) p.Flush(0);
+  secs += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   printf("PIPE n_out %llu l2 %llu\n", (unsigned long long)p.n_out, (unsigned long long)p.l2);
+  printf("TIME seconds %.6f\n", secs);
   for (auto &t : p.head) {
     printf("ROW");
     for (auto v : t) printf(" %lld", (long long)v);
@@ -259,10 +272,48 @@ int RunPipeline(size_t joins, size_t cf, size_t lhs, size_t rhs, int compact, bo
   return 0;
 }
 
+// Timed probe loop of simd_micro_bench.cpp:92-106 shape over a pre-generated key column (the
+// key generation and the per-chunk column fill stand in for DataCollection::FetchChunk and are
+// untimed, as in main.cpp:88-94): Probe + while (HasNext) Next, counting matches only.
+template <typename Table>
+void BenchProbe(Table &ht, Variant v, size_t n_probe, uint64_t range, uint64_t seed) {
+  std::vector<int64_t> keys(n_probe);
+  for (size_t i = 0; i < n_probe; ++i) keys[i] = ccj_uniform_key(seed, i, range);
+  std::vector<AttributeType> in_types{AttributeType::INTEGER};
+  std::vector<AttributeType> out_types{AttributeType::INTEGER, AttributeType::INTEGER, AttributeType::INTEGER};
+  DataChunk input(in_types);
+  DataChunk output(out_types);
+  uint64_t matches = 0;
+  double secs = 0;
+  for (size_t start = 0; start < n_probe; start += kBlockSize) {
+    const size_t n = std::min(kBlockSize, n_probe - start);
+    Vector &col = input.data_[0];
+    for (size_t i = 0; i < n; ++i) col.GetValue(i) = keys[start + i];
+    input.Reset();
+    input.count_ = n;
+    auto t0 = std::chrono::steady_clock::now();
+    const bool simd_probe = (v == kSimdNext || v == kSimdInOne);
+    auto ss = simd_probe ? ht.SIMDProbe(col, n, input.selection_vector_) : ht.Probe(col, n, input.selection_vector_);
+    while (ss.HasNext()) {
+      switch (v) {
+        case kNext: ss.Next(col, input, output); break;
+        case kInOne: ss.InOneNext(col, input, output); break;
+        case kSimdNext: ss.SIMDNext(col, input, output); break;
+        default: ss.SIMDInOneNext(col, input, output); break;
+      }
+      matches += output.count_;
+    }
+    secs += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  printf("BENCH matches %llu seconds %.6f tuples_per_s %.1f\n", (unsigned long long)matches, secs,
+         secs > 0 ? n_probe / secs : 0.0);
+}
+
 void Usage() {
   fprintf(stderr,
           "ref_driver probe <lp|chain> <next|inone|simdnext|simdinone> B n_build cf n_probe range seed gen selmode trace\n"
-          "ref_driver pipeline <lp|chain> B joins cf lhs rhs compact\n");
+          "ref_driver pipeline <lp|chain> B joins cf lhs rhs compact [count_only]\n"
+          "ref_driver bench <lp|chain> <next|inone|simdnext|simdinone> B n_build cf n_probe range seed\n");
   exit(2);
 }
 
@@ -299,11 +350,29 @@ int main(int argc, char **argv) {
     return 0;
   }
   if (cmd == "pipeline") {
-    if (argc != 9) Usage();
+    if (argc != 9 && argc != 10) Usage();
     bool lp = !strcmp(argv[2], "lp");
     kBlockSize = strtoull(argv[3], nullptr, 10);
     return RunPipeline(strtoull(argv[4], nullptr, 10), strtoull(argv[5], nullptr, 10),
-                       strtoull(argv[6], nullptr, 10), strtoull(argv[7], nullptr, 10), atoi(argv[8]), lp);
+                       strtoull(argv[6], nullptr, 10), strtoull(argv[7], nullptr, 10), atoi(argv[8]), lp,
+                       argc > 9 && atoi(argv[9]) != 0);
+  }
+  if (cmd == "bench") {
+    if (argc != 10) Usage();
+    const bool lp = !strcmp(argv[2], "lp");
+    const Variant v = ParseVariant(argv[3]);
+    kBlockSize = strtoull(argv[4], nullptr, 10);
+    const size_t n_build = strtoull(argv[5], nullptr, 10), cf = strtoull(argv[6], nullptr, 10);
+    const size_t n_probe = strtoull(argv[7], nullptr, 10);
+    const uint64_t range = strtoull(argv[8], nullptr, 10), seed = strtoull(argv[9], nullptr, 10);
+    if (lp) {
+      LPHashTable ht(n_build, cf);
+      BenchProbe(ht, v, n_probe, range, seed);
+    } else {
+      HashTable ht(n_build, cf);
+      BenchProbe(ht, v, n_probe, range, seed);
+    }
+    return 0;
   }
   Usage();
 }
