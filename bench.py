@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2", choices=["c2", "pipeline"])
+    ap.add_argument("--batches", type=int, default=4, help="N > 1: exchange batches per step (pipelined)")
+    ap.add_argument("--sharded", action="store_true", help="run the N > 1 protocol even at N = 1 (rehearsal)")
     ap.add_argument("--pipe-lhs", type=int, default=20000000)
     ap.add_argument("--pipe-rhs", type=int, default=2000000)
     ap.add_argument("--pipe-joins", type=int, default=3)
@@ -222,6 +224,21 @@ def bench_pipeline(args):
     print(json.dumps(line), flush=True)
 
 
+class _StdoutToStderr:
+    """Route fd 1 to stderr while RCCL creates its communicator (it prints a banner on stdout;
+    the driver reads bench.py's stdout as one JSON line)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def main():
     args = parse()
     if args.workload == "pipeline":  # runs the C++ driver in child processes
@@ -234,15 +251,22 @@ def main():
     torch.cuda.set_device(local)
     ccj.device_init(local)
     dist = None
-    if world > 1:
+    if world > 1 or args.sharded:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        with _StdoutToStderr():
+            if world == 1:
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                os.environ.setdefault("MASTER_PORT", "29533")
+                dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.barrier()  # creates the communicator (and its banner) now
     dev = torch.device("cuda", local)
     stream = torch.cuda.Stream(device=dev)
 
     n_build, n_probe, chunk = args.n_build, args.n_probe, args.chunk
     layout = ccj.LAYOUT_DEVICE if args.layout == "device" else ccj.LAYOUT_REFERENCE
-    if world > 1:
+    if world > 1 or args.sharded:
         return bench_multi(args, world, rank, local, dev, stream, dist)
 
     # ---- setup (untimed, as the reference builds before its timer: main.cpp:62-68 vs :92-94) ----
@@ -365,43 +389,54 @@ def main():
 
 def bench_multi(args, world, rank, local, dev, stream, dist):
     """C4 shape, weak scaling: each rank owns 1/N of a build side of n_build * N reference keys
-    (owner = top log2(N) hash bits) and probes 2^30 keys of its own; a step = owner partition +
-    RCCL all-to-all of (key, row) + local probe of what it received."""
+    (owner = top log2(N) hash bits) and probes 2^30 keys of its own; a step = batched owner
+    partition + RCCL all-to-all of (key, u32 row) + local probe, pipelined on two streams
+    (ccj_dist.ShardedProbe)."""
     import ccj_dist
     n_build_total = args.n_build * world
     n_probe, chunk = args.n_probe, args.chunk
     t0 = time.perf_counter()
     with torch.cuda.stream(stream):
-        sp = ccj_dist.ShardedProbe(n_build_total, 1, n_probe, chunk, world, rank, stream=stream)
+        sp = ccj_dist.ShardedProbe(n_build_total, 1, n_probe, chunk, world, rank, stream=stream,
+                                   batches=args.batches)
         keys = ccj.gen_uniform_keys(n_probe, SEED, n_build_total, first_row=rank * n_probe, stream=stream)
     torch.cuda.synchronize()
-    log(f"[rank {rank}] setup {time.perf_counter() - t0:.1f} s, local build {sp.n_build_local}")
+    log(f"[rank {rank}] setup {time.perf_counter() - t0:.1f} s, local build {sp.n_build_local}, "
+        f"{sp.batches} batches, segment capacity {sp.seg_cap}")
     for _ in range(args.warmup):
         sp.step(keys, rank * n_probe)
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
+    sp.probe_events.clear()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        sp.step(keys, rank * n_probe)
+        sp.step(keys, rank * n_probe, timing=True)
     torch.cuda.synchronize()
     dist.barrier()
     wall = time.perf_counter() - t0
     t = torch.tensor([wall], device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall = float(t.item())
+    probe_ms = sum(a.elapsed_time(b) for a, b in sp.probe_events) / args.steps
+    exact_fallback = sp.last_exact
     # verification (untimed): global L1 / L2 against the exact membership answer
-    out = sp.last
-    m, l2 = ccj.result_checksum(out, chunk, row_map=sp.recv_rows, stream=stream)
+    m, l2 = sp.step(keys, rank * n_probe, verify=True)
+    rk = sp.received_keys(sp.batches - 1)
+    examined, _ = sp.table.probe_cost(rk, stream=stream)
+    s_bar = examined / max(rk.numel(), 1)
     tot = torch.tensor([m, l2 - (1 << 64) if l2 >= (1 << 63) else l2], dtype=torch.int64, device=dev)
     dist.all_reduce(tot)
     m_all, l2_all = int(tot[0].item()), int(tot[1].item()) % (1 << 64)
-    parity = {"matches": m_all, "l2": hex(l2_all)}
+    parity = {"matches": m_all, "l2": hex(l2_all), "exact_size_fallback": exact_fallback}
     if not args.no_verify and rank == 0:
         from oracle import oracle as O
         want_m, want_l2 = O.count_uniform(SEED, 0, world * n_probe, n_build_total, n_build_total, 1,
                                           threads=args.cpu_threads)
         parity.update(expected_matches=want_m, l1_ok=want_m == m_all, l2_ok=want_l2 == l2_all)
+    m_bar = m_all / (world * n_probe)
+    alg = 8 + 8 * s_bar + 12 * m_bar
+    achieved = alg * n_probe / (probe_ms * 1e-3) / 1e9
     if rank == 0:
         value = world * n_probe / (wall / args.steps)
         line = {
@@ -412,8 +447,11 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
             "config": {"workload": f"C4 shape: {world}xMI355X radix-partitioned LP join, {n_build_total} build / "
                                    f"{world * n_probe} probe int64, chunk=2048, RCCL all-to-all tuple shuffle",
                        "table": "linear_probing", "n_build_total": n_build_total, "n_probe_per_gpu": n_probe,
-                       "chunk": chunk, "parallelism": f"dp{world} (owner-partitioned)"},
-            "roofline": None,
+                       "chunk": chunk, "batches": sp.batches, "parallelism": f"dp{world} (owner-partitioned)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "probe_chunks<LP,2> (local probe of received tuples, rank 0)",
+                         "kernel_ms": probe_ms, "alg_bytes_per_tuple": alg, "s_bar": s_bar, "m_bar": m_bar},
             "cpu_baseline": None,
             "parity": parity,
         }

@@ -61,7 +61,8 @@ EXPORTS = ["ccj_last_error", "ccj_abi_version", "ccj_device_init", "ccj_table_bu
            "ccj_compact_workspace_size", "ccj_compact", "ccj_partition_workspace_size", "ccj_partition_by_owner",
            "ccj_result_checksum_mapped", "ccj_gen_reference_keys", "ccj_table_set_payload",
            "ccj_probe_partitioned_workspace_size", "ccj_probe_partitioned", "ccj_pipeline_create",
-           "ccj_pipeline_run", "ccj_pipeline_free", "ccj_pipeline_checksum"]
+           "ccj_pipeline_run", "ccj_pipeline_free", "ccj_pipeline_checksum", "ccj_partition_by_owner_fixed",
+           "ccj_segment_chunk_counts"]
 
 MAX_JOINS = 8
 COMPACT_NONE, COMPACT_FULL = 0, 1
@@ -111,6 +112,9 @@ def lib():
         L.ccj_partition_by_owner.argtypes = [vp, u64, C.c_uint32, u64, vp, vp, vp, vp, C.c_size_t, vp]
         L.ccj_result_checksum_mapped.argtypes = [vp, vp, vp, u64, u64, C.c_uint32, vp, vp, vp]
         L.ccj_result_checksum.argtypes = [vp, vp, vp, u64, u64, C.c_uint32, u64, vp, vp]
+        L.ccj_partition_by_owner_fixed.argtypes = [vp, u64, C.c_uint32, C.c_uint32, u64, vp, vp, vp, vp, vp,
+                                                   C.c_size_t, vp]
+        L.ccj_segment_chunk_counts.argtypes = [vp, C.c_uint32, u64, C.c_uint32, vp, vp, vp]
         L.ccj_pipeline_create.argtypes = [C.POINTER(vp), C.c_uint32, C.c_uint32, i32, C.POINTER(vp)]
         L.ccj_pipeline_run.argtypes = [vp, C.POINTER(vp), u64, vp, C.POINTER(PipelineResult)]
         L.ccj_pipeline_free.argtypes = [vp]
@@ -281,6 +285,14 @@ class Table:
         return out
 
     def _args(self, keys, chunk, sel, counts, out):
+        # host-side shape checks: the kernel trusts these sizes (no out-of-bounds reads/writes)
+        n_chunks = (keys.numel() + chunk - 1) // chunk
+        if counts is not None and counts.numel() < n_chunks:
+            raise CCJError(f"counts has {counts.numel()} entries for {n_chunks} chunks")
+        if sel is not None and sel.numel() < (n_chunks * chunk if counts is not None else keys.numel()):
+            raise CCJError("sel shorter than the chunked key column")
+        if out["count"].numel() < n_chunks or out["sel"].numel() < n_chunks * out["cap"]:
+            raise CCJError("probe output buffers smaller than the input needs")
         a = ProbeArgs(keys=_ptr(keys).value, sel=_ptr(sel).value if sel is not None else None,
                       counts=_ptr(counts).value if counts is not None else None, n_rows=keys.numel(), chunk=chunk,
                       max_rounds=out["max_rounds"], cap=out["cap"], out_count=_ptr(out["count"]).value,
@@ -370,6 +382,31 @@ class OwnerPartitioner:
                                            _ptr(self.rows), _ptr(self.counts), _ptr(self.ws), self.ws_bytes,
                                            _stream(stream)), "ccj_partition_by_owner")
         return self.keys, self.rows, self.counts
+
+
+class FixedOwnerPartitioner:
+    """Fixed-capacity owner partitioning (ccj_partition_by_owner_fixed): destination d's keys and
+    u32 rows at [d*seg_cap, d*seg_cap + count_d), so an all-to-all needs no host-side sizes."""
+
+    def __init__(self, n: int, parts: int, seg_cap: int, device=None):
+        import torch
+        dev = device or torch.device("cuda", torch.cuda.current_device())
+        self.n, self.parts, self.seg_cap = n, parts, seg_cap
+        self.ws_bytes = lib().ccj_partition_workspace_size(n, parts)
+        self.ws = torch.empty(max(self.ws_bytes, 8), dtype=torch.uint8, device=dev)
+
+    def __call__(self, keys, row_base, out_keys, out_rows, out_counts, status, stream=None):
+        assert keys.numel() == self.n and out_keys.numel() >= self.parts * self.seg_cap
+        check(lib().ccj_partition_by_owner_fixed(_ptr(keys), self.n, self.parts, row_base, self.seg_cap,
+                                                 _ptr(out_keys), _ptr(out_rows), _ptr(out_counts), _ptr(status),
+                                                 _ptr(self.ws), self.ws_bytes, _stream(stream)),
+              "ccj_partition_by_owner_fixed")
+
+
+def segment_chunk_counts(seg_counts, seg_cap: int, chunk: int, out, status, stream=None):
+    check(lib().ccj_segment_chunk_counts(_ptr(seg_counts), seg_counts.numel(), seg_cap, chunk, _ptr(out),
+                                         _ptr(status), _stream(stream)), "ccj_segment_chunk_counts")
+    return out
 
 
 _HIP = None

@@ -272,8 +272,22 @@ int build_lp_device(const int64_t *d_keys, uint64_t n, hipStream_t s, uint64_t k
   t->info.n_keys = n;
   t->info.size = size;
   t->info.max_rounds = (uint32_t)best;
-  // all copies of a key share a home slot, so they sit in one run: multiplicity <= longest run.
-  t->info.max_dup = known_dup ? known_dup : best;
+  // Largest multiplicity of one key: it sizes every probe output (cap = chunk * max_dup).
+  uint64_t dup = known_dup;
+  if (!dup && n) {
+    uint32_t *d_dup = nullptr, h_dup = 0;
+    e = hipMalloc(&d_dup, sizeof(uint32_t));
+    if (e == hipSuccess) e = ccj::launch_lp_max_dup(t->d_table, size, (uint32_t)std::min<uint64_t>(best, size), d_dup, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(&h_dup, d_dup, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (d_dup) (void)hipFree(d_dup);
+    if (e != hipSuccess) {
+      cleanup();
+      return hip_fail(e, "device LP build (max dup)");
+    }
+    dup = h_dup;
+  }
+  t->info.max_dup = dup ? dup : 1;
   t->info.d_table = t->d_table;
   (void)hipGetDevice(&t->device);
   *out = t.release();
@@ -504,6 +518,34 @@ int ccj_partition_by_owner(const int64_t *d_keys, uint64_t n, uint32_t parts, ui
   HIP_TRY(ccj::launch_partition(d_keys, n, parts, row_base, d_out_keys, d_out_rows, d_out_counts, d_workspace,
                                 (hipStream_t)stream),
           "partition launch");
+  return CCJ_OK;
+}
+
+int ccj_partition_by_owner_fixed(const int64_t *d_keys, uint64_t n, uint32_t parts, uint32_t row_base,
+                                 uint64_t seg_cap, int64_t *d_out_keys, uint32_t *d_out_rows, uint64_t *d_out_counts,
+                                 uint32_t *d_status, void *d_workspace, size_t workspace_bytes, ccj_stream stream) {
+  if (parts == 0 || parts > ccj::kMaxParts || (parts & (parts - 1)))
+    return fail(CCJ_ERR_INVALID, "ccj_partition_by_owner_fixed: parts must be a power of two <= 64");
+  if (seg_cap == 0) return fail(CCJ_ERR_INVALID, "ccj_partition_by_owner_fixed: seg_cap == 0");
+  if (!d_out_counts || !d_status || (n && (!d_keys || !d_out_keys || !d_out_rows || !d_workspace)))
+    return fail(CCJ_ERR_INVALID, "ccj_partition_by_owner_fixed: missing buffer");
+  if (workspace_bytes < ccj::partition_workspace(n, parts))
+    return fail(CCJ_ERR_INVALID, "ccj_partition_by_owner_fixed: workspace too small");
+  if ((uint64_t)row_base + n > (1ull << 32)) return fail(CCJ_ERR_LIMIT, "ccj_partition_by_owner_fixed: rows exceed u32");
+  HIP_TRY(ccj::launch_partition_fixed(d_keys, n, parts, row_base, seg_cap, d_out_keys, d_out_rows, d_out_counts,
+                                      d_status, d_workspace, (hipStream_t)stream),
+          "partition launch");
+  return CCJ_OK;
+}
+
+int ccj_segment_chunk_counts(const uint64_t *d_seg_counts, uint32_t n_segs, uint64_t seg_cap, uint32_t chunk,
+                             uint32_t *d_out_counts, uint32_t *d_status, ccj_stream stream) {
+  if (chunk == 0 || chunk > ccj::kMaxChunk || seg_cap % chunk)
+    return fail(CCJ_ERR_INVALID, "ccj_segment_chunk_counts: seg_cap must be a multiple of chunk (1..2048)");
+  if (n_segs && (!d_seg_counts || !d_out_counts)) return fail(CCJ_ERR_INVALID, "ccj_segment_chunk_counts: null");
+  HIP_TRY(ccj::launch_segment_chunk_counts(d_seg_counts, n_segs, seg_cap, chunk, d_out_counts, d_status,
+                                           (hipStream_t)stream),
+          "segment chunk counts");
   return CCJ_OK;
 }
 

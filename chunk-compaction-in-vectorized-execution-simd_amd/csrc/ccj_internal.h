@@ -81,6 +81,8 @@ hipError_t launch_scatter_payload(const int64_t *src, uint32_t n_cols, const uin
                                   int64_t *dst, hipStream_t s);
 // Per-segment run statistics of an LP slot array (segment = 4096 slots): 4 x uint32 per segment:
 // {leading run, trailing run, longest run, all occupied}.
+// Largest multiplicity of one key (max_run = longest occupied run bounds the walk).
+hipError_t launch_lp_max_dup(const int64_t *slots, uint64_t n_slots, uint32_t max_run, uint32_t *out, hipStream_t s);
 hipError_t launch_lp_runs(const int64_t *slots, uint64_t n_slots, uint32_t *seg_stats, hipStream_t s);
 constexpr uint64_t kRunSegment = 4096;
 hipError_t launch_gen_uniform(int64_t *out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t range,
@@ -108,6 +110,11 @@ SlotPlan slot_plan(uint64_t table_size);
 size_t slot_partition_workspace(uint64_t n, const SlotPlan &pl);
 hipError_t launch_slot_partition(const int64_t *keys, uint64_t n, const SlotPlan &pl, int64_t *out_keys,
                                  uint32_t *out_rows, void *ws, hipStream_t s);
+hipError_t launch_partition_fixed(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t row_base, uint64_t seg_cap,
+                                  int64_t *out_keys, uint32_t *out_rows, uint64_t *out_counts, uint32_t *status,
+                                  void *ws, hipStream_t s);
+hipError_t launch_segment_chunk_counts(const uint64_t *counts, uint32_t n_segs, uint64_t seg_cap, uint32_t chunk,
+                                       uint32_t *out, uint32_t *status, hipStream_t s);
 hipError_t launch_partition(const int64_t *keys, uint64_t n, uint32_t parts, uint64_t row_base, int64_t *out_keys,
                             uint64_t *out_rows, uint64_t *out_counts, void *ws, hipStream_t s);
 

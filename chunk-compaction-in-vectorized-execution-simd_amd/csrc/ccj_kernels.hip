@@ -822,6 +822,41 @@ hipError_t launch_result_checksum(const uint32_t *count, const uint32_t *sel, co
   return hipGetLastError();
 }
 
+namespace {
+// Largest multiplicity of one key in an LP slot array: all copies of a key share a home slot and
+// so sit in one run; the first copy counts the equal keys from itself to the run's end.
+__global__ void lp_max_dup(const int64_t *slots, uint64_t n_slots, uint32_t max_run, uint32_t *out) {
+  uint32_t best = 0;
+  const uint64_t mask = n_slots - 1;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_slots;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const int64_t k = slots[i];
+    if (k == -1) continue;
+    uint32_t c = 1;
+    for (uint32_t t = 1; t <= max_run; ++t) {
+      const int64_t v = slots[(i + t) & mask];
+      if (v == -1) break;
+      c += v == k;
+    }
+    best = c > best ? c : best;
+  }
+  for (int d = 32; d > 0; d >>= 1) {
+    const uint32_t o = (uint32_t)__shfl_xor((int)best, d);
+    best = o > best ? o : best;
+  }
+  if ((threadIdx.x & 63u) == 0 && best) atomicMax(out, best);
+}
+}  // namespace
+
+hipError_t launch_lp_max_dup(const int64_t *slots, uint64_t n_slots, uint32_t max_run, uint32_t *out, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(out, 0, sizeof(uint32_t), s);
+  if (e != hipSuccess || n_slots == 0) return e;
+  const uint64_t want = (n_slots + 255) / 256;
+  hipLaunchKernelGGL(lp_max_dup, dim3((unsigned)(want < 8192 ? want : 8192)), dim3(256), 0, s, slots, n_slots,
+                     max_run, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_lp_runs(const int64_t *slots, uint64_t n_slots, uint32_t *seg_stats, hipStream_t s) {
   const uint64_t n_seg = (n_slots + kRunSegment - 1) / kRunSegment;
   hipLaunchKernelGGL(lp_runs, dim3((unsigned)((n_seg + 3) / 4)), dim3(256), 0, s, slots, n_slots, seg_stats);

@@ -53,7 +53,8 @@ template <typename RowT, bool STABLE>
 __global__ __launch_bounds__(kTileThreads) void part_scatter(const int64_t *keys, const RowT *in_rows, uint64_t n,
                                                              uint32_t parts, Digit dg, uint64_t n_tiles,
                                                              const uint64_t *cnt, const uint64_t *off,
-                                                             uint64_t row_base, int64_t *out_keys, RowT *out_rows) {
+                                                             uint64_t row_base, int64_t *out_keys, RowT *out_rows,
+                                                             uint64_t stride, uint32_t *status) {
   __shared__ int64_t s_k[kTile];
   __shared__ RowT s_r[kTile];
   __shared__ uint64_t s_glob[kMaxParts];
@@ -64,8 +65,10 @@ __global__ __launch_bounds__(kTileThreads) void part_scatter(const int64_t *keys
   const uint64_t t0 = tile * kTile;
   const uint32_t tn = (uint32_t)(n - t0 < kTile ? n - t0 : kTile);
   if (threadIdx.x < parts) {
-    s_glob[threadIdx.x] = off[(uint64_t)threadIdx.x * n_tiles + tile];
-    s_run[threadIdx.x] = (uint32_t)cnt[(uint64_t)threadIdx.x * n_tiles + tile];
+    const uint64_t d = threadIdx.x;
+    // compact: digit segments back to back; fixed (stride > 0): digit d owns [d*stride, (d+1)*stride)
+    s_glob[d] = stride ? d * stride + (off[d * n_tiles + tile] - off[d * n_tiles]) : off[d * n_tiles + tile];
+    s_run[d] = (uint32_t)cnt[d * n_tiles + tile];
   }
   __syncthreads();
   if (threadIdx.x == 0) {  // local exclusive offsets of the digit segments inside the tile image
@@ -128,13 +131,19 @@ __global__ __launch_bounds__(kTileThreads) void part_scatter(const int64_t *keys
     }
     __syncthreads();
   }
+  bool dropped = false;
   for (uint32_t q = threadIdx.x; q < tn; q += kTileThreads) {
     const int64_t k = s_k[q];
     const uint32_t d = dg(k);
     const uint64_t dest = s_glob[d] + (q - s_loc[d]);
+    if (stride && dest >= (uint64_t)(d + 1) * stride) {  // destination segment full
+      dropped = true;
+      continue;
+    }
     out_keys[dest] = k;
     out_rows[dest] = s_r[q];
   }
+  if (dropped && status) atomicOr(status, CCJ_FLAG_CAP_OVERFLOW);
 }
 
 __global__ void part_totals(const uint64_t *cnt, const uint64_t *off, uint32_t parts, uint64_t n_tiles,
@@ -163,7 +172,7 @@ size_t pass_workspace(uint64_t n, uint32_t parts) {
 template <typename RowT, bool STABLE>
 hipError_t split_pass(const int64_t *keys, const RowT *in_rows, uint64_t n, uint32_t parts, Digit dg,
                       uint64_t row_base, int64_t *out_keys, RowT *out_rows, uint64_t *out_counts, void *ws,
-                      hipStream_t s) {
+                      hipStream_t s, uint64_t stride = 0, uint32_t *status = nullptr) {
   const uint64_t n_tiles = (n + kTile - 1) / kTile;
   const uint64_t m = n_tiles * parts;
   if (n == 0) return out_counts ? hipMemsetAsync(out_counts, 0, parts * 8, s) : hipSuccess;
@@ -179,7 +188,7 @@ hipError_t split_pass(const int64_t *keys, const RowT *in_rows, uint64_t n, uint
   e = hipcub::DeviceScan::ExclusiveSum(w, tb, cnt, off, (int)m, s);
   if (e) return e;
   hipLaunchKernelGGL((part_scatter<RowT, STABLE>), dim3((unsigned)n_tiles), dim3(kTileThreads), 0, s, keys, in_rows, n, parts,
-                     dg, n_tiles, cnt, off, row_base, out_keys, out_rows);
+                     dg, n_tiles, cnt, off, row_base, out_keys, out_rows, stride, status);
   if (out_counts) hipLaunchKernelGGL(part_totals, dim3(1), dim3(64), 0, s, cnt, off, parts, n_tiles, out_counts);
   return hipGetLastError();
 }
@@ -199,6 +208,43 @@ hipError_t launch_partition(const int64_t *keys, uint64_t n, uint32_t parts, uin
   const uint32_t lp = log2u(parts);
   const Digit dg{lp == 0 ? 64u : 64u - lp, parts - 1};
   return split_pass<uint64_t, true>(keys, nullptr, n, parts, dg, row_base, out_keys, out_rows, out_counts, ws, s);
+}
+
+hipError_t launch_partition_fixed(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t row_base, uint64_t seg_cap,
+                                  int64_t *out_keys, uint32_t *out_rows, uint64_t *out_counts, uint32_t *status,
+                                  void *ws, hipStream_t s) {
+  const uint32_t lp = log2u(parts);
+  const Digit dg{lp == 0 ? 64u : 64u - lp, parts - 1};
+  return split_pass<uint32_t, true>(keys, nullptr, n, parts, dg, row_base, out_keys, out_rows, out_counts, ws, s,
+                                    seg_cap, status);
+}
+
+namespace {
+// Chunk counts of fixed-capacity segments: segment g holds counts[g] live rows at the front of its
+// seg_cap slots; chunk j of segment g is rows [j*chunk, (j+1)*chunk) of it.
+__global__ void seg_chunk_counts(const uint64_t *counts, uint32_t n_segs, uint64_t seg_cap, uint32_t chunk,
+                                 uint32_t *out, uint32_t *status) {
+  const uint64_t per = seg_cap / chunk;
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= per * n_segs) return;
+  const uint64_t g = i / per, j = i - g * per;
+  uint64_t live = counts[g];
+  if (live > seg_cap) {
+    if (j == 0 && status) atomicOr(status, CCJ_FLAG_CAP_OVERFLOW);
+    live = seg_cap;
+  }
+  const uint64_t lo = j * chunk;
+  out[i] = live <= lo ? 0u : (uint32_t)(live - lo < chunk ? live - lo : chunk);
+}
+}  // namespace
+
+hipError_t launch_segment_chunk_counts(const uint64_t *counts, uint32_t n_segs, uint64_t seg_cap, uint32_t chunk,
+                                       uint32_t *out, uint32_t *status, hipStream_t s) {
+  const uint64_t n = seg_cap / chunk * n_segs;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(seg_chunk_counts, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, counts, n_segs, seg_cap,
+                     chunk, out, status);
+  return hipGetLastError();
 }
 
 // ---- slot-range partitioning for the L2-resident probe ------------------------------------------

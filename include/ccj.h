@@ -246,6 +246,21 @@ int ccj_partition_by_owner(const int64_t *d_keys, uint64_t n, uint32_t parts, ui
                            int64_t *d_out_keys, uint64_t *d_out_rows, uint64_t *d_out_counts,
                            void *d_workspace, size_t workspace_bytes, ccj_stream stream);
 
+/* Fixed-capacity form for a host-synchronisation-free exchange: destination d's keys and their
+ * u32 row ids (row_base + i) go to [d*seg_cap, d*seg_cap + count_d), so every all-to-all split is
+ * seg_cap and the send/receive sizes need no host round trip; d_out_counts gets the true counts.
+ * Rows of a destination beyond seg_cap are dropped and CCJ_FLAG_CAP_OVERFLOW is OR-ed into
+ * *d_status (the caller re-runs that batch with ccj_partition_by_owner). */
+int ccj_partition_by_owner_fixed(const int64_t *d_keys, uint64_t n, uint32_t parts, uint32_t row_base,
+                                 uint64_t seg_cap, int64_t *d_out_keys, uint32_t *d_out_rows, uint64_t *d_out_counts,
+                                 uint32_t *d_status, void *d_workspace, size_t workspace_bytes, ccj_stream stream);
+/* Probe chunk counts for n_segs received fixed-capacity segments (seg_cap a multiple of chunk):
+ * chunk j of segment g gets min(chunk, max(0, count_g - j*chunk)) live rows, so ccj_probe over the
+ * whole receive buffer (counts = this, sel = NULL) skips the padding.  count_g > seg_cap raises
+ * CCJ_FLAG_CAP_OVERFLOW. */
+int ccj_segment_chunk_counts(const uint64_t *d_seg_counts, uint32_t n_segs, uint64_t seg_cap, uint32_t chunk,
+                             uint32_t *d_out_counts, uint32_t *d_status, ccj_stream stream);
+
 /* ---- workload + measurement helpers (not on the reference's path) ------------------------- */
 /* Synthetic probe column: d_out[i] = SplitMix64(seed) output (first_row + i) mod range — the
  * stream of oracle/ccj_gen.h ccj_uniform_key, so any row can be regenerated on the host.

@@ -56,3 +56,90 @@ def test_sharded_join_on_one_gpu(parts):
         m_tot += m
         l2_tot = (l2_tot + l2) % (1 << 64)
     assert (m_tot, l2_tot) == O.count_uniform(seed, 0, n_probe, rng, n_build, cf)
+
+
+@pytest.mark.parametrize("parts,n,base", [(1, 1000, 0), (2, 100000, 7), (8, 123457, 1 << 20), (64, 50000, 3)])
+def test_partition_fixed_segments(parts, n, base):
+    """ccj_partition_by_owner_fixed: segment d holds exactly owner-d keys in row order (stable),
+    with u32 rows base + i, and the true counts."""
+    from ccj_dist import seg_capacity
+    keys = O.uniform_keys(parts + 11, 0, n, 1 << 40)
+    cap = seg_capacity(n, parts, 256)
+    fp = ccj.FixedOwnerPartitioner(n, parts, cap)
+    ok = torch.full((parts * cap,), -7, dtype=torch.int64, device="cuda")
+    orow = torch.zeros(parts * cap, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(parts, dtype=torch.int64, device="cuda")
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    fp(torch.from_numpy(keys).cuda(), base, ok, orow, cnt, st)
+    torch.cuda.synchronize()
+    owner = np_owner(keys, parts)
+    want_cnt = np.bincount(owner, minlength=parts)
+    assert int(st.item()) == 0
+    assert np.array_equal(cnt.cpu().numpy(), want_cnt)
+    k, r = ok.cpu().numpy(), orow.cpu().numpy()
+    for d in range(parts):
+        idx = np.nonzero(owner == d)[0]
+        assert np.array_equal(k[d * cap:d * cap + len(idx)], keys[idx])
+        assert np.array_equal(r[d * cap:d * cap + len(idx)], base + idx)
+        assert (k[d * cap + len(idx):(d + 1) * cap] == -7).all()  # padding untouched
+
+
+def test_partition_fixed_overflow_flags_and_stays_in_bounds():
+    n, parts, cap = 100000, 4, 1024  # far too small: most rows dropped
+    keys = O.uniform_keys(1, 0, n, 1 << 40)
+    fp = ccj.FixedOwnerPartitioner(n, parts, cap)
+    ok = torch.full((parts * cap + 64,), -7, dtype=torch.int64, device="cuda")
+    orow = torch.zeros(parts * cap + 64, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(parts, dtype=torch.int64, device="cuda")
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    fp(torch.from_numpy(keys).cuda(), 0, ok, orow, cnt, st)
+    torch.cuda.synchronize()
+    assert int(st.item()) & 1
+    assert (ok[parts * cap:].cpu().numpy() == -7).all()
+    owner = np_owner(keys, parts)
+    for d in range(parts):  # the kept prefix is still exactly the first `cap` owner-d rows
+        idx = np.nonzero(owner == d)[0][:cap]
+        assert np.array_equal(ok[d * cap:(d + 1) * cap].cpu().numpy(), keys[idx])
+
+
+def test_segment_chunk_counts():
+    cap, chunk = 4096, 1024
+    cnt = torch.tensor([0, 1, 1024, 1025, 4096, 5000], dtype=torch.int64, device="cuda")
+    out = torch.full((len(cnt) * cap // chunk,), 99, dtype=torch.int32, device="cuda")
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ccj.segment_chunk_counts(cnt, cap, chunk, out, st)
+    torch.cuda.synchronize()
+    want = [0, 0, 0, 0, 1, 0, 0, 0, 1024, 0, 0, 0, 1024, 1, 0, 0, 1024] + [1024] * 7
+    assert out.cpu().tolist() == want[:len(want)]
+    assert int(st.item()) & 1  # 5000 > cap
+
+
+@pytest.fixture(scope="module")
+def pg1():
+    """A one-rank RCCL process group: all-to-all degenerates to a copy, but the streams, events,
+    double buffering and the fallback path of ShardedProbe run as they do at N ranks."""
+    import os
+    import torch.distributed as dist
+    from test_dist_cpu import free_port
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    yield dist
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("batches", [1, 3, 4])
+def test_sharded_probe_pipelined_one_rank(pg1, batches):
+    import ccj_dist
+    n_build, n_probe = 1 << 20, 3 << 20
+    sp = ccj_dist.ShardedProbe(n_build, 1, n_probe, 2048, 1, 0, batches=batches)
+    keys = ccj.gen_uniform_keys(n_probe, 42, n_build + (n_build >> 2))
+    want = O.count_uniform(42, 0, n_probe, n_build + (n_build >> 2), n_build, 1)
+    for _ in range(2):
+        sp.step(keys, 0)
+    assert sp.step(keys, 0, verify=True) == want
+    assert not sp.last_exact
+    # force the overflow fallback: shrink the segment capacity below the batch size
+    sp._resize(2048)
+    assert sp.step(keys, 0, verify=True) == want
+    assert sp.last_exact

@@ -188,3 +188,21 @@ def test_partitioned_probe_same_rows_as_chunk_probe():
     oa = np.lexsort((pa, ra))
     ob = np.lexsort((pb, rb))
     assert np.array_equal(ra[oa], rb[ob]) and np.array_equal(pa[oa], pb[ob])
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_device_build_reports_exact_max_dup(kind):
+    """Probe outputs are sized by max_dup (cap = chunk * max_dup): a device-built table reports the
+    exact largest multiplicity of one key, not a bound."""
+    rng = np.random.default_rng(3)
+    base = rng.integers(0, 1 << 40, size=5000)
+    reps = rng.integers(1, 4, size=5000)
+    reps[1234] = 9
+    keys = np.repeat(base, reps)
+    rng.shuffle(keys)
+    t = ccj.Table.on_device(kind, torch.from_numpy(keys).cuda())
+    assert t.max_dup == 9
+    out = t.probe(torch.from_numpy(base).cuda(), 2048)
+    torch.cuda.synchronize()
+    assert int(out["status"].item()) == 0
+    assert int(out["count"].sum().item()) == int(reps.sum())
