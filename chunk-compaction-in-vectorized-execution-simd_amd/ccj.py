@@ -48,7 +48,7 @@ class ProbeArgs(C.Structure):
 class CompactArgs(C.Structure):
     _fields_ = [("count", C.c_void_p), ("sel", C.c_void_p), ("payload", C.c_void_p), ("rounds", C.c_void_p),
                 ("round_counts", C.c_void_p), ("n_chunks", C.c_uint64), ("cap", C.c_uint64),
-                ("max_rounds", C.c_uint32), ("chunk", C.c_uint32), ("n_cols", C.c_uint32), ("reserved", C.c_uint32),
+                ("max_rounds", C.c_uint32), ("chunk", C.c_uint32), ("n_cols", C.c_uint32), ("threshold", C.c_uint32),
                 ("cols", C.c_void_p * 16), ("out_cols", C.c_void_p * 16), ("out_payload", C.c_void_p),
                 ("out_row", C.c_void_p), ("out_chunk_counts", C.c_void_p), ("out_cap_rows", C.c_uint64),
                 ("out_n_chunks", C.c_void_p), ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t),
@@ -62,7 +62,7 @@ EXPORTS = ["ccj_last_error", "ccj_abi_version", "ccj_device_init", "ccj_table_bu
            "ccj_result_checksum_mapped", "ccj_gen_reference_keys", "ccj_table_set_payload",
            "ccj_probe_partitioned_workspace_size", "ccj_probe_partitioned", "ccj_pipeline_create",
            "ccj_pipeline_run", "ccj_pipeline_free", "ccj_pipeline_checksum", "ccj_partition_by_owner_fixed",
-           "ccj_segment_chunk_counts"]
+           "ccj_segment_chunk_counts", "ccj_pipeline_set_thresholds"]
 
 MAX_JOINS = 8
 COMPACT_NONE, COMPACT_FULL = 0, 1
@@ -71,7 +71,7 @@ COMPACT_NONE, COMPACT_FULL = 0, 1
 class PipelineResult(C.Structure):
     _fields_ = [("n_out", C.c_uint64), ("cols", C.c_void_p * MAX_JOINS), ("payload", C.c_void_p * MAX_JOINS),
                 ("chunks_in", C.c_uint64 * MAX_JOINS), ("rows_in", C.c_uint64 * MAX_JOINS),
-                ("rows_out", C.c_uint64 * MAX_JOINS)]
+                ("rows_out", C.c_uint64 * MAX_JOINS), ("level_ms", C.c_float * MAX_JOINS)]
 
 
 def build(force: bool = False) -> str:
@@ -105,7 +105,7 @@ def lib():
         L.ccj_gen_reference_keys.argtypes = [vp, u64, u64, u64, u64, vp]
         L.ccj_probe_cost.argtypes = [vp, vp, u64, vp, vp]
         L.ccj_compact_workspace_size.restype = C.c_size_t
-        L.ccj_compact_workspace_size.argtypes = [u64, u64, C.c_uint32]
+        L.ccj_compact_workspace_size.argtypes = [u64, u64, C.c_uint32, C.c_uint32, C.c_uint32]
         L.ccj_compact.argtypes = [C.POINTER(CompactArgs), vp]
         L.ccj_partition_workspace_size.restype = C.c_size_t
         L.ccj_partition_workspace_size.argtypes = [u64, C.c_uint32]
@@ -118,6 +118,7 @@ def lib():
         L.ccj_pipeline_create.argtypes = [C.POINTER(vp), C.c_uint32, C.c_uint32, i32, C.POINTER(vp)]
         L.ccj_pipeline_run.argtypes = [vp, C.POINTER(vp), u64, vp, C.POINTER(PipelineResult)]
         L.ccj_pipeline_free.argtypes = [vp]
+        L.ccj_pipeline_set_thresholds.argtypes = [vp, vp]
         L.ccj_pipeline_checksum.argtypes = [C.POINTER(PipelineResult), C.c_uint32, vp, vp]
         _lib = L
     return _lib
@@ -319,19 +320,24 @@ class Table:
 
 
 
-def compact(probe_out, chunk: int, cols=(), payload: bool = True, rows: bool = True, stream=None):
+def compact(probe_out, chunk: int, cols=(), payload: bool = True, rows: bool = True, stream=None,
+            threshold: int = 0):
     """Device compaction of a probe output's Next results (include/ccj.h ccj_compact).
 
     Returns dict(n_chunks (int), counts, cols [list], payload, row, status) — dense output chunks of
-    `chunk` rows in the (fixed) NaiveCompactor order.
+    `chunk` rows in the (fixed) NaiveCompactor order; with threshold T, results of >= T rows pass
+    through as their own chunk (0 = chunk: NaiveCompactor).
     """
     import torch
     dev = probe_out["count"].device
     n_chunks, cap = probe_out["n_chunks"], probe_out["cap"]
     if probe_out.get("round_counts") is None:
         raise CCJError("compact needs the probe's per-round counts (alloc_outputs(rounds=True))")
-    out_rows = ((n_chunks * cap + chunk - 1) // chunk + 1) * chunk
-    ws_bytes = lib().ccj_compact_workspace_size(n_chunks, cap, chunk)
+    out_chunks = (n_chunks * cap + chunk - 1) // chunk + 1
+    if 0 < threshold < chunk:  # pass-through chunks are not full: at most one per Next result
+        out_chunks += n_chunks * min(probe_out["max_rounds"], cap // threshold + 1)
+    out_rows = out_chunks * chunk
+    ws_bytes = lib().ccj_compact_workspace_size(n_chunks, cap, chunk, probe_out["max_rounds"], threshold)
     ws = torch.empty(max(ws_bytes, 8), dtype=torch.uint8, device=dev)
     o = dict(
         counts=torch.zeros(out_rows // chunk, dtype=torch.int32, device=dev),
@@ -348,6 +354,7 @@ def compact(probe_out, chunk: int, cols=(), payload: bool = True, rows: bool = T
     a.rounds, a.round_counts = _ptr(probe_out["rounds"]).value, _ptr(probe_out["round_counts"]).value
     a.n_chunks, a.cap, a.max_rounds, a.chunk = n_chunks, cap, probe_out["max_rounds"], chunk
     a.n_cols = len(cols)
+    a.threshold = threshold
     for i, col in enumerate(cols):
         a.cols[i] = col.data_ptr()
         a.out_cols[i] = o["cols"][i].data_ptr()
@@ -452,9 +459,14 @@ class Pipeline:
         check(lib().ccj_pipeline_run(self.h, arr, n, _stream(stream), C.byref(self.res)), "ccj_pipeline_run")
         return self.res
 
+    def set_thresholds(self, thresholds=None):
+        """Per-join pass-through thresholds of the compactors (None: NaiveCompactor everywhere)."""
+        arr = None if thresholds is None else (C.c_uint32 * self.joins)(*thresholds)
+        check(lib().ccj_pipeline_set_thresholds(self.h, arr), "ccj_pipeline_set_thresholds")
+
     def stats(self):
         r = self.res
-        return [dict(chunks_in=r.chunks_in[l], rows_in=r.rows_in[l], rows_out=r.rows_out[l])
+        return [dict(chunks_in=r.chunks_in[l], rows_in=r.rows_in[l], rows_out=r.rows_out[l], ms=r.level_ms[l])
                 for l in range(self.joins)]
 
     def result_columns(self):

@@ -476,9 +476,10 @@ int ccj_probe(const ccj_table *t, const ccj_probe_args *a, ccj_stream stream) {
   return CCJ_OK;
 }
 
-size_t ccj_compact_workspace_size(uint64_t n_chunks, uint64_t cap, uint32_t chunk) {
+size_t ccj_compact_workspace_size(uint64_t n_chunks, uint64_t cap, uint32_t chunk, uint32_t max_rounds,
+                                  uint32_t threshold) {
   if (chunk == 0) return 0;
-  return ccj::compact_workspace(n_chunks, cap, chunk);
+  return ccj::compact_workspace(n_chunks, cap, chunk, max_rounds, threshold);
 }
 
 int ccj_compact(const ccj_compact_args *a, ccj_stream stream) {
@@ -495,7 +496,7 @@ int ccj_compact(const ccj_compact_args *a, ccj_stream stream) {
   if (a->out_payload && !a->payload) return fail(CCJ_ERR_INVALID, "ccj_compact: out_payload needs payload");
   for (uint32_t q = 0; q < a->n_cols; ++q)
     if (!a->cols[q] || !a->out_cols[q]) return fail(CCJ_ERR_INVALID, "ccj_compact: null column");
-  if (a->workspace_bytes < ccj::compact_workspace(a->n_chunks, a->cap, a->chunk))
+  if (a->workspace_bytes < ccj::compact_workspace(a->n_chunks, a->cap, a->chunk, a->max_rounds, a->threshold))
     return fail(CCJ_ERR_INVALID, "ccj_compact: workspace too small");
   HIP_TRY(ccj::launch_compact(*a, (hipStream_t)stream), "compact launch");
   return CCJ_OK;

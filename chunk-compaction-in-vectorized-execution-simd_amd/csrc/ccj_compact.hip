@@ -5,10 +5,12 @@
 // a full result bypasses the cache (:6); an overflowing result tops the cache up, the cache is
 // emitted, and the rest becomes the new cache (:22-35).  That order is a closed form of two
 // prefix sums, so it runs in parallel:
-//   P-stream  = rows of the non-full results, concatenated in pipeline order (t = position in it)
-//   F_s       = full results before result s;  E(t) = t == 0 ? 0 : ceil(t / chunk) - 1
-//   full result s           -> output chunk E(t_s) + F_s
-//   P-row u (chunk k = u/B)  -> output chunk k + #{full s : E(t_s) <= k}, row u % B
+//   pass-through results: the non-empty ones of >= T rows (T = threshold; T = chunk: the
+//   reference's full-chunk rule, compactor.cpp:6)
+//   P-stream  = rows of the other results, concatenated in pipeline order (t = position in it)
+//   F_s       = pass-through results before result s;  E(t) = t == 0 ? 0 : ceil(t / chunk) - 1
+//   pass-through result s   -> output chunk E(t_s) + F_s (keeping its own row count)
+//   P-row u (chunk k = u/B)  -> output chunk k + #{pass-through s : E(t_s) <= k}, row u % B
 // Kernels: per-chunk segment sums -> exclusive scans (hipCUB) -> full-result E list -> one wave
 // per probe chunk copies its rows (DataChunk::Append's gather, base.cpp:15-27) -> chunk counts.
 #include <hipcub/hipcub.hpp>
@@ -25,6 +27,8 @@ struct CompactParams {
   uint64_t *totals;   // [2]: T_total, F_total
   uint32_t *fullE;    // [max full results]
   uint64_t max_full;
+  uint32_t thr;       // pass-through threshold (>= 1)
+  __device__ __forceinline__ bool bypass(uint32_t rc) const { return rc != 0 && rc >= thr; }
 };
 
 __global__ void seg_sums(CompactParams p) {
@@ -34,7 +38,7 @@ __global__ void seg_sums(CompactParams p) {
   uint64_t nf = 0, f = 0;
   for (uint32_t r = 0; r < rounds && r < p.a.max_rounds; ++r) {
     const uint32_t rc = p.a.round_counts[c * p.a.max_rounds + r];
-    if (rc == p.a.chunk) ++f;
+    if (p.bypass(rc)) ++f;
     else nf += rc;
   }
   p.nonfull[c] = nf;
@@ -61,8 +65,12 @@ __global__ void full_list(CompactParams p) {
   uint64_t t = p.nonfull[c], f = p.full[c];
   for (uint32_t r = 0; r < rounds && r < p.a.max_rounds; ++r) {
     const uint32_t rc = p.a.round_counts[c * p.a.max_rounds + r];
-    if (rc == p.a.chunk) {
-      if (f < p.max_full) p.fullE[f] = (uint32_t)e_of(t, p.a.chunk);
+    if (p.bypass(rc)) {
+      if (f < p.max_full) {
+        const uint64_t e = e_of(t, p.a.chunk);
+        p.fullE[f] = (uint32_t)e;
+        if ((e + f + 1) * p.a.chunk <= p.a.out_cap_rows) p.a.out_chunk_counts[e + f] = rc;  // its own count
+      }
       ++f;
     } else {
       t += rc;
@@ -94,7 +102,7 @@ __global__ __launch_bounds__(256) void copy_rows(CompactParams p) {
   const uint32_t total = p.a.count[c];
   for (uint32_t r = 0; r < rounds && r < p.a.max_rounds; ++r) {
     const uint32_t rc = p.a.round_counts[c * p.a.max_rounds + r];
-    const bool is_full = rc == B;
+    const bool is_full = p.bypass(rc);
     const uint64_t fbase = (e_of(t, B) + f) * B;
     for (uint32_t j = lane; j < rc; j += 64) {
       if (src + j >= c * p.a.cap + total) break;  // probe capped this chunk (flagged there)
@@ -121,15 +129,16 @@ __global__ __launch_bounds__(256) void copy_rows(CompactParams p) {
 }
 
 __global__ void chunk_counts(CompactParams p) {
-  const uint64_t T = p.totals[0], F = p.totals[1], B = p.a.chunk;
-  const uint64_t n_out = F + (T + B - 1) / B;
+  // P-chunks (compacted): all full except the last; pass-through chunks were counted by full_list.
+  const uint64_t T = p.totals[0], B = p.a.chunk;
+  const uint64_t F = p.totals[1] < p.max_full ? p.totals[1] : p.max_full;
+  const uint64_t n_p = (T + B - 1) / B;
   const uint64_t lim = p.a.out_cap_rows / B;
-  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n_out && q < lim;
-       q += (uint64_t)gridDim.x * blockDim.x) {
-    // every output chunk is full except the last P-chunk, which is the last output chunk
-    uint32_t n = (uint32_t)B;
-    if (q == n_out - 1 && T > 0) n = (uint32_t)(T - ((T + B - 1) / B - 1) * B);
-    p.a.out_chunk_counts[q] = n;
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n_p;
+       k += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t q = k + (F ? full_before(p, F, k) : 0);
+    if (q >= lim) continue;
+    p.a.out_chunk_counts[q] = k + 1 < n_p ? (uint32_t)B : (uint32_t)(T - k * B);
   }
 }
 
@@ -141,8 +150,17 @@ size_t scan_temp_bytes(uint64_t n) {
 
 }  // namespace
 
-size_t compact_workspace(uint64_t n_chunks, uint64_t cap, uint32_t chunk) {
-  const uint64_t max_full = n_chunks * (cap / chunk + 1);
+// Pass-through results per probe chunk: at most cap / T of them (each has >= T rows) and at most
+// one per round.
+uint64_t max_bypass(uint64_t n_chunks, uint64_t cap, uint32_t chunk, uint32_t max_rounds, uint32_t threshold) {
+  const uint64_t t = threshold ? threshold : chunk;
+  uint64_t per = cap / t + 1;
+  if (max_rounds && max_rounds < per) per = max_rounds;
+  return n_chunks * per;
+}
+
+size_t compact_workspace(uint64_t n_chunks, uint64_t cap, uint32_t chunk, uint32_t max_rounds, uint32_t threshold) {
+  const uint64_t max_full = max_bypass(n_chunks, cap, chunk, max_rounds, threshold);
   return 256 + 4 * ((n_chunks * 8 + 255) & ~255ull) + ((max_full * 4 + 255) & ~255ull) + scan_temp_bytes(n_chunks);
 }
 
@@ -160,7 +178,8 @@ hipError_t launch_compact(const ccj_compact_args &a, hipStream_t s) {
   p.full = (uint64_t *)take(a.n_chunks * 8);
   uint64_t *nf_raw = (uint64_t *)take(a.n_chunks * 8);
   uint64_t *f_raw = (uint64_t *)take(a.n_chunks * 8);
-  p.max_full = a.n_chunks * (a.cap / a.chunk + 1);
+  p.max_full = max_bypass(a.n_chunks, a.cap, a.chunk, a.max_rounds, a.threshold);
+  p.thr = a.threshold ? (a.threshold < a.chunk ? a.threshold : a.chunk) : a.chunk;
   p.fullE = (uint32_t *)take(p.max_full * 4);
   size_t tb = scan_temp_bytes(a.n_chunks);
   void *tmp = take(tb);

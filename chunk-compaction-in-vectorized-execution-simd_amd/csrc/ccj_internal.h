@@ -97,7 +97,7 @@ hipError_t launch_result_checksum(const uint32_t *count, const uint32_t *sel, co
 int api_fail(int code, const std::string &msg);
 int api_check_device();
 
-size_t compact_workspace(uint64_t n_chunks, uint64_t cap, uint32_t chunk);
+size_t compact_workspace(uint64_t n_chunks, uint64_t cap, uint32_t chunk, uint32_t max_rounds, uint32_t threshold);
 hipError_t launch_compact(const ccj_compact_args &a, hipStream_t s);
 size_t partition_workspace(uint64_t n, uint32_t parts);
 // Slot-range partitioning for the L2-resident probe: partition p = slot >> window_bits, with the

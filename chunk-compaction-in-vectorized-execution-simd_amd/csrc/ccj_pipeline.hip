@@ -147,6 +147,33 @@ __global__ __launch_bounds__(256) void pipeline_sink(SinkParams p, unsigned long
   }
 }
 
+// Result collection (DataCollection::AppendChunk, data_collection.cpp:10-21): chunk by chunk, the
+// live rows of every column appended densely.  Needed after a threshold-gated compactor, whose
+// pass-through chunks are not full.
+__global__ void widen_counts(const uint32_t *c, uint64_t n, uint64_t *w) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) w[i] = c[i];
+}
+
+struct PackParams {
+  const int64_t *src[kCarry + 1];
+  int64_t *dst[kCarry + 1];
+  uint32_t n_cols, chunk;
+  uint64_t n_chunks;
+  const uint32_t *counts;
+  const uint64_t *pre;
+};
+
+__global__ __launch_bounds__(256) void dense_pack(PackParams p) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t c = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= p.n_chunks) return;
+  const uint32_t n = p.counts[c];
+  const uint64_t d0 = p.pre[c], s0 = c * p.chunk;
+  for (uint32_t q = 0; q < p.n_cols; ++q)
+    for (uint32_t j = lane; j < n; j += 64) p.dst[q][d0 + j] = p.src[q][s0 + j];
+}
+
 size_t scan_bytes(uint64_t n) {
   size_t b = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (uint64_t *)nullptr, (uint64_t *)nullptr, (int)n);
@@ -168,7 +195,14 @@ struct ccj_pipeline {
   uint32_t joins = 0, chunk = 0;
   int mode = CCJ_COMPACT_NONE;
   std::vector<std::unique_ptr<Level>> lv;
+  std::vector<uint32_t> thresholds;  // CCJ_COMPACT_FULL pass-through threshold per join (0 = chunk)
   ccj::DevBuf tot;  // [0] rows, [1] segments, [2] compact out chunks, [3] status
+  ccj::DevBuf res_cols[2 * CCJ_MAX_JOINS], pack_w, pack_pre, pack_tmp;  // dense result after gated compaction
+  hipEvent_t ev[CCJ_MAX_JOINS + 1] = {};
+  ~ccj_pipeline() {
+    for (auto e : ev)
+      if (e) (void)hipEventDestroy(e);
+  }
 };
 
 namespace {
@@ -199,7 +233,20 @@ extern "C" int ccj_pipeline_create(const ccj_table *const *tables, uint32_t n_jo
   pl->chunk = chunk;
   pl->mode = compact_mode;
   for (uint32_t l = 0; l < n_joins; ++l) pl->lv.emplace_back(new ccj_pipeline::Level);
+  pl->thresholds.assign(n_joins, 0);
+  for (uint32_t l = 0; l <= n_joins; ++l) {
+    if (hipEventCreate(&pl->ev[l]) != hipSuccess) {
+      delete pl;
+      return ccj::api_fail(CCJ_ERR_HIP, "ccj_pipeline_create: hipEventCreate failed");
+    }
+  }
   *out = pl;
+  return CCJ_OK;
+}
+
+extern "C" int ccj_pipeline_set_thresholds(ccj_pipeline *pl, const uint32_t *thresholds) {
+  if (!pl) return ccj::api_fail(CCJ_ERR_INVALID, "ccj_pipeline_set_thresholds: null pipeline");
+  for (uint32_t l = 0; l < pl->joins; ++l) pl->thresholds[l] = thresholds ? thresholds[l] : 0;
   return CCJ_OK;
 }
 
@@ -225,13 +272,19 @@ extern "C" int ccj_pipeline_run(ccj_pipeline *pl, const int64_t *const *d_cols, 
   for (uint32_t j = 0; j < J; ++j) in_cols[j] = n_rows ? d_cols[j] : nullptr;
   uint32_t in_ncols = J;
   uint64_t in_rows = n_rows, in_chunks = (n_rows + B - 1) / B;
+  uint64_t in_phys = n_rows;  // physical extent of the input columns (chunk-major after compaction)
   const uint32_t *in_counts = nullptr;       // NULL: every physical row of the chunk
   const uint64_t *in_base = nullptr, *in_obase = nullptr;
 
+  PL_TRY(hipEventRecord(pl->ev[0], s), "event");
+  uint32_t levels_run = 0;
+  bool gaps = false;           // the last compaction left pass-through chunks that are not full
+  uint64_t last_out_chunks = 0;
   for (uint32_t l = 0; l < J; ++l) {
     res->chunks_in[l] = in_chunks;
     res->rows_in[l] = in_rows;
     if (in_chunks == 0) break;
+    levels_run = l + 1;
     ccj_pipeline::Level &L = *pl->lv[l];
     const ccj_table *t = pl->tables[l];
     const uint64_t dup = t->info.max_dup ? t->info.max_dup : 1;
@@ -251,7 +304,7 @@ extern "C" int ccj_pipeline_run(ccj_pipeline *pl, const int64_t *const *d_cols, 
     p.mask = (uint32_t)(t->info.size - 1);
     p.keys = in_cols[l];
     p.counts = in_counts;
-    p.n_rows = in_rows;
+    p.n_rows = in_phys;
     p.n_chunks = in_chunks;
     p.chunk = B;
     p.max_rounds = R;
@@ -299,11 +352,14 @@ extern "C" int ccj_pipeline_run(ccj_pipeline *pl, const int64_t *const *d_cols, 
     const uint64_t next_dup =
         last ? 1 : (pl->tables[l + 1]->info.max_dup ? pl->tables[l + 1]->info.max_dup : 1);
     if (pl->mode == CCJ_COMPACT_FULL) {
-      const uint64_t out_chunks = (T + B - 1) / B;
+      const uint32_t thr = pl->thresholds[l];
+      // compacted chunks (all full but the last) + pass-through chunks (at most one per
+      // non-empty Next result, only when the threshold is below a full chunk)
+      const uint64_t out_chunks = (T + B - 1) / B + (thr != 0 && thr < B ? S : 0);
       const uint64_t cap_rows = out_chunks * B;
       for (uint32_t q = 0; q < ncols; ++q) PL_TRY(L.cols[q].ensure(cap_rows * 8), "alloc");
       PL_TRY(L.next_counts.ensure(out_chunks * 4), "alloc");
-      const size_t wsb = ccj::compact_workspace(in_chunks, cap, B);
+      const size_t wsb = ccj::compact_workspace(in_chunks, cap, B, R, thr);
       PL_TRY(L.compact_ws.ensure(wsb), "alloc");
       ccj_compact_args a{};
       a.count = p.out_count;
@@ -316,6 +372,7 @@ extern "C" int ccj_pipeline_run(ccj_pipeline *pl, const int64_t *const *d_cols, 
       a.max_rounds = R;
       a.chunk = B;
       a.n_cols = in_ncols;
+      a.threshold = thr;
       for (uint32_t q = 0; q < in_ncols; ++q) {
         a.cols[q] = in_cols[q];
         a.out_cols[q] = L.cols[q].as<int64_t>();
@@ -328,7 +385,13 @@ extern "C" int ccj_pipeline_run(ccj_pipeline *pl, const int64_t *const *d_cols, 
       a.workspace_bytes = L.compact_ws.bytes;
       a.status = (uint32_t *)(tot + 3);
       if (T) PL_TRY(ccj::launch_compact(a, s), "pipeline compact");
-      in_chunks = out_chunks;
+      // pass-through chunks add output chunks beyond ceil(T / B); read the true number
+      PL_TRY(hipMemcpyAsync(h, tot, sizeof(h), hipMemcpyDeviceToHost, s), "copy sizes");
+      PL_TRY(hipStreamSynchronize(s), "sync");
+      if (h[3]) return ccj::api_fail(CCJ_ERR_LIMIT, "ccj_pipeline_run: compaction status flags " + std::to_string(h[3]));
+      in_chunks = T ? h[2] : 0;
+      gaps = thr != 0 && thr < B;
+      last_out_chunks = in_chunks;
       in_counts = L.next_counts.as<uint32_t>();
       in_base = in_obase = nullptr;
     } else {
@@ -369,16 +432,52 @@ extern "C" int ccj_pipeline_run(ccj_pipeline *pl, const int64_t *const *d_cols, 
     for (uint32_t q = 0; q < ncols; ++q) in_cols[q] = L.cols[q].as<int64_t>();
     in_ncols = ncols;
     in_rows = T;
+    in_phys = pl->mode == CCJ_COMPACT_FULL ? in_chunks * B : T;
+    PL_TRY(hipEventRecord(pl->ev[l + 1], s), "event");
     if (last) {
       PL_TRY(hipMemcpyAsync(h, tot, sizeof(h), hipMemcpyDeviceToHost, s), "copy status");
       PL_TRY(hipStreamSynchronize(s), "sync");
       if (h[3]) return ccj::api_fail(CCJ_ERR_LIMIT, "ccj_pipeline_run: compaction status flags " + std::to_string(h[3]));
       res->n_out = T;
+      if (gaps && T) {  // collect the result densely, chunk by chunk
+        const uint64_t n = last_out_chunks;
+        PL_TRY(pl->pack_w.ensure(n * 8), "alloc");
+        PL_TRY(pl->pack_pre.ensure(n * 8), "alloc");
+        size_t tb = ccj::scan_bytes(n);
+        PL_TRY(pl->pack_tmp.ensure(tb), "alloc");
+        hipLaunchKernelGGL(ccj::widen_counts, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in_counts, n,
+                           pl->pack_w.as<uint64_t>());
+        PL_TRY(hipGetLastError(), "widen");
+        PL_TRY(hipcub::DeviceScan::ExclusiveSum(pl->pack_tmp.p, tb, pl->pack_w.as<uint64_t>(),
+                                                pl->pack_pre.as<uint64_t>(), (int)n, s),
+               "scan");
+        ccj::PackParams pp{};
+        pp.n_cols = 2 * J;
+        pp.chunk = B;
+        pp.n_chunks = n;
+        pp.counts = in_counts;
+        pp.pre = pl->pack_pre.as<uint64_t>();
+        for (uint32_t q = 0; q < 2 * J; ++q) {
+          PL_TRY(pl->res_cols[q].ensure(T * 8), "alloc");
+          pp.src[q] = in_cols[q];
+          pp.dst[q] = pl->res_cols[q].as<int64_t>();
+          in_cols[q] = pp.dst[q];
+        }
+        hipLaunchKernelGGL(ccj::dense_pack, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, pp);
+        PL_TRY(hipGetLastError(), "dense pack");
+        PL_TRY(hipEventRecord(pl->ev[l + 1], s), "event");
+      }
       for (uint32_t j = 0; j < J; ++j) {
         res->cols[j] = in_cols[j];
         res->payload[j] = in_cols[J + j];
       }
     }
+  }
+  PL_TRY(hipEventSynchronize(pl->ev[levels_run]), "sync");
+  for (uint32_t l = 0; l < levels_run; ++l) {
+    float ms = 0;
+    PL_TRY(hipEventElapsedTime(&ms, pl->ev[l], pl->ev[l + 1]), "event time");
+    res->level_ms[l] = ms;
   }
   return CCJ_OK;
 }

@@ -3,11 +3,16 @@
 //   ccj_pipeline --join-num 3 --chunk-factor 5 --lhs-size 200000 --rhs-size 20000
 //                [--table chain|lp] [--compact none|full] [--block-size 256] [--device 0]
 //                [--engine facade|batched] [--dump FILE] [--repeat N]
+//                [--compact dynamic] [--thresholds T0,T1,...]
 //
 // --engine facade (default) runs the reference's own recursion on the per-chunk operator facade;
 // --engine batched runs the same pipeline through ccj_pipeline_run (include/ccj.h): each join
 // probes all of its input chunks in one launch, with device concatenation / compaction between
 // joins.  --dump writes every result tuple (int64, row-major, all columns) for order checks.
+// Batched engine only: --thresholds gives each join's compactor a pass-through threshold
+// (results of >= T rows pass through, smaller ones are compacted; the BinaryCompactor idea of
+// setting.h:20-22), and --compact dynamic lets the UCB tuner (ccj_tuner.h, the DynamicCompactor
+// of setting.h:23-25 + negative_feedback.hpp) pick every join's threshold per run.
 //
 // Same data generation (main.cpp:41-55: std::mt19937(2), uniform_int_distribution<int>(0, rhs)),
 // same depth-first ExecutePipeline / FlushPipelineCache recursion (main.cpp:119-191), with every
@@ -24,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include "ccj_operators.h"
+#include "ccj_tuner.h"
 
 using namespace simd_compaction_amd;
 
@@ -58,7 +64,8 @@ struct Sink {
 };
 
 struct PipelineState {  // main.cpp:14-20
-  bool lp = false, compact = false;
+  bool lp = false, compact = false, dynamic = false;
+  vector<uint32_t> thresholds;
   vector<unique_ptr<HashTable>> hts;
   vector<unique_ptr<LPHashTable>> lps;
   vector<unique_ptr<DataChunk>> intermediates;
@@ -130,16 +137,47 @@ double RunBatched(PipelineState &st, const vector<vector<Attribute>> &table, siz
            "ccj_pipeline_create");
   ccj_pipeline_result res{};
   double latency = 0;
+  if (!st.thresholds.empty()) {
+    if (st.thresholds.size() != joins) throw std::runtime_error("--thresholds needs one value per join");
+    CcjCheck(ccj_pipeline_set_thresholds(pl, st.thresholds.data()), "ccj_pipeline_set_thresholds");
+  }
+  CompactTuner tuner(joins, (uint32_t)kBlockSize);
+  vector<size_t> arm(joins, 0);
+  vector<uint32_t> thr(joins, 0);
   fprintf(stderr, "TIMES");
   for (size_t r = 0; r < std::max<size_t>(repeat, 1); ++r) {
+    if (st.dynamic) {  // main.cpp:133-142: one threshold per compactor, chosen before the run
+      for (size_t l = 0; l < joins; ++l) {
+        arm[l] = tuner.SelectArm(l);
+        thr[l] = tuner.Threshold(arm[l]);
+      }
+      CcjCheck(ccj_pipeline_set_thresholds(pl, thr.data()), "ccj_pipeline_set_thresholds");
+    }
     HipCheck(hipDeviceSynchronize(), "sync");
     auto t0 = std::chrono::steady_clock::now();
     CcjCheck(ccj_pipeline_run(pl, (const int64_t *const *)d_cols.data(), n, nullptr, &res), "ccj_pipeline_run");
     HipCheck(hipDeviceSynchronize(), "sync");
     latency = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     fprintf(stderr, " %.6f", latency);
+    if (st.dynamic) {  // main.cpp:161-167: reward = speed of join l and everything it feeds
+      double tail_ms = 0;
+      for (size_t l = joins; l-- > 0;) {
+        tail_ms += res.level_ms[l];
+        if (tail_ms > 0) tuner.UpdateArm(l, arm[l], (double)res.rows_in[l] / (tail_ms * 1e6));
+      }
+    }
   }
   fprintf(stderr, "\n");
+  if (st.dynamic) {
+    for (size_t l = 0; l < joins; ++l) {
+      fprintf(stderr, "TUNER join %zu", l);
+      for (size_t a = 0; a < tuner.thresholds().size(); ++a)
+        fprintf(stderr, " thr=%u:sel=%zu:est=%.4f", tuner.thresholds()[a], tuner.bandit(l).Selections(a),
+                tuner.bandit(l).Estimate(a));
+      fprintf(stderr, "\n");
+    }
+  }
+  for (size_t l = 0; l < joins; ++l) fprintf(stderr, "[join %zu] ms %.4f\n", l, res.level_ms[l]);
   for (size_t l = 0; l < joins; ++l)
     fprintf(stderr, "[join %zu] chunks_in %llu rows_in %llu rows_out %llu\n", l, (unsigned long long)res.chunks_in[l],
             (unsigned long long)res.rows_in[l], (unsigned long long)res.rows_out[l]);
@@ -188,7 +226,16 @@ int main(int argc, char **argv) {
     else if (a == "--lhs-size") lhs = std::stoul(v);
     else if (a == "--rhs-size") rhs = std::stoul(v);
     else if (a == "--table") st.lp = v == "lp";
-    else if (a == "--compact") st.compact = v == "full";
+    else if (a == "--compact") {
+      st.compact = v == "full" || v == "dynamic";
+      st.dynamic = v == "dynamic";
+    } else if (a == "--thresholds") {
+      for (size_t p = 0; p < v.size();) {
+        const size_t q = v.find(',', p);
+        st.thresholds.push_back((uint32_t)std::stoul(v.substr(p, q == std::string::npos ? q : q - p)));
+        p = q == std::string::npos ? v.size() : q + 1;
+      }
+    }
     else if (a == "--block-size") kBlockSize = std::stoul(v);
     else if (a == "--device") device = std::stoi(v);
     else if (a == "--engine") engine = v;
@@ -218,6 +265,8 @@ int main(int argc, char **argv) {
     if (!dump.empty() && !(st.sink.dump = fopen(dump.c_str(), "wb"))) throw std::runtime_error("cannot open " + dump);
     vector<AttributeType> in_types(joins, AttributeType::INTEGER);
     double latency = 0;
+    if (engine != "batched" && (st.dynamic || !st.thresholds.empty()))
+      throw std::runtime_error("threshold / dynamic compaction runs on --engine batched");
     if (engine == "batched") {
       latency = RunBatched(st, table, joins, repeat);
     } else {

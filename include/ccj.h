@@ -160,6 +160,10 @@ int ccj_probe_partitioned(const ccj_table *table, const ccj_probe_args *args, ui
  * Next result of a ccj_probe output, in pipeline order (chunk-major, round-major), with the
  * reference's defect fixed (fresh temp chunk, the commented compactor.cpp:36):
  *   - a Next result of exactly `chunk` rows passes through as its own output chunk (:6);
+ *     with `threshold` T (the threshold-gated compaction setting.h:20-25 names as
+ *     BinaryCompactor / DynamicCompactor but never implements) every non-empty result of at
+ *     least T rows passes through as its own chunk, and only smaller ones are compacted:
+ *     T = chunk (or 0) is NaiveCompactor, T = 1 compacts nothing;
  *   - other results are appended (DataChunk::Append, base.cpp:15-27: every column gathered
  *     through the selection vector) into a cache that is emitted whenever the next result would
  *     overflow it (:22-35); Flush emits the final partial chunk.
@@ -179,20 +183,21 @@ typedef struct ccj_compact_args {
   uint32_t max_rounds;
   uint32_t chunk;
   uint32_t n_cols;              /* probe-side columns carried along, <= CCJ_MAX_COLS */
-  uint32_t reserved;
+  uint32_t threshold;           /* results with >= threshold rows pass through; 0 = chunk (NaiveCompactor) */
   const int64_t *cols[CCJ_MAX_COLS];     /* device int64[n_chunks*chunk] each (chunk-major) */
   int64_t *out_cols[CCJ_MAX_COLS];       /* device int64[out_cap_rows] each */
   int64_t *out_payload;         /* device int64[out_cap_rows] or NULL */
   uint64_t *out_row;            /* device uint64[out_cap_rows] or NULL */
-  uint32_t *out_chunk_counts;   /* device uint32[out_cap_rows / chunk] */
+  uint32_t *out_chunk_counts;   /* device uint32[out_cap_rows / chunk]; pass-through chunks keep their count */
   uint64_t out_cap_rows;        /* multiple of chunk */
   uint64_t *out_n_chunks;       /* device word: output chunks written */
-  void *workspace;              /* device scratch of ccj_compact_workspace_size(n_chunks, ...) bytes */
+  void *workspace;              /* device scratch of ccj_compact_workspace_size(...) bytes */
   size_t workspace_bytes;
   uint32_t *status;             /* device word (ccj_flag bits) or NULL */
 } ccj_compact_args;
 
-size_t ccj_compact_workspace_size(uint64_t n_chunks, uint64_t cap, uint32_t chunk);
+size_t ccj_compact_workspace_size(uint64_t n_chunks, uint64_t cap, uint32_t chunk, uint32_t max_rounds,
+                                  uint32_t threshold);
 int ccj_compact(const ccj_compact_args *args, ccj_stream stream);
 
 /* ---- multi-join pipeline ------------------------------------------------------------------ */
@@ -220,6 +225,7 @@ typedef struct ccj_pipeline_result {
   uint64_t chunks_in[CCJ_MAX_JOINS];     /* chunks probed by join l (probe workgroups) */
   uint64_t rows_in[CCJ_MAX_JOINS];       /* tuples probed by join l */
   uint64_t rows_out[CCJ_MAX_JOINS];      /* tuples produced by join l */
+  float level_ms[CCJ_MAX_JOINS];         /* device time of join l: probe + sizes + concat/compact */
 } ccj_pipeline_result;
 /* tables[l] must outlive the pipeline; chunk = kBlockSize (1..2048). */
 int ccj_pipeline_create(const ccj_table *const *tables, uint32_t n_joins, uint32_t chunk, int compact_mode,
@@ -228,6 +234,10 @@ int ccj_pipeline_create(const ccj_table *const *tables, uint32_t n_joins, uint32
  * buffers belong to the pipeline and stay valid until the next run or ccj_pipeline_free. */
 int ccj_pipeline_run(ccj_pipeline *pl, const int64_t *const *d_cols, uint64_t n_rows, ccj_stream stream,
                      ccj_pipeline_result *res);
+/* CCJ_COMPACT_FULL: join l's compactor lets results of >= thresholds[l] rows pass through and
+ * compacts the smaller ones (ccj_compact_args.threshold; 0 = chunk = NaiveCompactor, the
+ * default; NULL restores it) — the threshold a DynamicCompactor tunes per run (host/ccj_tuner.h). */
+int ccj_pipeline_set_thresholds(ccj_pipeline *pl, const uint32_t *thresholds);
 int ccj_pipeline_free(ccj_pipeline *pl);
 /* Result verification: d_acc[0] += tuples, d_acc[1] += sum over tuples of fmix64(t), where
  * t = 0x51ED27 folded over the tuple's columns k in order as t = fmix64(t ^ v_k) + k (the

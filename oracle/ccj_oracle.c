@@ -263,15 +263,16 @@ uint64_t ccj_o_count_uniform(uint64_t seed, uint64_t row_begin, uint64_t row_end
  * removes the aliasing defect of SURVEY §A.3): a full chunk passes through (:6); otherwise rows
  * are appended to the cache (:12-19); on overflow the cache is topped up to `chunk`, emitted,
  * and the remainder becomes the new cache (:22-35).  Flush emits what is cached (compactor.h:23). */
-uint64_t ccj_o_compact_plan(const uint32_t *seg_counts, uint64_t n_segs, uint32_t chunk, uint64_t *dest,
-                            uint32_t *out_chunk_counts) {
+uint64_t ccj_o_compact_plan_threshold(const uint32_t *seg_counts, uint64_t n_segs, uint32_t chunk,
+                                      uint32_t threshold, uint64_t *dest, uint32_t *out_chunk_counts) {
+  const uint64_t thr = threshold == 0 || threshold > chunk ? chunk : threshold;
   uint64_t *cache = (uint64_t *)malloc((uint64_t)chunk * sizeof(uint64_t));
   uint64_t q = 0, n_out = 0, row = 0;
   for (uint64_t s = 0; s < n_segs; ++s) {
     uint64_t c = seg_counts[s];
-    if (c == chunk) {
+    if (c != 0 && c >= thr) {  /* compactor.cpp:6 (thr = chunk); threshold-gated pass-through */
       for (uint64_t j = 0; j < c; ++j) dest[row + j] = n_out * chunk + j;
-      if (out_chunk_counts) out_chunk_counts[n_out] = chunk;
+      if (out_chunk_counts) out_chunk_counts[n_out] = (uint32_t)c;
       ++n_out;
     } else if (c <= chunk - q) {
       for (uint64_t j = 0; j < c; ++j) cache[q++] = row + j;
@@ -293,4 +294,9 @@ uint64_t ccj_o_compact_plan(const uint32_t *seg_counts, uint64_t n_segs, uint32_
   }
   free(cache);
   return n_out;
+}
+
+uint64_t ccj_o_compact_plan(const uint32_t *seg_counts, uint64_t n_segs, uint32_t chunk, uint64_t *dest,
+                            uint32_t *out_chunk_counts) {
+  return ccj_o_compact_plan_threshold(seg_counts, n_segs, chunk, chunk, dest, out_chunk_counts);
 }

@@ -68,6 +68,10 @@ uint64_t ccj_o_count_uniform(uint64_t seed, uint64_t row_begin, uint64_t row_end
  * Returns the number of output chunks (the final partial one included, an empty flush not). */
 uint64_t ccj_o_compact_plan(const uint32_t *seg_counts, uint64_t n_segs, uint32_t chunk, uint64_t *dest,
                             uint32_t *out_chunk_counts);
+/* Same with a pass-through threshold: non-empty results of >= threshold rows leave as their own
+ * chunk (keeping their count), smaller ones are compacted (threshold 0 = chunk: the above). */
+uint64_t ccj_o_compact_plan_threshold(const uint32_t *seg_counts, uint64_t n_segs, uint32_t chunk,
+                                      uint32_t threshold, uint64_t *dest, uint32_t *out_chunk_counts);
 
 #ifdef __cplusplus
 }

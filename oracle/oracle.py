@@ -56,6 +56,8 @@ def lib():
         L.ccj_o_count_uniform.argtypes = [u64, u64, u64, u64, u64, u64, u64p, C.c_int]
         L.ccj_o_compact_plan.restype = u64
         L.ccj_o_compact_plan.argtypes = [u32p, u64, C.c_uint32, u64p, u32p]
+        L.ccj_o_compact_plan_threshold.restype = u64
+        L.ccj_o_compact_plan_threshold.argtypes = [u32p, u64, C.c_uint32, C.c_uint32, u64p, u32p]
     return _LIB
 
 
@@ -143,12 +145,15 @@ def count_uniform(seed, row_begin, row_end, rng, n_build, cf, threads=0):
     return int(m), int(l2.value)
 
 
-def compact_plan(seg_counts, chunk):
+def compact_plan(seg_counts, chunk, threshold=0):
+    """Literal sequential NaiveCompactor (fixed) over Next results of seg_counts rows: destination
+    slot (out_chunk * chunk + offset) of every row, and the output chunks' row counts."""
     seg = np.ascontiguousarray(seg_counts, dtype=np.uint32)
     total = int(seg.sum())
     dest = np.zeros(total, np.uint64)
     occ = np.zeros(total // max(chunk, 1) + len(seg) + 2, np.uint32)
-    n = lib().ccj_o_compact_plan(_p(seg, C.c_uint32), len(seg), chunk, _p(dest, C.c_uint64), _p(occ, C.c_uint32))
+    n = lib().ccj_o_compact_plan_threshold(_p(seg, C.c_uint32), len(seg), chunk, threshold, _p(dest, C.c_uint64),
+                                           _p(occ, C.c_uint32))
     return dest, occ[:n]
 
 

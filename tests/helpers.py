@@ -80,14 +80,15 @@ def ref_keys(n, cf):
     return O.ref_build_keys(n, cf)
 
 
-def oracle_pipeline(tables, cols, B, compact, cap_factor, max_rounds=256):
+def oracle_pipeline(tables, cols, B, compact, cap_factor, max_rounds=256, thresholds=None):
     """main.cpp's ExecutePipeline / FlushPipelineCache (main.cpp:119-191) restated join by join on
     the oracle (TEST INFRASTRUCTURE): join l probes column l of every input chunk with the
     oracle's L3 probe (round-major Next order), then the Next results, in pipeline order, either
     become the next join's chunks one by one (no compaction) or are re-chunked by the oracle's
     literal NaiveCompactor simulation (compact_plan, compactor.cpp:5-41 with the :36 fix).
     Returns the result table's carried columns (probe columns, then one payload per join) in the
-    ResultCollector's append order."""
+    ResultCollector's append order.  thresholds[l]: join l's compactor lets results of at least
+    that many rows pass through (0 = chunk: NaiveCompactor)."""
     from oracle import oracle as O
 
     carried = [np.asarray(c, np.int64) for c in cols]
@@ -108,7 +109,8 @@ def oracle_pipeline(tables, cols, B, compact, cap_factor, max_rounds=256):
         pay = np.concatenate(seg_pay) if seg_pay else np.zeros(0, np.int64)
         stream = [c[rows] for c in carried] + [pay]
         if compact:
-            dest, occ = O.compact_plan(np.array(seg_counts, np.uint32), B)
+            thr = thresholds[l] if thresholds is not None else 0
+            dest, occ = O.compact_plan(np.array(seg_counts, np.uint32), B, thr)
             nxt = []
             for col in stream:
                 a = np.zeros(len(occ) * B, np.int64)

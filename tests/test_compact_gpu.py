@@ -20,7 +20,7 @@ def _device():
     ccj.device_init(0)
 
 
-def expected_compaction(ores, chunk, keys, extra):
+def expected_compaction(ores, chunk, keys, extra, threshold=0):
     """Segments = every round of every chunk in pipeline order; rows concatenated accordingly."""
     cap, mr = ores["cap"], ores["max_rounds"]
     segs, rows, pays = [], [], []
@@ -32,7 +32,7 @@ def expected_compaction(ores, chunk, keys, extra):
         pays.append(ores["payload"][c * cap:c * cap + n])
     rows = np.concatenate(rows) if rows else np.zeros(0, np.int64)
     pays = np.concatenate(pays) if pays else np.zeros(0, np.int64)
-    dest, occ = O.compact_plan(np.array(segs, np.uint32), chunk)
+    dest, occ = O.compact_plan(np.array(segs, np.uint32), chunk, threshold)
     total = len(rows)
     want_row = np.full(len(occ) * chunk, -1, np.int64)
     want_pay = np.zeros(len(occ) * chunk, np.int64)
@@ -102,3 +102,31 @@ def test_compact_empty():
     comp = ccj.compact(out, 256)
     torch.cuda.synchronize()
     assert int(comp["n"].item()) == 0
+
+
+@pytest.mark.parametrize("kind", [ccj.LP, ccj.CHAIN])
+@pytest.mark.parametrize("chunk,threshold", [(256, 1), (256, 64), (256, 200), (2048, 512), (64, 63), (100, 0)])
+def test_threshold_gated_compaction(kind, chunk, threshold):
+    """Results of >= threshold rows pass through as their own (sparse) chunk, smaller ones are
+    compacted — the sequential simulation (oracle compact_plan with a threshold) decides every
+    row's output slot and every output chunk's count."""
+    bkeys = ref_keys(20000, 3)
+    n_probe = 30 * chunk + 17
+    keys = O.uniform_keys(chunk + threshold, 0, n_probe, 60000)
+    table = ccj.Table.from_host(kind, bkeys)
+    dkeys = torch.from_numpy(keys).cuda()
+    out = table.probe(dkeys, chunk)
+    comp = ccj.compact(out, chunk, cols=[dkeys], threshold=threshold)
+    torch.cuda.synchronize()
+    assert int(out["status"].item()) == 0 and int(comp["status"].item()) == 0
+    ores = {k: (v.cpu().numpy() if isinstance(v, torch.Tensor) else v) for k, v in out.items()}
+    ores["sel"] = ores["sel"].view(np.uint32)
+    occ, want_row, want_pay, want_cols, total = expected_compaction(ores, chunk, keys, [keys], threshold)
+    n_out = int(comp["n"].item())
+    assert n_out == len(occ)
+    assert np.array_equal(comp["counts"].cpu().numpy()[:n_out].view(np.uint32), occ)
+    valid = want_row >= 0
+    assert np.array_equal(comp["row"].cpu().numpy()[:n_out * chunk][valid], want_row[valid])
+    assert np.array_equal(comp["payload"].cpu().numpy()[:n_out * chunk][valid], want_pay[valid])
+    assert np.array_equal(comp["cols"][0].cpu().numpy()[:n_out * chunk][valid], want_cols[0][valid])
+    assert valid.sum() == total

@@ -138,10 +138,11 @@ def test_compact_plan_properties(B):
         assert d[0] % B == 0 and (np.diff(d.astype(np.int64)) == 1).all()
 
 
-def closed_form_compaction(segs, B):
+def closed_form_compaction(segs, B, threshold=0):
     """The prefix-sum form the device compactor uses (csrc/ccj_compact.hip header)."""
     segs = np.asarray(segs, np.int64)
-    full = segs == B
+    thr = B if threshold == 0 or threshold > B else threshold
+    full = (segs != 0) & (segs >= thr)
     t = np.concatenate([[0], np.cumsum(np.where(full, 0, segs))[:-1]])
     F = np.concatenate([[0], np.cumsum(full)[:-1]])
     E = np.where(t == 0, 0, (t + B - 1) // B - 1)
@@ -159,12 +160,17 @@ def closed_form_compaction(segs, B):
 
 
 @pytest.mark.parametrize("B,seed", [(4, 0), (4, 1), (8, 2), (16, 3), (5, 4)])
-def test_compaction_closed_form_equals_sequential(B, seed):
+@pytest.mark.parametrize("threshold", [0, 1, 2, 3])
+def test_compaction_closed_form_equals_sequential(B, seed, threshold):
     rng = np.random.default_rng(seed)
     segs = rng.integers(0, B + 1, size=400)
     segs[rng.random(400) < 0.2] = B
-    dest, _ = O.compact_plan(segs.astype(np.uint32), B)
-    assert np.array_equal(closed_form_compaction(segs, B), dest.astype(np.int64))
+    dest, occ = O.compact_plan(segs.astype(np.uint32), B, threshold)
+    assert np.array_equal(closed_form_compaction(segs, B, threshold), dest.astype(np.int64))
+    # every row kept once; pass-through chunks keep their count, compacted ones are full but the last
+    assert len(np.unique(dest)) == len(dest) and int(occ.sum()) == int(segs.sum())
+    if threshold == 1:  # compacts nothing: one output chunk per non-empty result
+        assert np.array_equal(occ, segs[segs > 0])
 
 
 @pytest.mark.parametrize("kind", [0, 1])

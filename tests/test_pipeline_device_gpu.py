@@ -67,6 +67,36 @@ def test_pipeline_l3_vs_oracle(kind, compact, joins, n, rhs, cf, B):
     assert all(f["chunks_in"] <= g["chunks_in"] for f, g in zip(full.stats(), none.stats()))
 
 
+@pytest.mark.parametrize("kind", [0, 1])
+@pytest.mark.parametrize("thresholds,B", [((1, 1, 1), 256), ((64, 128, 0), 256), ((200, 1, 100), 256),
+                                          ((1000, 0, 2048), 2048)])
+def test_pipeline_threshold_compaction_l3(kind, thresholds, B):
+    """Threshold-gated compactors between joins (ccj_pipeline_set_thresholds): the whole result
+    table in order against the oracle pipeline with the same thresholds, and the same multiset as
+    no compaction."""
+    import torch
+    import ccj
+    from oracle import oracle as O
+    dev = _dev()
+    joins, n, rhs, cf = 3, 20000, 4000, 2
+    cols = _inputs(joins, n, rhs, 5)
+    dt = [ccj.Table.reference(kind, rhs, cf, ccj.LAYOUT_REFERENCE) for _ in range(joins)]
+    ot = [O.Table(kind, O.ref_build_keys(rhs, cf)) for _ in range(joins)]
+    want = oracle_pipeline(ot, cols, B, True, cap_factor=cf, thresholds=thresholds)
+    pl = ccj.Pipeline(dt, B, True)
+    pl.set_thresholds(thresholds)
+    pl.run([torch.from_numpy(c).to(dev) for c in cols])
+    got = pl.result_columns()
+    got = got[:joins] + [got[joins + 2 * l + 1] for l in range(joins)]
+    assert pl.res.n_out == len(want[0])
+    for g, w in zip(got, want):
+        np.testing.assert_array_equal(g, w)
+    none = ccj.Pipeline(dt, B, False)
+    none.run([torch.from_numpy(c).to(dev) for c in cols])
+    assert none.checksum() == pl.checksum()
+    assert all(s["ms"] > 0 for s in pl.stats())
+
+
 def test_pipeline_empty_and_no_match():
     import torch
     import ccj
@@ -81,10 +111,10 @@ def test_pipeline_empty_and_no_match():
         assert pl.checksum() == (0, 0)
 
 
-def run_bin(spec, engine, dump=None):
+def run_bin(spec, engine, dump=None, extra=()):
     args = [BIN, "--join-num", spec["joins"], "--chunk-factor", spec["cf"], "--lhs-size", spec["lhs"],
             "--rhs-size", spec["rhs"], "--table", spec["kind"], "--compact", "full" if spec["compact"] else "none",
-            "--block-size", spec["B"], "--engine", engine]
+            "--block-size", spec["B"], "--engine", engine] + list(extra)
     if dump:
         args += ["--dump", dump]
     return subprocess.run([str(a) for a in args], capture_output=True, text=True, timeout=600)
@@ -122,3 +152,20 @@ def test_batched_engine_order_equals_facade(name, tmp_path):
     assert q.returncode == 0, q.stderr
     assert os.path.getsize(a) == KA[name]["n_out"] * 8 * 3 * spec["joins"]
     assert filecmp.cmp(a, b, shallow=False)
+
+
+@pytest.mark.parametrize("name", [k for k in CASES if k.startswith("main_") and "_j3_" in k and "compact" not in k])
+@pytest.mark.parametrize("mode", ["thresholds", "dynamic"])
+def test_gated_and_dynamic_compaction_match_reference(name, mode):
+    """Threshold-gated compaction (fixed per join) and the UCB-tuned dynamic compaction give the
+    reference's result multiset (count + order-insensitive checksum over every column)."""
+    spec = KA[name]["spec"]
+    B = spec["B"]
+    extra = (["--compact", "full", "--thresholds", f"{B // 8},1,{B}"] if mode == "thresholds"
+             else ["--compact", "dynamic", "--repeat", "60"])
+    p = run_bin(spec, "batched", extra=extra)
+    assert p.returncode == 0, p.stderr
+    res, _ = parse(p.stdout)
+    assert (res["n_out"], res["l2"]) == (KA[name]["n_out"], KA[name]["l2"])
+    if mode == "dynamic":
+        assert p.stderr.count("TUNER join") == 3
