@@ -167,8 +167,11 @@ def bench_pipeline(args):
                              "--rhs-size", args.pipe_rhs, "--table", args.pipe_table,
                              "--block-size", args.pipe_block, "--engine", "batched", "--repeat", reps)]
     runs = {}
-    for mode in ("full", "none"):
-        p = subprocess.run([binp] + spec + ["--compact", mode], capture_output=True, text=True, timeout=900)
+    for mode in ("full", "none", "dynamic"):
+        extra = ["--compact", mode]
+        if mode == "dynamic":  # the UCB tuner needs its warm-up (4 pulls per arm) before it settles
+            extra += ["--repeat", str(max(reps, 100))]
+        p = subprocess.run([binp] + spec + extra, capture_output=True, text=True, timeout=900)
         if p.returncode != 0:
             raise RuntimeError(f"ccj_pipeline failed: {p.stderr[-500:]}")
         out = {}
@@ -179,14 +182,17 @@ def bench_pipeline(args):
             elif t and t[0] == "TIMES":
                 out["times"] = [float(x) for x in t[1:]]
             elif t and t[0] == "[join":
-                out.setdefault("joins", []).append({t[i]: int(t[i + 1]) for i in range(2, len(t), 2)})
-        tt = out["times"][args.warmup:]
+                out.setdefault("joins", []).append({t[i]: (float(t[i + 1]) if t[i] == "ms" else int(t[i + 1]))
+                                                    for i in range(2, len(t), 2)})
+            elif t and t[0] == "TUNER":
+                out.setdefault("tuner", []).append(" ".join(t[3:]))
+        tt = out["times"][args.warmup:] if mode != "dynamic" else out["times"][-args.steps:]
         out["s_per_step"] = sum(tt) / len(tt)
         runs[mode] = out
         log(f"[pipeline] {mode}: {out['s_per_step'] * 1e3:.2f} ms/step, n_out {out['n_out']}")
     cpu, parity = None, {"n_out": runs["full"]["n_out"], "l2": hex(runs["full"]["l2"]),
-                         "modes_agree": runs["full"]["n_out"] == runs["none"]["n_out"]
-                         and runs["full"]["l2"] == runs["none"]["l2"]}
+                         "modes_agree": all(runs[m]["n_out"] == runs["full"]["n_out"] and runs[m]["l2"] == runs["full"]["l2"]
+                                            for m in runs)}
     if not args.no_cpu and os.path.exists(REF_DRIVER) and has_avx512():
         base = [REF_DRIVER, "pipeline", args.pipe_table, str(args.pipe_block), str(args.pipe_joins), "1",
                 str(args.pipe_lhs), str(args.pipe_rhs)]
@@ -217,6 +223,10 @@ def bench_pipeline(args):
                    "compaction": "NaiveCompactor (fixed) between joins", "parallelism": "dp1"},
         "no_compaction": {"ms_per_step": none["s_per_step"] * 1e3, "value": args.pipe_lhs / none["s_per_step"],
                           "joins": none.get("joins")},
+        "dynamic_compaction": {"ms_per_step": runs["dynamic"]["s_per_step"] * 1e3,
+                               "value": args.pipe_lhs / runs["dynamic"]["s_per_step"],
+                               "note": "UCB-tuned per-join thresholds (host/ccj_tuner.h), last steps after warm-up",
+                               "tuner": runs["dynamic"].get("tuner")},
         "joins": full.get("joins"),
         "cpu_baseline": cpu,
         "parity": parity,

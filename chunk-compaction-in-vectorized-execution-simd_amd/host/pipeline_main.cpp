@@ -177,10 +177,10 @@ double RunBatched(PipelineState &st, const vector<vector<Attribute>> &table, siz
       fprintf(stderr, "\n");
     }
   }
-  for (size_t l = 0; l < joins; ++l) fprintf(stderr, "[join %zu] ms %.4f\n", l, res.level_ms[l]);
   for (size_t l = 0; l < joins; ++l)
-    fprintf(stderr, "[join %zu] chunks_in %llu rows_in %llu rows_out %llu\n", l, (unsigned long long)res.chunks_in[l],
-            (unsigned long long)res.rows_in[l], (unsigned long long)res.rows_out[l]);
+    fprintf(stderr, "[join %zu] chunks_in %llu rows_in %llu rows_out %llu ms %.4f\n", l,
+            (unsigned long long)res.chunks_in[l], (unsigned long long)res.rows_in[l],
+            (unsigned long long)res.rows_out[l], res.level_ms[l]);
   uint64_t *d_acc = nullptr, acc[2] = {0, 0};
   HipCheck(hipMalloc(&d_acc, 16), "alloc");
   HipCheck(hipMemset(d_acc, 0, 16), "memset");
