@@ -1,13 +1,15 @@
 #!/usr/bin/env python3
 """bench.py — probe throughput of the MI355X hash-join hot path (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|pipeline] [--no-cpu]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c5|pipeline] [--no-cpu]
   N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 Step = one pass of the hot path over one batch:
   c2 (default; BASELINE configs[1]): LP table of 2^26 reference-generator keys (2 GiB, alpha 1/4),
       2^30 uniform probe keys in [0, 2^26) resident in HBM, chunk 2048 -> one ccj_probe launch
       (hash, probe rounds, ballot packs, payload) writing row ids + payloads + per-round counts.
+  c5 (BASELINE configs[4]): C2 plus 8 int64 build-side payload columns p_c = k*(c+1)+c, gathered
+      on every match (position-major payload rows: one 64-byte row read per match).
   pipeline: main.cpp's default 3-join pipeline (2e7 LHS rows, 2e6-key chaining tables, cf 1,
       B 256, main.cpp's own mt19937(2) data) on the device (ccj_pipeline_run, host/ccj_pipeline
       --engine batched) with the compactor between joins, no-compaction timed beside it.
@@ -48,7 +50,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=["c2", "pipeline"])
+    ap.add_argument("--workload", default="c2", choices=["c2", "c5", "pipeline"])
     ap.add_argument("--batches", type=int, default=4, help="N > 1: exchange batches per step (pipelined)")
     ap.add_argument("--sharded", action="store_true", help="run the N > 1 protocol even at N = 1 (rehearsal)")
     ap.add_argument("--pipe-lhs", type=int, default=20000000)
@@ -281,10 +283,20 @@ def main():
 
     # ---- setup (untimed, as the reference builds before its timer: main.cpp:62-68 vs :92-94) ----
     t0 = time.perf_counter()
+    c5 = args.workload == "c5"
+    P = 8 if c5 else 0
+    if c5:
+        args.path = "chunk"  # the partitioned path does not gather payload columns
     with torch.cuda.stream(stream):
         table = ccj.Table.reference(ccj.LP, n_build, 1, layout, stream=stream)
+        if c5:  # C5 payload of build tuple t (key k): p_c = k*(c+1)+c, row-major [n_build, 8]
+            bk = ccj.gen_reference_keys(0, n_build, n_build, 1, stream=stream)
+            mult = torch.arange(1, P + 1, dtype=torch.int64, device=dev)
+            pay = bk[:, None] * mult[None, :] + (mult[None, :] - 1)
+            table.set_payload(pay.reshape(-1), P, stream=stream)
+            del bk, pay
         keys = ccj.gen_uniform_keys(n_probe, SEED, n_build, first_row=rank * n_probe, stream=stream)
-        out = table.alloc_outputs(n_probe, chunk, rounds=True)
+        out = table.alloc_outputs(n_probe, chunk, rounds=True, payload_cols=P)
         part = table.alloc_partitioned(n_probe) if args.path == "partitioned" else None
     stream.synchronize()
     log(f"[setup] table {table.size} slots, max_rounds {table.max_rounds}, keys {n_probe}: "
@@ -332,19 +344,31 @@ def main():
         matches, l2 = ccj.result_checksum(out, chunk, row_base=rank * n_probe, stream=stream)
     # the other path, timed the same way (reported beside the headline)
     other = "chunk" if args.path == "partitioned" else "partitioned"
-    if other == "partitioned":
-        part = table.alloc_partitioned(n_probe)
-    step(other)
-    stream.synchronize()
-    ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
-    for a, b in ev2:
-        a.record(stream)
+    other_ms = None
+    if not c5:
+        if other == "partitioned":
+            part = table.alloc_partitioned(n_probe)
         step(other)
-        b.record(stream)
-    stream.synchronize()
-    other_ms = sum(a.elapsed_time(b) for a, b in ev2) / len(ev2)
+        stream.synchronize()
+        ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
+        for a, b in ev2:
+            a.record(stream)
+            step(other)
+            b.record(stream)
+        stream.synchronize()
+        other_ms = sum(a.elapsed_time(b) for a, b in ev2) / len(ev2)
     examined, cost_matches = table.probe_cost(keys, stream=stream)
     parity = {"status_flags": status, "matches": matches, "l2": hex(l2)}
+    if c5:  # every gathered payload column holds the matched build tuple's p_c (key == payload)
+        torch.cuda.current_stream().wait_stream(stream)
+        cnt = out["count"].to(torch.int64)
+        valid = torch.arange(out["cap"], device=dev)[None, :] < cnt[:, None]
+        pk = out["payload"].view(-1, out["cap"])
+        parity["payload_cols_ok"] = all(
+            bool(((out["payload_cols"][c].view(-1, out["cap"]) == pk * (c + 1) + c) | ~valid).all())
+            for c in range(P))
+        del cnt, valid, pk
+
     if not args.no_verify:
         from oracle import oracle as O
         want_m, want_l2 = O.count_uniform(SEED, rank * n_probe, (rank + 1) * n_probe, n_build, n_build, 1,
@@ -352,11 +376,11 @@ def main():
         parity.update(expected_matches=want_m, l1_ok=(want_m == matches), l2_ok=(want_l2 == l2))
     s_bar = examined / n_probe
     m_bar = matches / n_probe
-    alg_bytes_per_tuple = 8 + 8 * s_bar + m_bar * 12
+    alg_bytes_per_tuple = 8 + 8 * s_bar + m_bar * (12 + 16 * P)  # +16 B per payload column
     alg_bytes = alg_bytes_per_tuple * n_probe
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_c2.json")
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
     if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
@@ -366,7 +390,7 @@ def main():
             pass
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and not c5:  # the reference has no payload gather
         cpu = cpu_baseline(args)
 
     if rank == 0:
@@ -375,7 +399,9 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
             "data": "synthetic (reference key generator build side; SplitMix64 uniform probe keys, seed 42)",
-            "config": {"workload": "C2: 1xMI355X linear-probe, 64M build / 1B probe int64 uniform keys, chunk=2048",
+            "config": {"workload": ("C5: 1xMI355X wide-payload LP join, 64M build / 1B probe int64, 8 int64 payload "
+                                    "columns gathered on match, chunk=2048") if c5 else
+                       "C2: 1xMI355X linear-probe, 64M build / 1B probe int64 uniform keys, chunk=2048",
                        "table": "linear_probing", "layout": args.layout, "n_build": n_build,
                        "n_probe_per_gpu": n_probe, "chunk": chunk, "parallelism": f"dp{world}"},
             "hbm_gbs_algorithmic": achieved,
@@ -388,9 +414,10 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "path": args.path,
-            "other_path": {"path": other, "ms_per_step": other_ms, "value": n_probe / (other_ms * 1e-3),
-                           "frac": alg_bytes / (other_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                           "parity": "L3 (reference order)" if other == "chunk" else "L1/L2"},
+            "other_path": None if other_ms is None else {
+                "path": other, "ms_per_step": other_ms, "value": n_probe / (other_ms * 1e-3),
+                "frac": alg_bytes / (other_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "parity": "L3 (reference order)" if other == "chunk" else "L1/L2"},
         }
         print(json.dumps(line), flush=True)
     if dist:

@@ -472,7 +472,21 @@ int ccj_probe(const ccj_table *t, const ccj_probe_args *a, ccj_stream stream) {
   ccj::ProbeParams p;
   if (int rc = fill_probe_params(t, a, p)) return rc;
   if (a->n_rows == 0) return CCJ_OK;  // no chunks: nothing to launch
-  HIP_TRY(ccj::launch_probe(t->info.kind, p, (hipStream_t)stream), "probe launch");
+  hipStream_t s = (hipStream_t)stream;
+  if (p.n_pay == 0) {
+    HIP_TRY(ccj::launch_probe(t->info.kind, p, s), "probe launch");
+    return CCJ_OK;
+  }
+  // Wide payload: the probe records every match's table position, a second pass gathers rows.
+  uint32_t *pos = p.out_pos;
+  if (!pos) HIP_TRY(hipMallocAsync((void **)&pos, p.n_chunks * p.cap * sizeof(uint32_t), s), "payload positions");
+  ccj::ProbeParams q = p;
+  q.out_pos = pos;
+  q.n_pay = 0;
+  hipError_t e = ccj::launch_probe(t->info.kind, q, s);
+  if (e == hipSuccess) e = ccj::launch_gather_payload(p, pos, s);
+  if (!p.out_pos) (void)hipFreeAsync(pos, s);
+  HIP_TRY(e, "probe + payload gather launch");
   return CCJ_OK;
 }
 

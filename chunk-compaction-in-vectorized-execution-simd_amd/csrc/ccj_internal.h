@@ -71,6 +71,8 @@ constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 // Launchers (ccj_kernels.hip).  Return hipError_t of the launch.
 hipError_t launch_probe(int kind, const ProbeParams &p, hipStream_t s);
 hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s);
+// C5 payload columns of a finished probe: out_cols[q][slot] = payload row of pos[slot], column q.
+hipError_t launch_gather_payload(const ProbeParams &p, const uint32_t *pos, hipStream_t s);
 hipError_t launch_gen_reference_keys(int64_t *out, uint64_t first, uint64_t n, uint64_t n_total, uint64_t cf,
                                      hipStream_t s);
 hipError_t launch_fill(int64_t *p, uint64_t n, int64_t v, hipStream_t s);

@@ -753,6 +753,121 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
   return hipGetLastError();
 }
 
+namespace {
+// Wide-payload materialisation (C5) after the probe: every match's table position -> its
+// position-major payload row (one 64-byte line for 8 columns), written column by column.  Run as
+// its own pass so each thread keeps two rows' loads in flight instead of the probe's emit phase
+// waiting on one dependent row per match.
+struct GatherParams {
+  const uint32_t *count, *pos;
+  const uint64_t *out_base;
+  uint64_t cap;
+  const int64_t *pay;
+  uint32_t stride;
+  int64_t *cols[CCJ_MAX_PAYLOAD_COLS];
+};
+
+template <int NP, bool VEC>
+__global__ __launch_bounds__(256) void gather_payload(GatherParams g) {
+  const uint64_t c = blockIdx.x;
+  const uint64_t ob = g.out_base ? g.out_base[c] : c * g.cap;
+  const uint32_t n = g.count[c];
+  for (uint32_t j0 = threadIdx.x; j0 < n; j0 += 512) {
+    int64_t v[2][NP];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const uint32_t j = j0 + u * 256;
+      if (j < n) {
+        const int64_t *row = g.pay + (uint64_t)g.pos[ob + j] * g.stride;
+        if (VEC) {
+#pragma unroll
+          for (int q = 0; q + 1 < NP; q += 2) {
+            const longlong2 x = *reinterpret_cast<const longlong2 *>(row + q);
+            v[u][q] = x.x;
+            v[u][q + 1] = x.y;
+          }
+          if (NP & 1) v[u][NP - 1] = row[NP - 1];
+        } else {
+#pragma unroll
+          for (int q = 0; q < NP; ++q) v[u][q] = row[q];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const uint32_t j = j0 + u * 256;
+      if (j < n) {
+#pragma unroll
+        for (int q = 0; q < NP; ++q) __builtin_nontemporal_store(v[u][q], g.cols[q] + ob + j);
+      }
+    }
+  }
+}
+
+// 8 columns, 64-byte rows: four lanes share a row, each loading 16 bytes of it, so one wave
+// instruction fetches 16 whole rows (one request per row instead of four); lane q then writes
+// columns 2q and 2q+1 of its row (16 consecutive rows per column per instruction).
+template <int U>
+__global__ __launch_bounds__(256) void gather_payload_quad(GatherParams g) {
+  __shared__ int64_t *s_cols[CCJ_MAX_PAYLOAD_COLS];
+  if (threadIdx.x < CCJ_MAX_PAYLOAD_COLS) s_cols[threadIdx.x] = g.cols[threadIdx.x];
+  __syncthreads();
+  const uint64_t c = blockIdx.x;
+  const uint64_t ob = g.out_base ? g.out_base[c] : c * g.cap;
+  const uint32_t n = g.count[c];
+  const uint32_t q = threadIdx.x & 3u, r0 = threadIdx.x >> 2;  // 64 rows per block step
+  int64_t *c0 = s_cols[2 * q], *c1 = s_cols[2 * q + 1];
+  for (uint32_t base = 0; base < n; base += 64 * U) {
+    longlong2 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t j = base + u * 64 + r0;
+      if (j < n) v[u] = reinterpret_cast<const longlong2 *>(g.pay + (uint64_t)g.pos[ob + j] * g.stride)[q];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t j = base + u * 64 + r0;
+      if (j < n) {
+        __builtin_nontemporal_store(v[u].x, c0 + ob + j);
+        __builtin_nontemporal_store(v[u].y, c1 + ob + j);
+      }
+    }
+  }
+}
+
+template <int NP>
+hipError_t launch_gather_np(const GatherParams &g, uint64_t n_chunks, hipStream_t s) {
+  const bool vec = (g.stride % 2 == 0) && ((uintptr_t)g.pay % 16 == 0);
+  static const bool quad = getenv("CCJ_GATHER_SCALAR") == nullptr;
+  if (NP == 8 && vec && quad) hipLaunchKernelGGL((gather_payload_quad<4>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
+  else if (vec) hipLaunchKernelGGL((gather_payload<NP, true>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((gather_payload<NP, false>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
+  return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_gather_payload(const ProbeParams &p, const uint32_t *pos, hipStream_t s) {
+  GatherParams g{};
+  g.count = p.out_count;
+  g.pos = pos;
+  g.out_base = p.out_base;
+  g.cap = p.cap;
+  g.pay = p.pay;
+  g.stride = p.pay_stride;
+  for (uint32_t q = 0; q < p.n_pay; ++q) g.cols[q] = p.out_cols[q];
+  switch (p.n_pay) {
+    case 1: return launch_gather_np<1>(g, p.n_chunks, s);
+    case 2: return launch_gather_np<2>(g, p.n_chunks, s);
+    case 3: return launch_gather_np<3>(g, p.n_chunks, s);
+    case 4: return launch_gather_np<4>(g, p.n_chunks, s);
+    case 5: return launch_gather_np<5>(g, p.n_chunks, s);
+    case 6: return launch_gather_np<6>(g, p.n_chunks, s);
+    case 7: return launch_gather_np<7>(g, p.n_chunks, s);
+    case 8: return launch_gather_np<8>(g, p.n_chunks, s);
+    default: return hipSuccess;
+  }
+}
+
 hipError_t launch_probe(int kind, const ProbeParams &p, hipStream_t s) {
   if (p.n_chunks == 0) return hipSuccess;
   return kind == CCJ_TABLE_LP ? launch_kind<CCJ_TABLE_LP>(p, s) : launch_kind<CCJ_TABLE_CHAIN>(p, s);

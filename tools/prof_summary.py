@@ -3,7 +3,7 @@
 
   profiles/TAG_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (as written by rocprofv3)
   profiles/TAG_pmc.json           per-kernel PMC counters (last dispatch of each counter pass)
-  profiles/pmc_c2.json            HBM traffic per probe launch for bench.py's roofline.traffic
+  profiles/pmc_<workload>.json    HBM traffic per probe launch for bench.py's roofline.traffic
 
 Traffic = (FETCH_SIZE + WRITE_SIZE) * 1024 bytes per launch (rocprofv3 reports both in KiB).  The
 gfx950 x2 correction of FETCH_SIZE (MI355X_MICROARCH.md §HBM) applies to wide coalesced streaming
@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--kernel", default="probe_chunks")
     ap.add_argument("--n-probe", type=int, default=1 << 30)
     ap.add_argument("--n-build", type=int, default=1 << 26)
+    ap.add_argument("--workload", default="c2", help="writes profiles/pmc_<workload>.json for bench.py")
     a = ap.parse_args()
     src = os.path.join(ROOT, "gpurun_out", f"prof_{a.tag}")
     dst = os.path.join(ROOT, "profiles")
@@ -59,7 +60,7 @@ def main():
                           "l2_hit_rate": (k["TCC_HIT_sum"] / (k["TCC_HIT_sum"] + k["TCC_MISS_sum"])
                                           if "TCC_HIT_sum" in k else None),
                           "hbm_GBps": traffic / avg_ns if avg_ns else None}
-        with open(os.path.join(dst, "pmc_c2.json"), "w") as f:
+        with open(os.path.join(dst, f"pmc_{a.workload}.json"), "w") as f:
             json.dump({"tag": a.tag, "kernel": a.kernel, "n_probe": a.n_probe, "n_build": a.n_build,
                        "hbm_bytes_per_launch": traffic, "fetch_size_kib": k["FETCH_SIZE"],
                        "write_size_kib": k["WRITE_SIZE"], "kernel_avg_ns": avg_ns}, f, indent=1)
