@@ -1,13 +1,16 @@
 #!/usr/bin/env python3
 """bench.py — probe throughput of the MI355X hash-join hot path (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c5|pipeline] [--no-cpu]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c5|pipeline] [--no-cpu]
   N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 Step = one pass of the hot path over one batch:
   c2 (default; BASELINE configs[1]): LP table of 2^26 reference-generator keys (2 GiB, alpha 1/4),
       2^30 uniform probe keys in [0, 2^26) resident in HBM, chunk 2048 -> one ccj_probe launch
       (hash, probe rounds, ballot packs, payload) writing row ids + payloads + per-round counts.
+  c3 (BASELINE configs[2]): chaining table of 2^26 reference keys, 2^30 probe keys with ~10 %
+      Zipf-skewed hits (ccj_gen_c3_keys), chunk 2048; a step = probe + compaction of every Next
+      result (the selection-vector pack stress case).
   c5 (BASELINE configs[4]): C2 plus 8 int64 build-side payload columns p_c = k*(c+1)+c, gathered
       on every match (position-major payload rows: one 64-byte row read per match).
   pipeline: main.cpp's default 3-join pipeline (2e7 LHS rows, 2e6-key chaining tables, cf 1,
@@ -50,7 +53,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c5", "pipeline"])
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5", "pipeline"])
     ap.add_argument("--batches", type=int, default=4, help="N > 1: exchange batches per step (pipelined)")
     ap.add_argument("--sharded", action="store_true", help="run the N > 1 protocol even at N = 1 (rehearsal)")
     ap.add_argument("--pipe-lhs", type=int, default=20000000)
@@ -157,6 +160,88 @@ def cpu_baseline(args):
         "cpu_model": cpu_model(),
         "nproc": os.cpu_count(),
     }
+
+
+def bench_c3(args, dev, stream):
+    """C3: chaining probe + NaiveCompactor under Zipf-skewed keys with ~10 % matches."""
+    import subprocess
+    n_build, n_probe, chunk = args.n_build, args.n_probe, args.chunk
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        table = ccj.Table.reference(ccj.CHAIN, n_build, 1, ccj.LAYOUT_DEVICE, stream=stream)
+        keys = ccj.gen_c3_keys(n_probe, SEED, n_build, 1, stream=stream)
+        out = table.alloc_outputs(n_probe, chunk, rounds=True)
+    stream.synchronize()
+    log(f"[setup c3] {table.size} buckets, max chain {table.max_rounds}: {time.perf_counter() - t0:.1f} s")
+    comp = None
+
+    def step(ev=None):
+        nonlocal comp
+        if ev:
+            ev[0].record(stream)
+        table.probe(keys, chunk, out=out, stream=stream)
+        if ev:
+            ev[1].record(stream)
+        comp = ccj.compact(out, chunk, cols=[keys], rows=False, stream=stream)
+        if ev:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    stream.synchronize()
+    torch.cuda.synchronize()
+    evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    stream.synchronize()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    probe_ms = sum(a.elapsed_time(b) for a, b, _ in evs) / args.steps
+    comp_ms = sum(b.elapsed_time(c) for _, b, c in evs) / args.steps
+    matches, l2 = ccj.result_checksum(out, chunk, stream=stream)
+    n_comp = int(comp["counts"][:int(comp["n"].item())].to(torch.int64).sum().item())
+    examined, _ = table.probe_cost(keys, stream=stream)
+    parity = {"status_flags": int(out["status"].item()) | int(comp["status"].item()), "matches": matches,
+              "l2": hex(l2), "compacted_rows": n_comp, "compaction_keeps_all": n_comp == matches}
+    cpu = None
+    if not args.no_verify or not args.no_cpu:
+        from oracle import oracle as O
+        if not args.no_verify:
+            want = O.count_c3(SEED, 0, n_probe, n_build, 1, threads=args.cpu_threads)
+            parity.update(expected_matches=want[0], l1_ok=want[0] == matches, l2_ok=want[1] == l2)
+        if not args.no_cpu and os.path.exists(REF_DRIVER) and has_avx512():
+            n_ref = args.cpu_sample // 4
+            p = subprocess.run([REF_DRIVER, "bench", "chain", "next", str(chunk), str(n_build), "1", str(n_ref),
+                                str(n_build), str(SEED), "c3"], capture_output=True, text=True, timeout=600)
+            t = p.stdout.split()
+            if p.returncode == 0 and "BENCH" in t:
+                rm, rs = int(t[t.index("BENCH") + 2]), float(t[t.index("BENCH") + 4])
+                cpu = {"value": n_ref / rs, "unit": "probe tuples/s", "cores": 1, "kind": "reference",
+                       "sample": (f"the reference's HashTable(2^26, 1) + Probe/Next loop (chaining_ht.cpp, compiled "
+                                  f"from its sources), one thread, on the first {n_ref} keys of the same C3 stream: "
+                                  f"{rs:.2f} s, {rm} matches (expected "
+                                  f"{O.count_c3(SEED, 0, n_ref, n_build, 1, threads=args.cpu_threads)[0]})"),
+                       "cpu_model": cpu_model()}
+    n_bar, m_bar = examined / n_probe, matches / n_probe
+    alg = 8 + 8 + 8 * n_bar + 12 * m_bar  # key + off[b], off[b+1] + chain keys + (sel, payload)
+    achieved = alg * n_probe / (probe_ms * 1e-3) / 1e9
+    line = {
+        "metric": METRIC, "value": n_probe / (wall / args.steps), "unit": "probe tuples/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall * 1e3 / args.steps,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic (reference key generator build side; C3 stream: ~10 % Zipf-skewed hits, seed 42)",
+        "config": {"workload": "C3: 1xMI355X chaining_ht + compactor, Zipf-skewed keys, ~10% match rate, "
+                               f"{n_build} build / {n_probe} probe, chunk={chunk}", "parallelism": "dp1"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "probe_chunks<CHAIN,2>",
+                     "kernel_ms": probe_ms, "alg_bytes_per_tuple": alg, "chain_keys_per_tuple": n_bar,
+                     "m_bar": m_bar},
+        "compaction_ms": comp_ms,
+        "cpu_baseline": cpu,
+        "parity": parity,
+    }
+    print(json.dumps(line), flush=True)
 
 
 def bench_pipeline(args):
@@ -280,6 +365,8 @@ def main():
     layout = ccj.LAYOUT_DEVICE if args.layout == "device" else ccj.LAYOUT_REFERENCE
     if world > 1 or args.sharded:
         return bench_multi(args, world, rank, local, dev, stream, dist)
+    if args.workload == "c3":
+        return bench_c3(args, dev, stream)
 
     # ---- setup (untimed, as the reference builds before its timer: main.cpp:62-68 vs :92-94) ----
     t0 = time.perf_counter()

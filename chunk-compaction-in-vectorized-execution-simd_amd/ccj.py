@@ -62,7 +62,7 @@ EXPORTS = ["ccj_last_error", "ccj_abi_version", "ccj_device_init", "ccj_table_bu
            "ccj_result_checksum_mapped", "ccj_gen_reference_keys", "ccj_table_set_payload",
            "ccj_probe_partitioned_workspace_size", "ccj_probe_partitioned", "ccj_pipeline_create",
            "ccj_pipeline_run", "ccj_pipeline_free", "ccj_pipeline_checksum", "ccj_partition_by_owner_fixed",
-           "ccj_segment_chunk_counts", "ccj_pipeline_set_thresholds"]
+           "ccj_segment_chunk_counts", "ccj_pipeline_set_thresholds", "ccj_gen_c3_keys"]
 
 MAX_JOINS = 8
 COMPACT_NONE, COMPACT_FULL = 0, 1
@@ -103,6 +103,7 @@ def lib():
         L.ccj_probe.argtypes = [vp, C.POINTER(ProbeArgs), vp]
         L.ccj_gen_uniform_keys.argtypes = [vp, u64, u64, u64, u64, vp]
         L.ccj_gen_reference_keys.argtypes = [vp, u64, u64, u64, u64, vp]
+        L.ccj_gen_c3_keys.argtypes = [vp, u64, u64, u64, u64, u64, C.c_uint32, vp]
         L.ccj_probe_cost.argtypes = [vp, vp, u64, vp, vp]
         L.ccj_compact_workspace_size.restype = C.c_size_t
         L.ccj_compact_workspace_size.argtypes = [u64, u64, C.c_uint32, C.c_uint32, C.c_uint32]
@@ -173,6 +174,17 @@ def result_checksum(out, chunk: int, row_base: int = 0, row_map=None, stream=Non
     torch.cuda.synchronize()
     m, l2 = acc.cpu().tolist()
     return m, l2 & 0xFFFFFFFFFFFFFFFF
+
+
+def gen_c3_keys(n: int, seed: int, n_build: int, cf: int = 1, hit_ppm: int = 100000, first_row: int = 0,
+                out=None, stream=None):
+    """Device C3 probe column (Zipf-skewed hits at hit_ppm / 1e6, misses never match)."""
+    import torch
+    if out is None:
+        out = torch.empty(n, dtype=torch.int64, device=torch.device("cuda", torch.cuda.current_device()))
+    check(lib().ccj_gen_c3_keys(_ptr(out), n, seed, first_row, n_build, cf, hit_ppm, _stream(stream)),
+          "ccj_gen_c3_keys")
+    return out
 
 
 def gen_reference_keys(first: int, n: int, n_total: int, cf: int = 1, out=None, stream=None):

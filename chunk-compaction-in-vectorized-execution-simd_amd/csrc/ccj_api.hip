@@ -571,6 +571,14 @@ int ccj_gen_uniform_keys(int64_t *d_out, uint64_t n, uint64_t seed, uint64_t fir
   return CCJ_OK;
 }
 
+int ccj_gen_c3_keys(int64_t *d_out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t n_build, uint64_t cf,
+                    uint32_t hit_ppm, ccj_stream stream) {
+  if ((!d_out && n) || cf == 0 || n_build == 0 || n_build >= (1ull << 62) || hit_ppm > 1000000)
+    return fail(CCJ_ERR_INVALID, "ccj_gen_c3_keys: bad argument");
+  HIP_TRY(ccj::launch_gen_c3(d_out, n, seed, first_row, n_build, cf, hit_ppm, (hipStream_t)stream), "gen c3 keys");
+  return CCJ_OK;
+}
+
 int ccj_gen_reference_keys(int64_t *d_out, uint64_t first, uint64_t n, uint64_t n_total, uint64_t cf,
                            ccj_stream stream) {
   if ((!d_out && n) || cf == 0 || first + n > n_total) return fail(CCJ_ERR_INVALID, "ccj_gen_reference_keys: bad argument");

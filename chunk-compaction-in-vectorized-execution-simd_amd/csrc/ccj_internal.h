@@ -87,6 +87,8 @@ hipError_t launch_scatter_payload(const int64_t *src, uint32_t n_cols, const uin
 hipError_t launch_lp_max_dup(const int64_t *slots, uint64_t n_slots, uint32_t max_run, uint32_t *out, hipStream_t s);
 hipError_t launch_lp_runs(const int64_t *slots, uint64_t n_slots, uint32_t *seg_stats, hipStream_t s);
 constexpr uint64_t kRunSegment = 4096;
+hipError_t launch_gen_c3(int64_t *out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t n_build, uint64_t cf,
+                         uint32_t hit_ppm, hipStream_t s);
 hipError_t launch_gen_uniform(int64_t *out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t range,
                               hipStream_t s);
 hipError_t launch_probe_cost(int kind, const int64_t *table, const uint32_t *off, uint32_t mask,

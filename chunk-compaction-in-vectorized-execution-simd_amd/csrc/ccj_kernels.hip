@@ -667,6 +667,42 @@ __device__ __forceinline__ uint64_t splitmix_at(uint64_t seed, uint64_t i) {
   return z ^ (z >> 31);
 }
 
+// C3 probe stream: the device twin of oracle/ccj_gen.h ccj_c3_key (same integer arithmetic).
+__device__ __forceinline__ uint32_t bitlen64(uint64_t x) { return x ? 64u - (uint32_t)__clzll(x) : 0u; }
+
+__device__ __forceinline__ uint64_t perm_n(uint64_t x, uint64_t n, uint64_t seed) {
+  const uint32_t k = n > 1 ? bitlen64(n - 1) : 1u;
+  const uint64_t mask = k >= 64 ? ~0ull : (1ull << k) - 1;
+  do {
+    x = (x * 0xd1342543de82ef95ull + (seed | 1ull)) & mask;
+    x ^= x >> (k / 2 + 1);
+  } while (x >= n);
+  return x;
+}
+
+__global__ void gen_c3(int64_t *out, uint64_t n, uint64_t seed, uint64_t first, uint64_t n_build, uint64_t cf,
+                       uint32_t hit_ppm) {
+  const uint64_t n_unique = n_build / cf + (n_build % cf != 0);
+  const uint64_t step = n_unique ? n_build / n_unique : 1;
+  const uint32_t levels = bitlen64(n_unique);
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = first + t;
+    const uint64_t z1 = splitmix_at(seed, 3 * i), z2 = splitmix_at(seed, 3 * i + 1);
+    const uint64_t z3 = splitmix_at(seed, 3 * i + 2);
+    int64_t key;
+    if (z1 % 1000000ull < hit_ppm && n_unique) {
+      const uint32_t b = (uint32_t)((z2 >> 32) % levels);
+      const uint64_t lo = 1ull << b;
+      const uint64_t hi = (b + 1 < 64 && (2ull << b) - 1 < n_unique) ? (2ull << b) - 1 : n_unique;
+      const uint64_t r = lo + (z2 & 0xffffffffull) % (hi - lo + 1);
+      key = (int64_t)(perm_n(r - 1, n_unique, seed) * step);
+    } else {
+      key = (int64_t)(n_build + z3 % ((1ull << 62) - n_build));
+    }
+    out[t] = key;
+  }
+}
+
 __global__ void gen_uniform(int64_t *out, uint64_t n, uint64_t seed, uint64_t first, uint64_t range) {
   for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x)
     out[t] = (int64_t)(splitmix_at(seed, first + t) % range);
@@ -909,6 +945,13 @@ hipError_t launch_scatter_payload(const int64_t *src, uint32_t n_cols, const uin
   if (positions == 0 || n_cols == 0) return hipSuccess;
   hipLaunchKernelGGL(scatter_payload, dim3(grid_for(positions * n_cols, 256)), dim3(256), 0, s, src, n_cols, row,
                      positions, dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_gen_c3(int64_t *out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t n_build, uint64_t cf,
+                         uint32_t hit_ppm, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(gen_c3, dim3(grid_for(n, 256)), dim3(256), 0, s, out, n, seed, first_row, n_build, cf, hit_ppm);
   return hipGetLastError();
 }
 

@@ -277,6 +277,12 @@ int ccj_segment_chunk_counts(const uint64_t *d_seg_counts, uint32_t n_segs, uint
  * Replaces the reference's host-side source (main.cpp:41-55 + DataCollection::FetchChunk). */
 int ccj_gen_uniform_keys(int64_t *d_out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t range,
                          ccj_stream stream);
+/* C3 probe column (BASELINE configs[2]): row i is, with probability hit_ppm / 1e6, a
+ * build key of the reference generator (n_build, cf) drawn with Zipf-like skew (log-uniform rank
+ * over dyadic levels, ranks spread by a fixed permutation), else a key in [n_build, 2^62) that
+ * matches nothing — the stream of oracle/ccj_gen.h ccj_c3_key. */
+int ccj_gen_c3_keys(int64_t *d_out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t n_build, uint64_t cf,
+                    uint32_t hit_ppm, ccj_stream stream);
 /* Build-side keys first..first+n-1 of the reference generator for n_total tuples
  * (linear_probing_ht.cpp:14-25: key t = (t / cf) * step), e.g. for sharding the build side. */
 int ccj_gen_reference_keys(int64_t *d_out, uint64_t first, uint64_t n, uint64_t n_total, uint64_t cf,

@@ -1,6 +1,6 @@
 /* ccj_gen.h — fully specified synthetic-input generators shared by the oracle, the
  * reference driver and the tests.  TEST INFRASTRUCTURE (see oracle/README.md): the product
- * library carries its own device copy of the same generator in csrc/ccj_gen_device.h.
+ * library carries its own device copy of the same generators in csrc/ccj_kernels.hip.
  *
  * Nothing here exists in the reference; the reference's main.cpp draws probe keys with
  * std::mt19937(2) + std::uniform_int_distribution<int>(0, n) (main.cpp:43,53), whose algorithm
@@ -34,6 +34,43 @@ static inline uint64_t ccj_splitmix_at(uint64_t seed, uint64_t i) {
 /* Uniform probe key in [0, range): the i-th key of the stream (seed, range). */
 static inline int64_t ccj_uniform_key(uint64_t seed, uint64_t i, uint64_t range) {
   return (int64_t)(ccj_splitmix_at(seed, i) % range);
+}
+
+/* ---- C3 probe stream: Zipf-skewed hits, ~hit_ppm/1e6 match rate ---- */
+static inline uint32_t ccj_bitlen(uint64_t x) { return x ? 64u - (uint32_t)__builtin_clzll(x) : 0u; }
+
+/* A fixed bijection on [0, n) (n >= 1): an odd multiply + add + xor-shift on the enclosing
+ * power-of-two range, cycle-walked back into [0, n). */
+static inline uint64_t ccj_perm(uint64_t x, uint64_t n, uint64_t seed) {
+  const uint32_t k = n > 1 ? ccj_bitlen(n - 1) : 1u;
+  const uint64_t mask = k >= 64 ? ~0ULL : (1ULL << k) - 1;
+  do {
+    x = (x * 0xd1342543de82ef95ULL + (seed | 1ULL)) & mask;
+    x ^= x >> (k / 2 + 1);
+  } while (x >= n);
+  return x;
+}
+
+/* Row i of the C3 stream over the reference generator's build side (n_build, cf): with
+ * probability hit_ppm / 1e6 a build key whose rank r in [1, n_unique] is log-uniform over dyadic
+ * levels (a bit length b uniform in [1, bitlen(n_unique)], r uniform in that level: the
+ * integer-only stand-in for Zipf s = 1, density ~ 1/r), mapped through ccj_perm so the popular
+ * keys spread over the table; otherwise a key in [n_build, 2^62), which is never a build key
+ * (every build key is < n_build, linear_probing_ht.cpp:16-25). */
+static inline int64_t ccj_c3_key(uint64_t seed, uint64_t i, uint64_t n_build, uint64_t cf, uint32_t hit_ppm) {
+  const uint64_t z1 = ccj_splitmix_at(seed, 3 * i), z2 = ccj_splitmix_at(seed, 3 * i + 1);
+  const uint64_t z3 = ccj_splitmix_at(seed, 3 * i + 2);
+  const uint64_t n_unique = n_build / cf + (n_build % cf != 0);
+  if (z1 % 1000000ULL < hit_ppm && n_unique) {
+    const uint64_t step = n_build / n_unique;
+    const uint32_t levels = ccj_bitlen(n_unique);
+    const uint32_t b = (uint32_t)((z2 >> 32) % levels); /* rank bit length b + 1 */
+    const uint64_t lo = 1ULL << b;
+    const uint64_t hi = (b + 1 < 64 && (2ULL << b) - 1 < n_unique) ? (2ULL << b) - 1 : n_unique;
+    const uint64_t r = lo + (z2 & 0xffffffffULL) % (hi - lo + 1);
+    return (int64_t)(ccj_perm(r - 1, n_unique, seed) * step);
+  }
+  return (int64_t)(n_build + z3 % ((1ULL << 62) - n_build));
 }
 
 /* ---- mt19937 / mt19937_64 (Matsumoto & Nishimura), std:: parameterisation ---- */

@@ -259,6 +259,28 @@ uint64_t ccj_o_count_uniform(uint64_t seed, uint64_t row_begin, uint64_t row_end
   return matches;
 }
 
+void ccj_o_gen_c3(uint64_t seed, uint64_t row_begin, uint64_t n, uint64_t n_build, uint64_t cf, uint32_t hit_ppm,
+                  int64_t *out, int threads) {
+  if (threads <= 0) threads = omp_get_max_threads();
+#pragma omp parallel for num_threads(threads) schedule(static)
+  for (uint64_t i = 0; i < n; ++i) out[i] = ccj_c3_key(seed, row_begin + i, n_build, cf, hit_ppm);
+}
+
+uint64_t ccj_o_count_c3(uint64_t seed, uint64_t row_begin, uint64_t row_end, uint64_t n_build, uint64_t cf,
+                        uint32_t hit_ppm, uint64_t *l2_out, int threads) {
+  uint64_t matches = 0, l2 = 0;
+  if (threads <= 0) threads = omp_get_max_threads();
+#pragma omp parallel for num_threads(threads) schedule(static) reduction(+ : matches, l2)
+  for (uint64_t i = row_begin; i < row_end; ++i) {
+    int64_t k = ccj_c3_key(seed, i, n_build, cf, hit_ppm);
+    uint64_t m = ccj_o_ref_multiplicity(k, n_build, cf);
+    matches += m;
+    l2 += m * ccj_l2_term(i, k);
+  }
+  if (l2_out) *l2_out = l2;
+  return matches;
+}
+
 /* compactor.cpp:5-41 simulated literally (with the fresh temp chunk of the commented :36, which
  * removes the aliasing defect of SURVEY §A.3): a full chunk passes through (:6); otherwise rows
  * are appended to the cache (:12-19); on overflow the cache is topped up to `chunk`, emitted,

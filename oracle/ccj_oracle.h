@@ -62,6 +62,13 @@ void ccj_o_gen_uniform(uint64_t seed, uint64_t row_begin, uint64_t n, uint64_t r
 uint64_t ccj_o_count_uniform(uint64_t seed, uint64_t row_begin, uint64_t row_end, uint64_t range,
                              uint64_t n_build, uint64_t cf, uint64_t *l2, int threads);
 
+/* C3 probe stream (ccj_gen.h ccj_c3_key): rows [row_begin, row_begin + n), and its exact L1/L2
+ * answer by membership over rows [row_begin, row_end). */
+void ccj_o_gen_c3(uint64_t seed, uint64_t row_begin, uint64_t n, uint64_t n_build, uint64_t cf, uint32_t hit_ppm,
+                  int64_t *out, int threads);
+uint64_t ccj_o_count_c3(uint64_t seed, uint64_t row_begin, uint64_t row_end, uint64_t n_build, uint64_t cf,
+                        uint32_t hit_ppm, uint64_t *l2, int threads);
+
 /* Compaction order of compactor.cpp:5-41 (with the fresh-temp fix of :36).  Segments are the
  * Next results in pipeline order, seg_counts[s] rows each.  For every input row (segments
  * concatenated) writes its destination slot dest[row] = out_chunk * chunk + offset.

@@ -54,6 +54,9 @@ def lib():
         L.ccj_o_gen_uniform.argtypes = [u64, u64, u64, u64, i64p, C.c_int]
         L.ccj_o_count_uniform.restype = u64
         L.ccj_o_count_uniform.argtypes = [u64, u64, u64, u64, u64, u64, u64p, C.c_int]
+        L.ccj_o_gen_c3.argtypes = [u64, u64, u64, u64, u64, C.c_uint32, i64p, C.c_int]
+        L.ccj_o_count_c3.restype = u64
+        L.ccj_o_count_c3.argtypes = [u64, u64, u64, u64, u64, C.c_uint32, u64p, C.c_int]
         L.ccj_o_compact_plan.restype = u64
         L.ccj_o_compact_plan.argtypes = [u32p, u64, C.c_uint32, u64p, u32p]
         L.ccj_o_compact_plan_threshold.restype = u64
@@ -142,6 +145,19 @@ class Table:
 def count_uniform(seed, row_begin, row_end, rng, n_build, cf, threads=0):
     l2 = C.c_uint64(0)
     m = lib().ccj_o_count_uniform(seed, row_begin, row_end, rng, n_build, cf, C.byref(l2), threads)
+    return int(m), int(l2.value)
+
+
+def c3_keys(seed, begin, end, n_build, cf, hit_ppm=100000, threads=0):
+    """C3 probe keys of rows [begin, end) (ccj_gen.h ccj_c3_key)."""
+    out = np.empty(end - begin, dtype=np.int64)
+    lib().ccj_o_gen_c3(seed, begin, end - begin, n_build, cf, hit_ppm, _p(out, C.c_int64), threads)
+    return out
+
+
+def count_c3(seed, begin, end, n_build, cf, hit_ppm=100000, threads=0):
+    l2 = C.c_uint64(0)
+    m = lib().ccj_o_count_c3(seed, begin, end, n_build, cf, hit_ppm, C.byref(l2), threads)
     return int(m), int(l2.value)
 
 

@@ -276,9 +276,11 @@ int RunPipeline(size_t joins, size_t cf, size_t lhs, size_t rhs, int compact, bo
 // key generation and the per-chunk column fill stand in for DataCollection::FetchChunk and are
 // untimed, as in main.cpp:88-94): Probe + while (HasNext) Next, counting matches only.
 template <typename Table>
-void BenchProbe(Table &ht, Variant v, size_t n_probe, uint64_t range, uint64_t seed) {
+void BenchProbe(Table &ht, Variant v, size_t n_probe, uint64_t range, uint64_t seed, bool c3, size_t n_build,
+                size_t cf) {
   std::vector<int64_t> keys(n_probe);
-  for (size_t i = 0; i < n_probe; ++i) keys[i] = ccj_uniform_key(seed, i, range);
+  for (size_t i = 0; i < n_probe; ++i)
+    keys[i] = c3 ? ccj_c3_key(seed, i, n_build, cf, 100000) : ccj_uniform_key(seed, i, range);
   std::vector<AttributeType> in_types{AttributeType::INTEGER};
   std::vector<AttributeType> out_types{AttributeType::INTEGER, AttributeType::INTEGER, AttributeType::INTEGER};
   DataChunk input(in_types);
@@ -313,7 +315,7 @@ void Usage() {
   fprintf(stderr,
           "ref_driver probe <lp|chain> <next|inone|simdnext|simdinone> B n_build cf n_probe range seed gen selmode trace\n"
           "ref_driver pipeline <lp|chain> B joins cf lhs rhs compact [count_only]\n"
-          "ref_driver bench <lp|chain> <next|inone|simdnext|simdinone> B n_build cf n_probe range seed\n");
+          "ref_driver bench <lp|chain> <next|inone|simdnext|simdinone> B n_build cf n_probe range seed [c3]\n");
   exit(2);
 }
 
@@ -358,7 +360,8 @@ int main(int argc, char **argv) {
                        argc > 9 && atoi(argv[9]) != 0);
   }
   if (cmd == "bench") {
-    if (argc != 10) Usage();
+    if (argc != 10 && argc != 11) Usage();
+    const bool c3 = argc == 11 && !strcmp(argv[10], "c3");  // ccj_gen.h C3 stream instead of uniform
     const bool lp = !strcmp(argv[2], "lp");
     const Variant v = ParseVariant(argv[3]);
     kBlockSize = strtoull(argv[4], nullptr, 10);
@@ -367,10 +370,10 @@ int main(int argc, char **argv) {
     const uint64_t range = strtoull(argv[8], nullptr, 10), seed = strtoull(argv[9], nullptr, 10);
     if (lp) {
       LPHashTable ht(n_build, cf);
-      BenchProbe(ht, v, n_probe, range, seed);
+      BenchProbe(ht, v, n_probe, range, seed, c3, n_build, cf);
     } else {
       HashTable ht(n_build, cf);
-      BenchProbe(ht, v, n_probe, range, seed);
+      BenchProbe(ht, v, n_probe, range, seed, c3, n_build, cf);
     }
     return 0;
   }

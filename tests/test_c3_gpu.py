@@ -73,3 +73,27 @@ def test_c3_chaining_zipf_probe_and_compact(cf, chunk):
     assert np.array_equal(comp["row"].cpu().numpy()[:n_out * chunk][v], want_row[v])
     assert np.array_equal(comp["cols"][0].cpu().numpy()[:n_out * chunk][v], want_cols[0][v])
     assert np.array_equal(comp["payload"].cpu().numpy()[:n_out * chunk][v], want_pay[v])
+
+
+def test_c3_device_stream_equals_oracle():
+    """ccj_gen_c3_keys (device) is the oracle's ccj_c3_key stream, row for row."""
+    for n_build, cf, first in ((1 << 26, 1, 0), (100000, 3, 12345), (7, 2, 1 << 40)):
+        got = ccj.gen_c3_keys(1 << 18, 42, n_build, cf, first_row=first).cpu().numpy()
+        assert np.array_equal(got, O.c3_keys(42, first, first + (1 << 18), n_build, cf))
+
+
+@pytest.mark.parametrize("n_build,cf", [(1 << 20, 1), (1 << 20, 2)])
+def test_c3_probe_and_compact_at_scale(n_build, cf):
+    """C3 at 2^24 probes on a device-built chaining table: L1 + L2 against the membership answer,
+    and compaction keeps every match."""
+    n = 1 << 24
+    table = ccj.Table.reference(ccj.CHAIN, n_build, cf, ccj.LAYOUT_DEVICE)
+    keys = ccj.gen_c3_keys(n, 42, n_build, cf)
+    out = table.probe(keys, 2048)
+    m, l2 = ccj.result_checksum(out, 2048)
+    assert int(out["status"].item()) == 0
+    assert (m, l2) == O.count_c3(42, 0, n, n_build, cf)
+    comp = ccj.compact(out, 2048, cols=[keys])
+    torch.cuda.synchronize()
+    assert int(comp["status"].item()) == 0
+    assert int(comp["counts"][:int(comp["n"].item())].to(torch.int64).sum().item()) == m

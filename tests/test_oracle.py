@@ -195,3 +195,23 @@ def test_oracle_pipeline_is_the_join(kind, joins, n, rhs, cf, B):
     assert res[False] == res[True]
     want = sorted(tuple(int(c[i]) for c in cols) for i in range(n) for _ in range(int(mult[i])))
     assert [r[:joins] for r in res[False]] == want
+
+
+@pytest.mark.parametrize("n_build,cf", [(1 << 16, 1), (100000, 3)])
+def test_c3_stream(n_build, cf):
+    """C3 probe stream (ccj_gen.h ccj_c3_key): ~10 % hits, Zipf-like skew over the build keys,
+    misses never match; count_c3 is the exact membership answer."""
+    n = 1 << 20
+    keys = O.c3_keys(42, 5, 5 + n, n_build, cf)
+    mult = np.array([O.ref_multiplicity(int(k), n_build, cf) for k in keys[:20000]])
+    hit = keys < n_build
+    assert 0.095 < hit.mean() < 0.105
+    assert ((mult > 0) == hit[:20000]).all()  # a hit is a build key, a miss never is
+    _, c = np.unique(keys[hit], return_counts=True)
+    assert c.max() > 50 * np.median(c)  # skewed: the top rank is hit far more than a typical key
+    m, l2 = O.count_c3(42, 5, 5 + n, n_build, cf)
+    rows = np.arange(5, 5 + n, dtype=np.uint64)
+    mm = np.where(hit, np.array([O.ref_multiplicity(int(k), n_build, cf) if h else 0
+                                 for k, h in zip(keys, hit)]), 0)
+    assert m == int(mm.sum())
+    assert l2 == O.l2_sum(np.repeat(rows, mm), np.repeat(keys, mm))
