@@ -1,8 +1,8 @@
 """Multi-GPU radix-partitioned probe: one process per GPU, torch.distributed over
 RCCL ("nccl" backend = RCCL on ROCm, xGMI between the GPUs of a node).
 
-Per step, on every rank, the 2^30 local probe keys go through in B batches, pipelined on two HIP
-streams (compute, comm) with double-buffered send/receive slots:
+Per step, on every rank, the 2^30 local probe keys go through in B batches, pipelined on three
+HIP streams (partition, comm, probe) with double-buffered send/receive slots:
   1. owner partition of batch i (ccj_partition_by_owner_fixed, HIP): destination d's keys and u32
      row ids in fixed-capacity segment d, true counts beside them;
   2. all-to-all of counts, keys, rows with equal splits (three all_to_all_single calls on the comm
@@ -83,6 +83,7 @@ class ShardedProbe:
         dev = torch.device("cuda", torch.cuda.current_device())
         self.stream = stream or torch.cuda.Stream(device=dev)
         self.comm = torch.cuda.Stream(device=dev)
+        self.pstream = torch.cuda.Stream(device=dev)  # partitions run beside the previous probe
         # build side: reference generator keys (linear_probing_ht.cpp:14-25) of the whole table,
         # generated in slices, each slice split by owner; this rank keeps its own part.
         own = []
@@ -137,9 +138,9 @@ class ShardedProbe:
         lo, n = self._batch(i)
         if n not in self.fparts:
             self.fparts[n] = ccj.FixedOwnerPartitioner(n, self.world, self.seg_cap, device=keys.device)
-        self.stream.wait_event(self.ev_comm[s])  # the previous all-to-all from send slot s is done
-        self.fparts[n](keys[lo:lo + n], lo, self.sk[s], self.sr[s], self.sc[s], self.status, stream=self.stream)
-        self.ev_part[s].record(self.stream)
+        self.pstream.wait_event(self.ev_comm[s])  # the previous all-to-all from send slot s is done
+        self.fparts[n](keys[lo:lo + n], lo, self.sk[s], self.sr[s], self.sc[s], self.status, stream=self.pstream)
+        self.ev_part[s].record(self.pstream)
 
     def _exchange(self, i):
         s = i % 2
@@ -183,6 +184,7 @@ class ShardedProbe:
         assert keys.numel() == self.n_probe and row_base == self.rank * self.n_probe
         self.status.zero_()
         self.stream.wait_stream(torch.cuda.current_stream())
+        self.pstream.wait_stream(torch.cuda.current_stream())
         self._partition(keys, 0)
         self._exchange(0)
         m, l2 = 0, 0
@@ -196,6 +198,7 @@ class ShardedProbe:
                                              stream=self.stream)
                 m, l2 = m + bm, (l2 + bl) % (1 << 64)
         torch.cuda.current_stream().wait_stream(self.stream)
+        torch.cuda.current_stream().wait_stream(self.pstream)
         if int(self.status.item()):  # a fixed-capacity segment overflowed: redo with exact sizes
             self.last_exact = True
             return self.step_exact(keys, row_base, verify)

@@ -215,8 +215,9 @@ hipError_t launch_partition_fixed(const int64_t *keys, uint64_t n, uint32_t part
                                   void *ws, hipStream_t s) {
   const uint32_t lp = log2u(parts);
   const Digit dg{lp == 0 ? 64u : 64u - lp, parts - 1};
-  return split_pass<uint32_t, true>(keys, nullptr, n, parts, dg, row_base, out_keys, out_rows, out_counts, ws, s,
-                                    seg_cap, status);
+  // order inside a destination segment does not matter to the probe: rank with LDS atomics
+  return split_pass<uint32_t, false>(keys, nullptr, n, parts, dg, row_base, out_keys, out_rows, out_counts, ws, s,
+                                     seg_cap, status);
 }
 
 namespace {

@@ -257,7 +257,8 @@ int ccj_partition_by_owner(const int64_t *d_keys, uint64_t n, uint32_t parts, ui
                            void *d_workspace, size_t workspace_bytes, ccj_stream stream);
 
 /* Fixed-capacity form for a host-synchronisation-free exchange: destination d's keys and their
- * u32 row ids (row_base + i) go to [d*seg_cap, d*seg_cap + count_d), so every all-to-all split is
+ * u32 row ids (row_base + i) go to [d*seg_cap, d*seg_cap + count_d) — grouped exactly, in no
+ * particular order inside a segment — so every all-to-all split is
  * seg_cap and the send/receive sizes need no host round trip; d_out_counts gets the true counts.
  * Rows of a destination beyond seg_cap are dropped and CCJ_FLAG_CAP_OVERFLOW is OR-ed into
  * *d_status (the caller re-runs that batch with ccj_partition_by_owner). */
