@@ -143,6 +143,109 @@ constexpr int kBlock = kWave * kChunkWaves;
 // Count + scan: per (round, row group) ballot counts, exclusive scan.  Emit: every match goes to
 // s_off[r][j] + its ballot prefix — the reference's round-major, idx-ascending result_vector
 // order (L3) — with the payload (== probe key) taken from LDS.
+// Walk: every row's whole run (LP: home slot up to the first empty slot; chain: the bucket's CSR
+// range) through aligned 32-byte windows; s_mm[row] gets bit r for every round r in which the row
+// matches.  Lane `lane` of wave `wave` owns rows (q * 4 + wave) * 64 + lane for the q set in
+// `act`; G cursors per lane each take every G-th of them and move on as soon as their run ends.
+// on_end(row, rounds) reports a finished run (rounds = occupied slots / chain keys walked).
+// Returns true if some run is longer than kMaxFastRounds (the caller then uses rounds_generic).
+template <int KIND, int G, typename OnEnd>
+__device__ __forceinline__ bool walk_rows(const ProbeParams &p, const int64_t *s_key, uint32_t *s_mm, uint32_t act,
+                                          uint32_t nq, uint32_t wave, uint32_t lane, OnEnd on_end) {
+  bool long_run = false;
+  uint32_t q[G], cur[G], r0[G], lim[G], mm[G];
+  int64_t kj[G];
+  uint32_t live = 0, start = 0;  // bit g: cursor has a row / row still needs its CSR range
+  auto next_active = [&](uint32_t from) -> uint32_t {
+    for (uint32_t t = from; t < nq; t += G)
+      if ((act >> t) & 1u) return t;
+    return nq;
+  };
+  auto begin_row = [&](int g) {
+    kj[g] = s_key[(q[g] * kChunkWaves + wave) * kWave + lane];
+    const uint32_t h = (uint32_t)murmurhash64((uint64_t)kj[g]) & p.mask;
+    cur[g] = h;  // LP: home slot; chain: bucket until its CSR range is loaded
+    r0[g] = 0;
+    mm[g] = 0;
+    live |= 1u << g;
+    if (KIND == CCJ_TABLE_CHAIN) start |= 1u << g;
+  };
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    cur[g] = r0[g] = lim[g] = mm[g] = 0;
+    kj[g] = 0;
+    q[g] = next_active(g);
+    if (q[g] < nq) begin_row(g);
+  }
+  while (__ballot(live != 0u) != 0ull) {
+    longlong2 v[G][kWin / 2];
+    uint32_t o0[G], o1[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if ((live >> g) & 1u) {
+        if (KIND == CCJ_TABLE_CHAIN && ((start >> g) & 1u)) {
+          o0[g] = p.off[cur[g]];  // chaining_ht.cpp:46-49: bucket -> chain (CSR range)
+          o1[g] = p.off[cur[g] + 1];
+        } else {
+          const longlong2 *w = reinterpret_cast<const longlong2 *>(p.table + (cur[g] & ~(uint32_t)(kWin - 1)));
+#pragma unroll
+          for (int t = 0; t < kWin / 2; ++t) v[g][t] = w[t];
+        }
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if ((live >> g) & 1u) {
+        const uint32_t row = (q[g] * kChunkWaves + wave) * kWave + lane;
+        bool done = false;
+        if (KIND == CCJ_TABLE_CHAIN && ((start >> g) & 1u)) {
+          start &= ~(1u << g);
+          cur[g] = o0[g];
+          lim[g] = o1[g];
+          done = cur[g] == lim[g];  // empty bucket: not in the active set (chaining_ht.cpp:52-55)
+        } else {
+          const uint32_t blk = cur[g] & ~(uint32_t)(kWin - 1);
+          const uint32_t off = cur[g] - blk;
+          bool go = true;
+#pragma unroll
+          for (int t = 0; t < kWin; ++t) {
+            const int64_t val = (t & 1) ? v[g][t >> 1].y : v[g][t >> 1].x;
+            if (go && (uint32_t)t >= off) {
+              const uint32_t r = r0[g] + (uint32_t)t - off;
+              const bool stop = KIND == CCJ_TABLE_LP ? (val == -1) : (blk + (uint32_t)t == lim[g]);
+              if (stop) {
+                go = false;
+                on_end(row, r);
+              } else if (r >= (uint32_t)kMaxFastRounds) {
+                go = false;
+                long_run = true;
+              } else if (val == kj[g]) {
+                mm[g] |= 1u << r;
+              }
+            }
+          }
+          if (go) {
+            r0[g] += (uint32_t)kWin - off;
+            cur[g] = KIND == CCJ_TABLE_LP ? ((blk + kWin) & p.mask) : blk + kWin;
+            if (KIND == CCJ_TABLE_CHAIN && cur[g] == lim[g]) {
+              on_end(row, r0[g]);
+              go = false;
+            }
+          }
+          done = !go;
+        }
+        if (done) {
+          s_mm[row] = mm[g];
+          live &= ~(1u << g);
+          q[g] = next_active(q[g] + G);
+          if (q[g] < nq) begin_row(g);
+        }
+      }
+    }
+  }
+  return long_run;
+}
+
 template <int KIND, int G>
 __global__ __launch_bounds__(kBlock) void probe_chunks(ProbeParams p) {
   __shared__ int64_t s_key[kMaxChunk];
@@ -191,98 +294,9 @@ __global__ __launch_bounds__(kBlock) void probe_chunks(ProbeParams p) {
 
   // Walk.
   uint32_t lane_rounds = 0;
-  bool long_run = false;
-  {
-    uint32_t q[G], cur[G], r0[G], lim[G], mm[G];
-    int64_t kj[G];
-    uint32_t live = 0, start = 0;  // bit g: cursor has a row / row still needs its CSR range
-    auto next_active = [&](uint32_t from) -> uint32_t {
-      for (uint32_t t = from; t < nq; t += G)
-        if ((act >> t) & 1u) return t;
-      return nq;
-    };
-    auto begin_row = [&](int g) {
-      kj[g] = s_key[(q[g] * kChunkWaves + wave) * kWave + lane];
-      const uint32_t h = (uint32_t)murmurhash64((uint64_t)kj[g]) & p.mask;
-      cur[g] = h;  // LP: home slot; chain: bucket until its CSR range is loaded
-      r0[g] = 0;
-      mm[g] = 0;
-      live |= 1u << g;
-      if (KIND == CCJ_TABLE_CHAIN) start |= 1u << g;
-    };
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      cur[g] = r0[g] = lim[g] = mm[g] = 0;
-      kj[g] = 0;
-      q[g] = next_active(g);
-      if (q[g] < nq) begin_row(g);
-    }
-    while (__ballot(live != 0u) != 0ull) {
-      longlong2 v[G][kWin / 2];
-      uint32_t o0[G], o1[G];
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        if ((live >> g) & 1u) {
-          if (KIND == CCJ_TABLE_CHAIN && ((start >> g) & 1u)) {
-            o0[g] = p.off[cur[g]];  // chaining_ht.cpp:46-49: bucket -> chain (CSR range)
-            o1[g] = p.off[cur[g] + 1];
-          } else {
-            const longlong2 *w = reinterpret_cast<const longlong2 *>(p.table + (cur[g] & ~(uint32_t)(kWin - 1)));
-#pragma unroll
-            for (int t = 0; t < kWin / 2; ++t) v[g][t] = w[t];
-          }
-        }
-      }
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        if ((live >> g) & 1u) {
-          bool done = false;
-          if (KIND == CCJ_TABLE_CHAIN && ((start >> g) & 1u)) {
-            start &= ~(1u << g);
-            cur[g] = o0[g];
-            lim[g] = o1[g];
-            done = cur[g] == lim[g];  // empty bucket: not in the active set (chaining_ht.cpp:52-55)
-          } else {
-            const uint32_t blk = cur[g] & ~(uint32_t)(kWin - 1);
-            const uint32_t off = cur[g] - blk;
-            bool go = true;
-#pragma unroll
-            for (int t = 0; t < kWin; ++t) {
-              const int64_t val = (t & 1) ? v[g][t >> 1].y : v[g][t >> 1].x;
-              if (go && (uint32_t)t >= off) {
-                const uint32_t r = r0[g] + (uint32_t)t - off;
-                const bool stop = KIND == CCJ_TABLE_LP ? (val == -1) : (blk + (uint32_t)t == lim[g]);
-                if (stop) {
-                  go = false;
-                  lane_rounds = r > lane_rounds ? r : lane_rounds;
-                } else if (r >= (uint32_t)kMaxFastRounds) {
-                  go = false;
-                  long_run = true;
-                } else if (val == kj[g]) {
-                  mm[g] |= 1u << r;
-                }
-              }
-            }
-            if (go) {
-              r0[g] += (uint32_t)kWin - off;
-              cur[g] = KIND == CCJ_TABLE_LP ? ((blk + kWin) & p.mask) : blk + kWin;
-              if (KIND == CCJ_TABLE_CHAIN && cur[g] == lim[g]) {
-                lane_rounds = r0[g] > lane_rounds ? r0[g] : lane_rounds;
-                go = false;
-              }
-            }
-            done = !go;
-          }
-          if (done) {
-            s_mm[(q[g] * kChunkWaves + wave) * kWave + lane] = mm[g];
-            live &= ~(1u << g);
-            q[g] = next_active(q[g] + G);
-            if (q[g] < nq) begin_row(g);
-          }
-        }
-      }
-    }
-  }
+  const bool long_run = walk_rows<KIND, G>(p, s_key, s_mm, act, nq, wave, lane, [&](uint32_t, uint32_t r) {
+    lane_rounds = r > lane_rounds ? r : lane_rounds;
+  });
 
   // Block-wide round count and long-run flag.
   {
@@ -559,6 +573,183 @@ __global__ __launch_bounds__(kFlatThreads) void probe_flat(ProbeParams p) {
   if (p.status && (overflow || total > p.cap)) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
 }
 
+// Several small chunks per workgroup (chunk B a multiple of 64, B <= 512: the reference's default
+// kBlockSize 256, base.h:42).  One chunk per workgroup would leave each lane a single row — one
+// window load in flight and a workgroup's fixed cost per 256 rows; here 2048 / B chunks share the
+// 256 threads, so every lane again walks 8 rows.  Row group j (64 rows) belongs to chunk
+// j / (B / 64); the walk is probe_chunks', and counts, scan and emit are done per chunk, so each
+// chunk's output is exactly probe_chunks' (L3).
+template <int KIND, int G>
+__global__ __launch_bounds__(kBlock) void probe_multi(ProbeParams p) {
+  constexpr uint32_t kMaxSub = kMaxChunk / kWave;  // 32 chunks of 64 rows at most
+  __shared__ int64_t s_key[kMaxChunk];
+  __shared__ uint32_t s_mm[kMaxChunk];
+  __shared__ uint32_t s_off[kMaxFastRounds * 32];  // (round r, row group j) -> count, then offset
+  __shared__ uint32_t s_rounds[kMaxSub], s_total[kMaxSub], s_cnt[kMaxSub];
+  __shared__ uint64_t s_base[kMaxSub];
+  __shared__ uint32_t s_long;
+  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  const uint32_t B = p.chunk, gpc = B / kWave, K = kMaxChunk / B;
+  const uint64_t c0 = (uint64_t)blockIdx.x * K;
+  const uint32_t nk = (uint32_t)(p.n_chunks - c0 < K ? p.n_chunks - c0 : K);  // chunks of this block
+  uint32_t flags = 0;
+  if (tid < kMaxSub) {
+    s_rounds[tid] = 0;
+    s_total[tid] = 0;
+    uint64_t base = 0;
+    uint32_t cnt = 0;
+    if (tid < nk) {
+      const uint64_t c = c0 + tid;
+      base = p.chunk_base ? p.chunk_base[c] : c * B;
+      const uint64_t rem = p.n_rows - base;
+      const uint32_t phys = rem < B ? (uint32_t)rem : B;
+      cnt = p.counts ? p.counts[c] : phys;
+      if (cnt > B) {
+        flags |= CCJ_FLAG_BAD_INPUT;
+        cnt = B;
+      }
+    }
+    s_base[tid] = base;
+    s_cnt[tid] = cnt;
+  }
+  if (tid == 0) s_long = 0;
+  for (uint32_t q = tid; q < kMaxFastRounds * 32; q += kBlock) s_off[q] = 0u;
+  __syncthreads();
+
+  // Stage: the row of group j, lane l is row (j - k*gpc)*64 + l of chunk k = j / gpc.
+  uint32_t act = 0;
+  for (uint32_t i = tid, q = 0; i < kMaxChunk; i += kBlock, ++q) {
+    const uint32_t k = i / B, li = i - k * B;
+    int64_t key = 0;
+    if (k < nk && li < s_cnt[k]) {
+      const uint64_t base = s_base[k];
+      const uint64_t rem = p.n_rows - base;
+      const uint32_t phys = rem < B ? (uint32_t)rem : B;
+      const uint32_t r = phys_row(p, base, li);
+      if (r < phys) {
+        key = p.keys[base + r];
+        act |= 1u << q;
+      } else {
+        flags |= CCJ_FLAG_BAD_INPUT;
+      }
+    }
+    s_key[i] = key;
+    s_mm[i] = 0u;
+  }
+  __syncthreads();
+  const uint32_t nq = kMaxChunk / kWave / kChunkWaves;  // 8 row groups per wave
+
+  // Walk (rounds per chunk through LDS max).
+  const bool long_run = walk_rows<KIND, G>(p, s_key, s_mm, act, nq, wave, lane, [&](uint32_t row, uint32_t r) {
+    if (r) atomicMax(&s_rounds[row / B], r);
+  });
+  if (__ballot(long_run) != 0ull && lane == 0) s_long = 1;
+  __syncthreads();
+
+  if (s_long) {
+    // Rare: some run exceeds kMaxFastRounds; every chunk of the block takes the generic path.
+    if (wave == 0) {
+      for (uint32_t k = 0; k < nk; ++k) {
+        const uint64_t c = c0 + k, base = s_base[k];
+        const uint64_t rem = p.n_rows - base;
+        const uint32_t phys = rem < B ? (uint32_t)rem : B;
+        uint32_t act_k = 0;
+        for (uint32_t j = 0; j < gpc; ++j) {
+          const uint32_t i = j * kWave + lane;
+          if (i < s_cnt[k] && phys_row(p, base, i) < phys) act_k |= 1u << j;
+        }
+        uint64_t total = 0;
+        uint32_t rounds = 0;
+        rounds_generic<KIND>(p, c, base, gpc, act_k, s_key + k * B, flags, total, rounds);
+        if (total > p.cap) flags |= CCJ_FLAG_CAP_OVERFLOW;
+        if (lane == 0) {
+          p.out_count[c] = (uint32_t)(total < p.cap ? total : p.cap);
+          if (p.out_rounds) p.out_rounds[c] = rounds;
+        }
+      }
+    }
+  } else {
+    // Count: matches per (round r, row group j).
+    for (uint32_t j = wave; j < kMaxChunk / kWave; j += kChunkWaves) {
+      const uint32_t m = s_mm[j * kWave + lane];
+      for (uint32_t any = wave_or(m); any != 0u; any &= any - 1u) {
+        const uint32_t r = (uint32_t)__builtin_ctz(any);
+        const uint32_t n = (uint32_t)__popcll(__ballot((m >> r) & 1u));
+        if (lane == 0) s_off[r * 32 + j] = n;
+      }
+    }
+    __syncthreads();
+    // Scan per chunk, round-major: wave w takes chunks k = w, w+4, ...; lane r holds round r.
+    for (uint32_t k = wave; k < nk; k += kChunkWaves) {
+      uint32_t tk = 0;
+      if (lane < kMaxFastRounds)
+        for (uint32_t j = k * gpc; j < (k + 1) * gpc; ++j) tk += s_off[lane * 32 + j];
+      uint32_t incl = tk;
+#pragma unroll
+      for (int d = 1; d < kMaxFastRounds; d <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
+        if (lane >= (uint32_t)d) incl += o;
+      }
+      if (lane < kMaxFastRounds) {
+        uint32_t run = incl - tk;
+        for (uint32_t j = k * gpc; j < (k + 1) * gpc; ++j) {
+          const uint32_t n = s_off[lane * 32 + j];
+          s_off[lane * 32 + j] = run;
+          run += n;
+        }
+        const uint64_t c = c0 + k;
+        const uint32_t rounds = s_rounds[k];
+        if (p.out_round_counts && lane < rounds) {
+          if (lane < p.max_rounds) p.out_round_counts[c * p.max_rounds + lane] = tk;  // Next return values
+        }
+        if (lane == kMaxFastRounds - 1) s_total[k] = incl;
+      }
+    }
+    __syncthreads();
+    // Emit: group j's matches of round r go to s_off[r][j] + ballot prefix in its chunk's output.
+    for (uint32_t jb = wave; jb < kMaxChunk / kWave; jb += kChunkWaves * kEmitRows) {
+      uint32_t m[kEmitRows], rr[kEmitRows];
+#pragma unroll
+      for (int g = 0; g < kEmitRows; ++g) {
+        const uint32_t j = jb + g * kChunkWaves, k = j / gpc;
+        m[g] = s_mm[j * kWave + lane];
+        rr[g] = m[g] ? phys_row(p, s_base[k], (j - k * gpc) * kWave + lane) : 0u;
+      }
+#pragma unroll
+      for (int g = 0; g < kEmitRows; ++g) {
+        const uint32_t j = jb + g * kChunkWaves, k = j / gpc;
+        const uint64_t c = c0 + k;
+        const uint64_t obase = (k < nk && p.out_base) ? p.out_base[c] : c * p.cap;
+        for (uint32_t any = wave_or(m[g]); any != 0u; any &= any - 1u) {
+          const uint32_t r = (uint32_t)__builtin_ctz(any);
+          const bool bit = (m[g] >> r) & 1u;
+          const uint64_t mb = __ballot(bit);
+          if (bit) {
+            const uint64_t o = (uint64_t)s_off[r * 32 + j] + lane_prefix(mb);
+            if (o < p.cap) {
+              const int64_t key = s_key[j * kWave + lane];
+              p.out_sel[obase + o] = rr[g];
+              if (p.out_payload) p.out_payload[obase + o] = key;  // matched table value == probe key
+              emit_extra<KIND>(p, obase, o, key, r);
+            }
+          }
+        }
+      }
+    }
+    if (tid < nk) {
+      const uint64_t c = c0 + tid;
+      const uint32_t total = s_total[tid];
+      if (total > p.cap) flags |= CCJ_FLAG_CAP_OVERFLOW;
+      if (p.out_round_counts && s_rounds[tid] > p.max_rounds) flags |= CCJ_FLAG_ROUND_OVERFLOW;
+      p.out_count[c] = (uint32_t)(total < p.cap ? total : p.cap);
+      if (p.out_rounds) p.out_rounds[c] = s_rounds[tid];
+    }
+  }
+  if (p.status) {
+    if (__ballot(flags != 0u) && flags) atomicOr(p.status, flags);
+  }
+}
+
 template <int KIND>
 hipError_t launch_kind(const ProbeParams &p, hipStream_t s) {
   // CCJ_WALK_ROWS (tuning override): rows per lane walked concurrently.
@@ -566,6 +757,12 @@ hipError_t launch_kind(const ProbeParams &p, hipStream_t s) {
     const char *e = getenv("CCJ_WALK_ROWS");
     return e ? atoi(e) : kWalkRows;
   }();
+  static const bool multi = getenv("CCJ_NO_MULTI") == nullptr;
+  if (multi && p.chunk % kWave == 0 && p.chunk <= 512 && !p.xcd_swizzle) {
+    const uint64_t per = kMaxChunk / p.chunk;
+    hipLaunchKernelGGL((probe_multi<KIND, 2>), dim3((unsigned)((p.n_chunks + per - 1) / per)), dim3(kBlock), 0, s, p);
+    return hipGetLastError();
+  }
   const dim3 g((unsigned)p.n_chunks), b(kBlock);
   if (walk <= 2) hipLaunchKernelGGL((probe_chunks<KIND, 2>), g, b, 0, s, p);
   else if (walk <= 4) hipLaunchKernelGGL((probe_chunks<KIND, 4>), g, b, 0, s, p);
