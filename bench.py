@@ -494,6 +494,8 @@ def main():
             "hbm_gbs_algorithmic": achieved,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         # measured DRAM bytes (whole 128-B lines per random slot read) per second
+                         "traffic_GBps": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
                          "kernel": ("ccj_probe_partitioned (2 slot-partition passes + probe_chunks)"
                                     if args.path == "partitioned" else "probe_chunks<LP,2>"),
                          "kernel_ms": kern_ms,

@@ -5,11 +5,12 @@
   profiles/TAG_pmc.json           per-kernel PMC counters (last dispatch of each counter pass)
   profiles/pmc_<workload>.json    HBM traffic per probe launch for bench.py's roofline.traffic
 
-Traffic = (FETCH_SIZE + WRITE_SIZE) * 1024 bytes per launch (rocprofv3 reports both in KiB).  The
-gfx950 x2 correction of FETCH_SIZE (MI355X_MICROARCH.md §HBM) applies to wide coalesced streaming
-reads; the probe's reads are dominated by random 32-byte window gathers issued as 64-byte requests
-(FETCH_SIZE == TCC_EA0_RDREQ x 64 B, RDREQ_32B == 0), so no factor is applied — both raw numbers are
-kept in TAG_pmc.json.
+Traffic = HBM bytes per launch from the L2's memory-side request counters, by request size:
+  reads  = 128 B x TCC_EA0_RDREQ_128B + 64 B x TCC_EA0_RDREQ_64B + 32 B x TCC_EA0_RDREQ_32B
+  writes = 64 B x TCC_EA0_WRREQ_64B + 32 B x (TCC_EA0_WRREQ - TCC_EA0_WRREQ_64B)
+Every read miss of the probe is a whole 128-B line (RDREQ_128B == RDREQ), which FETCH_SIZE tallies at
+64 B (MI355X_MICROARCH.md §HBM: double it) — so the request-size form equals 2 x FETCH_SIZE here.  The
+raw FETCH_SIZE / WRITE_SIZE (KiB) are kept in TAG_pmc.json beside it.
   usage: tools/prof_summary.py TAG [--n-probe N --n-build N]
 """
 import argparse
@@ -50,8 +51,11 @@ def main():
                 pmc[r["Kernel_Name"]]["VGPR_Count"] = int(r["VGPR_Count"])
     out = {"tag": a.tag, "kernel_stats": stats, "pmc": pmc}
     k = pmc.get(a.kernel, {})
-    if "FETCH_SIZE" in k and "WRITE_SIZE" in k:
-        fetch, write = k["FETCH_SIZE"] * 1024, k["WRITE_SIZE"] * 1024
+    if "TCC_EA0_RDREQ_128B_sum" in k and "TCC_EA0_WRREQ_sum" in k:
+        fetch = (128 * k["TCC_EA0_RDREQ_128B_sum"] + 64 * k.get("TCC_EA0_RDREQ_64B_sum", 0)
+                 + 32 * k.get("TCC_EA0_RDREQ_32B_sum", 0))
+        w64 = k.get("TCC_EA0_WRREQ_64B_sum", k["TCC_EA0_WRREQ_sum"])
+        write = 64 * w64 + 32 * (k["TCC_EA0_WRREQ_sum"] - w64)
         traffic = fetch + write
         avg_ns = stats.get(a.kernel, {}).get("avg_ns")
         out["traffic"] = {"fetch_bytes": fetch, "write_bytes": write, "hbm_bytes_per_launch": traffic,
@@ -62,8 +66,10 @@ def main():
                           "hbm_GBps": traffic / avg_ns if avg_ns else None}
         with open(os.path.join(dst, f"pmc_{a.workload}.json"), "w") as f:
             json.dump({"tag": a.tag, "kernel": a.kernel, "n_probe": a.n_probe, "n_build": a.n_build,
-                       "hbm_bytes_per_launch": traffic, "fetch_size_kib": k["FETCH_SIZE"],
-                       "write_size_kib": k["WRITE_SIZE"], "kernel_avg_ns": avg_ns}, f, indent=1)
+                       "hbm_bytes_per_launch": traffic, "read_bytes": fetch, "write_bytes": write,
+                       "rdreq_128b": k["TCC_EA0_RDREQ_128B_sum"], "wrreq": k["TCC_EA0_WRREQ_sum"],
+                       "fetch_size_kib": k.get("FETCH_SIZE"), "write_size_kib": k.get("WRITE_SIZE"),
+                       "kernel_avg_ns": avg_ns}, f, indent=1)
     with open(os.path.join(dst, f"{a.tag}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
     print(json.dumps(out.get("traffic", {}), indent=1))

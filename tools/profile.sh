@@ -12,7 +12,8 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 echo "[profile] kernel trace: bench.py $ARGS"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -f csv -d "$OUT/kt" -o kt -- python3 bench.py $ARGS > "$OUT/kt_bench.log" 2>&1 || exit $?
-for grp in FETCH_SIZE WRITE_SIZE "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" "TCC_HIT_sum TCC_MISS_sum" \
+for grp in FETCH_SIZE WRITE_SIZE "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" \
+           "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum" "TCC_HIT_sum TCC_MISS_sum" \
            "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES" "GRBM_GUI_ACTIVE"; do
   name=$(echo "$grp" | tr ' ' '+')
   echo "[profile] pmc $grp"
