@@ -106,7 +106,7 @@ hipError_t launch_compact(const ccj_compact_args &a, hipStream_t s);
 size_t partition_workspace(uint64_t n, uint32_t parts);
 // Slot-range partitioning for the L2-resident probe: partition p = slot >> window_bits, with the
 // partition bits split into a low digit (first LSD pass) and a high digit (second pass).
-constexpr uint32_t kWindowBits = 17;  // 2^17 slots = 1 MiB table window per partition
+constexpr uint32_t kWindowBits = 18;  // 2^18 slots = 2 MiB table window per partition
 struct SlotPlan {
   uint32_t window_bits, lo_bits, hi_bits;
 };

@@ -19,8 +19,8 @@ namespace ccj {
 namespace {
 
 constexpr int kTileThreads = 256;
-constexpr int kTileIters = 16;
-constexpr uint64_t kTile = (uint64_t)kTileThreads * kTileIters;  // 4096 keys per tile
+constexpr int kTileIters = 8;
+constexpr uint64_t kTile = (uint64_t)kTileThreads * kTileIters;  // 2048 keys per tile (24 KB of LDS image)
 
 struct Digit {
   uint32_t shift;  // >= 64: every key to digit 0
@@ -60,7 +60,14 @@ __global__ __launch_bounds__(kTileThreads) void part_scatter(const int64_t *keys
   __shared__ uint64_t s_glob[kMaxParts];
   __shared__ uint32_t s_loc[kMaxParts], s_run[kMaxParts];
   __shared__ uint32_t s_wave[kTileThreads / 64][kMaxParts];
-  const uint64_t tile = blockIdx.x;
+  // XCD-aware tile order: workgroups are dealt round-robin to the 8 XCDs; block b takes tile
+  // (b % 8) * (n8 / 8) + b / 8, so each XCD writes a contiguous range of tiles and the partial
+  // lines where one tile's digit segment meets the next one's are completed in one XCD's L2.
+  uint64_t tile = blockIdx.x;
+  {
+    const uint64_t n8 = n_tiles & ~7ull;
+    if (tile < n8) tile = (tile & 7) * (n8 >> 3) + (tile >> 3);
+  }
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint64_t t0 = tile * kTile;
   const uint32_t tn = (uint32_t)(n - t0 < kTile ? n - t0 : kTile);
@@ -250,12 +257,17 @@ hipError_t launch_segment_chunk_counts(const uint64_t *counts, uint32_t n_segs, 
 
 // ---- slot-range partitioning for the L2-resident probe ------------------------------------------
 SlotPlan slot_plan(uint64_t table_size) {
+  // CCJ_WINDOW_BITS (tuning override): log2 slots of table per partition.
+  static const uint32_t wbits = [] {
+    const char *e = getenv("CCJ_WINDOW_BITS");
+    return e ? (uint32_t)atoi(e) : kWindowBits;
+  }();
   SlotPlan pl{};
   const uint32_t sbits = log2u(table_size);  // table_size is a power of two
-  pl.window_bits = kWindowBits < sbits ? kWindowBits : sbits;
+  pl.window_bits = wbits < sbits ? wbits : sbits;
   if (sbits - pl.window_bits > 12) pl.window_bits = sbits - 12;  // two passes of <= 64 digits
   const uint32_t dbits = sbits - pl.window_bits;
-  pl.lo_bits = dbits < 6 ? dbits : 6;
+  pl.lo_bits = (dbits + 1) / 2 < 6 ? (dbits + 1) / 2 : 6;  // balanced passes
   pl.hi_bits = dbits - pl.lo_bits;
   return pl;
 }
