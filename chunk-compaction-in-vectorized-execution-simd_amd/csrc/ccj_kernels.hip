@@ -976,11 +976,198 @@ unsigned grid_for(uint64_t n, unsigned block) {
 
 }  // namespace
 
+// Pair variant of probe_flat: two lanes walk one row together through aligned 32-byte windows,
+// each loading 16 bytes of it, so the pair's two loads of one window are one L2 request (the
+// single-lane walk needs ~2.1 16-byte requests per row, this ~1.4).  The pair agrees on where the
+// run ends with one lane swap.  Keys are staged in LDS; R rows per pair are in flight, a finished
+// row's cursor takes the pair's next row at once.
+template <int KIND, int R>
+__global__ __launch_bounds__(kFlatThreads) void probe_pair(ProbeParams p) {
+  constexpr uint32_t WS = 4;                       // slots per window
+  constexpr uint32_t kPairs = kFlatThreads / 2;    // 128 rows walked side by side per step
+  constexpr uint32_t kStride = kPairs * R;         // row step of a refilled cursor
+  __shared__ uint32_t s_cnt, s_rounds;
+  __shared__ int64_t s_key[kMaxChunk];
+  __shared__ uint32_t s_sel[kFlatStage];
+  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1);
+  const uint32_t h = tid & 1u, pr = tid >> 1;
+  uint64_t c = blockIdx.x;
+  if (p.xcd_swizzle) {
+    const uint64_t n8 = p.n_chunks & ~7ull;
+    if (c < n8) c = (c & 7) * (n8 >> 3) + (c >> 3);
+  }
+  const uint64_t base = c * p.chunk;
+  const uint64_t rem = p.n_rows - base;
+  const uint32_t phys = rem < p.chunk ? (uint32_t)rem : p.chunk;
+  const uint64_t obase = c * p.cap;
+  for (uint32_t i = tid; i < phys; i += kFlatThreads) s_key[i] = __builtin_nontemporal_load(p.keys + base + i);
+  if (tid == 0) {
+    s_cnt = 0;
+    s_rounds = 0;
+  }
+  __syncthreads();
+  int64_t key[R];
+  uint32_t row[R], cur[R], lim[R], r0[R];
+  uint32_t need = 0, lane_rounds = 0, overflow = 0;
+  auto start = [&](int k, uint32_t i) {
+    row[k] = i;
+    r0[k] = 0;
+    while (i < phys) {
+      key[k] = s_key[i];
+      const uint32_t hh = (uint32_t)murmurhash64((uint64_t)key[k]) & p.mask;
+      if (KIND == CCJ_TABLE_LP) {
+        cur[k] = hh;
+        need |= 1u << k;
+        return;
+      }
+      cur[k] = p.off[hh];
+      lim[k] = p.off[hh + 1];
+      if (cur[k] != lim[k]) {
+        need |= 1u << k;
+        return;
+      }
+      i += kStride;  // empty bucket: no round
+      row[k] = i;
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    key[k] = 0;
+    cur[k] = lim[k] = 0;
+    start(k, k * kPairs + pr);
+  }
+  while (__ballot(need != 0u) != 0ull) {
+    longlong2 v[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      v[k].x = v[k].y = 0;
+      const uint32_t s0 = (cur[k] & ~(WS - 1)) + 2 * h;
+      if (((need >> k) & 1u) && (KIND == CCJ_TABLE_LP || s0 < lim[k])) {
+        if (p.ablate & 2u) {
+          v[k].x = key[k];
+          v[k].y = -1;
+        } else {
+          v[k] = *reinterpret_cast<const longlong2 *>(p.table + s0);
+        }
+      }
+    }
+    uint32_t hits[R];
+    uint32_t n_hits = 0, done = 0;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const bool act = (need >> k) & 1u;
+      const uint32_t blk = cur[k] & ~(WS - 1);
+      const uint32_t off = cur[k] - blk;
+      const uint32_t p0 = 2 * h, p1 = 2 * h + 1;
+      uint32_t f;  // first window position ending the run (WS: none)
+      if (KIND == CCJ_TABLE_LP) {
+        uint32_t fl = WS;
+        if (act && p1 >= off && v[k].y == -1) fl = p1;
+        if (act && p0 >= off && v[k].x == -1) fl = p0;
+        const uint32_t fo = (uint32_t)__shfl_xor((int)fl, 1);
+        f = fl < fo ? fl : fo;
+      } else {
+        const uint32_t d = lim[k] - blk;
+        f = d < WS ? d : WS;
+      }
+      hits[k] = 0;
+      if (act) {
+        if (p0 >= off && p0 < f && v[k].x == key[k]) hits[k] |= 1u;
+        if (p1 >= off && p1 < f && v[k].y == key[k]) hits[k] |= 2u;
+        n_hits += (uint32_t)__builtin_popcount(hits[k]);
+        if (f < WS) {
+          const uint32_t r = r0[k] + f - off;
+          lane_rounds = r > lane_rounds ? r : lane_rounds;
+          done |= 1u << k;
+        } else {
+          r0[k] += WS - off;
+          cur[k] = KIND == CCJ_TABLE_LP ? ((blk + WS) & p.mask) : blk + WS;
+          if (KIND == CCJ_TABLE_CHAIN && cur[k] == lim[k]) {
+            lane_rounds = r0[k] > lane_rounds ? r0[k] : lane_rounds;
+            done |= 1u << k;
+          }
+        }
+      }
+    }
+    uint32_t incl = n_hits;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
+      if (lane >= (uint32_t)d) incl += o;
+    }
+    const uint32_t wave_total = (uint32_t)__shfl((int)incl, kWave - 1);
+    uint32_t wbase = 0;
+    if (wave_total) {
+      if (lane == 0) wbase = atomicAdd(&s_cnt, wave_total);
+      wbase = (uint32_t)__shfl((int)wbase, 0);
+    }
+    if (n_hits && !(p.ablate & 1u)) {
+      uint32_t o = wbase + incl - n_hits;
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        for (uint32_t hm = hits[k]; hm; hm &= hm - 1u, ++o) {
+          if (o < kFlatStage) {
+            s_sel[o] = row[k];  // payload = s_key[row]: the matched table value == probe key
+          } else if (o < p.cap) {
+            p.out_sel[obase + o] = row[k];
+            if (p.out_payload) p.out_payload[obase + o] = key[k];
+          } else {
+            overflow = 1;
+          }
+        }
+      }
+    }
+    if (done) {
+#pragma unroll
+      for (int k = 0; k < R; ++k)
+        if ((done >> k) & 1u) {
+          need &= ~(1u << k);
+          start(k, row[k] + kStride);
+        }
+    }
+  }
+  {
+    const uint32_t wr = wave_max(lane_rounds);
+    if (lane == 0) atomicMax(&s_rounds, wr);
+  }
+  __syncthreads();
+  const uint32_t total = s_cnt;
+  const uint32_t staged = total < kFlatStage ? total : kFlatStage;
+  if (!(p.ablate & 1u)) {
+    for (uint32_t o = tid; o < staged && o < p.cap; o += kFlatThreads) {
+      __builtin_nontemporal_store(s_sel[o], p.out_sel + obase + o);
+      if (p.out_payload) __builtin_nontemporal_store(s_key[s_sel[o]], p.out_payload + obase + o);
+    }
+  }
+  if (tid == 0) {
+    p.out_count[c] = total < p.cap ? total : (uint32_t)p.cap;
+    if (p.out_rounds) p.out_rounds[c] = s_rounds;
+  }
+  if (p.status && (overflow || total > p.cap)) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
+}
+
 hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
   if (p.n_chunks == 0) return hipSuccess;
   const dim3 g((unsigned)p.n_chunks), b(kFlatThreads);
   // 16-byte windows: probe_flat<.., 4> (two loads per step) measured 14.3 ms vs 13.2 ms at C2, and a
   // 4-lane cooperative 64-byte-window walk 23 ms (VALU-bound: 4 lanes per row).
+  static const int pair = [] {
+    const char *e = getenv("CCJ_FLAT_PAIR");  // 0: one lane per row (probe_flat)
+    return e ? atoi(e) : 4;
+  }();
+  const uint64_t size = (uint64_t)p.mask + 1;
+  if (pair && (kind != CCJ_TABLE_LP || size >= 4)) {
+    if (kind == CCJ_TABLE_LP) {
+      if (pair == 2) hipLaunchKernelGGL((probe_pair<CCJ_TABLE_LP, 2>), g, b, 0, s, p);
+      else if (pair == 3) hipLaunchKernelGGL((probe_pair<CCJ_TABLE_LP, 3>), g, b, 0, s, p);
+      else if (pair == 6) hipLaunchKernelGGL((probe_pair<CCJ_TABLE_LP, 6>), g, b, 0, s, p);
+      else if (pair == 8) hipLaunchKernelGGL((probe_pair<CCJ_TABLE_LP, 8>), g, b, 0, s, p);
+      else hipLaunchKernelGGL((probe_pair<CCJ_TABLE_LP, 4>), g, b, 0, s, p);
+    } else {
+      hipLaunchKernelGGL((probe_pair<CCJ_TABLE_CHAIN, 4>), g, b, 0, s, p);
+    }
+    return hipGetLastError();
+  }
   if (kind == CCJ_TABLE_LP) hipLaunchKernelGGL((probe_flat<CCJ_TABLE_LP, 2>), g, b, 0, s, p);
   else hipLaunchKernelGGL((probe_flat<CCJ_TABLE_CHAIN, 2>), g, b, 0, s, p);
   return hipGetLastError();
