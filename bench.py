@@ -61,7 +61,11 @@ def parse():
     ap.add_argument("--pipe-joins", type=int, default=3)
     ap.add_argument("--pipe-block", type=int, default=256)
     ap.add_argument("--pipe-table", default="chain", choices=["chain", "lp"])
-    ap.add_argument("--n-build", type=int, default=1 << 26)
+    ap.add_argument("--n-build", type=int, default=1 << 26, help="N = 1: build keys (C2)")
+    ap.add_argument("--n-build-per-gpu", type=int, default=1 << 27,
+                    help="N > 1: build keys per GPU (C4: 2^30 total at 8 GPUs)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="N > 1: weak = --n-probe keys per GPU (C4), strong = --n-probe keys in total")
     ap.add_argument("--n-probe", type=int, default=1 << 30, help="probe keys per GPU")
     ap.add_argument("--chunk", type=int, default=2048)
     ap.add_argument("--layout", default="device", choices=["device", "reference"])
@@ -514,13 +518,14 @@ def main():
 
 
 def bench_multi(args, world, rank, local, dev, stream, dist):
-    """C4 shape, weak scaling: each rank owns 1/N of a build side of n_build * N reference keys
-    (owner = top log2(N) hash bits) and probes 2^30 keys of its own; a step = batched owner
-    partition + RCCL all-to-all of (key, u32 row) + local probe, pipelined on two streams
-    (ccj_dist.ShardedProbe)."""
+    """C4 (BASELINE configs[3]): each rank owns 1/N of a build side of 2^27 * N reference keys
+    (owner = top log2(N) hash bits; 2^30 in total at N = 8) and probes 2^30 keys of its own (weak
+    scaling; --scaling strong: 2^30 / N each); a step = batched owner partition + RCCL
+    all-to-all of (key, u32 row) + local probe, pipelined on three streams (ccj_dist.ShardedProbe)."""
     import ccj_dist
-    n_build_total = args.n_build * world
-    n_probe, chunk = args.n_probe, args.chunk
+    n_build_total = args.n_build_per_gpu * world
+    n_probe = args.n_probe if args.scaling == "weak" else args.n_probe // world
+    chunk = args.chunk
     t0 = time.perf_counter()
     with torch.cuda.stream(stream):
         sp = ccj_dist.ShardedProbe(n_build_total, 1, n_probe, chunk, world, rank, stream=stream,
@@ -568,9 +573,9 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
         line = {
             "metric": METRIC, "value": value, "unit": "probe tuples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall * 1e3 / args.steps,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "int64",
             "data": "synthetic (reference key generator build side; SplitMix64 uniform probe keys, seed 42)",
-            "config": {"workload": f"C4 shape: {world}xMI355X radix-partitioned LP join, {n_build_total} build / "
+            "config": {"workload": f"C4: {world}xMI355X radix-partitioned LP join, {n_build_total} build / "
                                    f"{world * n_probe} probe int64, chunk=2048, RCCL all-to-all tuple shuffle",
                        "table": "linear_probing", "n_build_total": n_build_total, "n_probe_per_gpu": n_probe,
                        "chunk": chunk, "batches": sp.batches, "parallelism": f"dp{world} (owner-partitioned)"},
