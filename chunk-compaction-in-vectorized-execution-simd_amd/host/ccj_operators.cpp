@@ -1,4 +1,6 @@
 // ccj_operators.cpp — reference operator surface over the ccj C ABI (see ccj_operators.h).
+#include <cstring>
+
 #include "ccj_operators.h"
 
 #include <hip/hip_runtime.h>
@@ -72,76 +74,76 @@ class DeviceTable {
     (void)hipStreamDestroy(stream_);
   }
 
-  // Probe + every Next round of one chunk: the whole ScanStructure lifetime in one launch.
+  // Probe + every Next round of one chunk: the whole ScanStructure lifetime in one launch.  One
+  // pinned staging buffer mirrors one device buffer: [keys | sel | count | out header (zeroed) |
+  // round counts | out sel | payload]; one upload of the input + header, one launch, one download
+  // of the outputs, one synchronisation.
   ChunkProbeResult Run(Vector &join_key, size_t count, const vector<uint32_t> &sel) {
     Ensure();
     const size_t n = kBlockSize;
     if (count > n || sel.size() < count) throw EngineError("Probe: count exceeds kBlockSize / sel");
-    const uint32_t cnt = (uint32_t)count;
-    hip_check(hipMemcpyAsync(d_keys_, join_key.Data(), n * sizeof(int64_t), hipMemcpyHostToDevice, stream_), "H2D");
-    if (count) hip_check(hipMemcpyAsync(d_sel_, sel.data(), count * 4, hipMemcpyHostToDevice, stream_), "H2D");
-    hip_check(hipMemcpyAsync(d_counts_, &cnt, 4, hipMemcpyHostToDevice, stream_), "H2D");
-    hip_check(hipMemsetAsync(d_status_, 0, 4, stream_), "memset");
+    char *h = h_buf_;
+    std::memcpy(h + off_keys_, join_key.Data(), n * sizeof(int64_t));
+    if (count) std::memcpy(h + off_sel_, sel.data(), count * 4);
+    *reinterpret_cast<uint32_t *>(h + off_cnt_) = (uint32_t)count;
+    std::memset(h + off_hdr_, 0, 16);  // out count, rounds, status
+    hip_check(hipMemcpyAsync(d_buf_, h, off_hdr_ + 16, hipMemcpyHostToDevice, stream_), "H2D");
+    char *d = d_buf_;
     ccj_probe_args a{};
-    a.keys = d_keys_;
-    a.sel = d_sel_;
-    a.counts = d_counts_;
+    a.keys = reinterpret_cast<const int64_t *>(d + off_keys_);
+    a.sel = reinterpret_cast<const uint32_t *>(d + off_sel_);
+    a.counts = reinterpret_cast<const uint32_t *>(d + off_cnt_);
     a.n_rows = n;
     a.chunk = (uint32_t)n;
     a.max_rounds = max_rounds_;
     a.cap = cap_;
-    a.out_count = d_count_;
-    a.out_sel = d_osel_;
-    a.out_payload = d_pay_;
-    a.out_rounds = d_rounds_;
-    a.out_round_counts = d_rc_;
-    a.status = d_status_;
+    a.out_count = reinterpret_cast<uint32_t *>(d + off_hdr_);
+    a.out_rounds = reinterpret_cast<uint32_t *>(d + off_hdr_ + 4);
+    a.status = reinterpret_cast<uint32_t *>(d + off_hdr_ + 8);
+    a.out_round_counts = reinterpret_cast<uint32_t *>(d + off_rc_);
+    a.out_sel = reinterpret_cast<uint32_t *>(d + off_osel_);
+    a.out_payload = reinterpret_cast<int64_t *>(d + off_pay_);
     check(ccj_probe(t_, &a, stream_), "ccj_probe");
-    uint32_t hdr[3];
-    hip_check(hipMemcpyAsync(&hdr[0], d_count_, 4, hipMemcpyDeviceToHost, stream_), "D2H");
-    hip_check(hipMemcpyAsync(&hdr[1], d_rounds_, 4, hipMemcpyDeviceToHost, stream_), "D2H");
-    hip_check(hipMemcpyAsync(&hdr[2], d_status_, 4, hipMemcpyDeviceToHost, stream_), "D2H");
+    hip_check(hipMemcpyAsync(h + off_hdr_, d + off_hdr_, end_ - off_hdr_, hipMemcpyDeviceToHost, stream_), "D2H");
     hip_check(hipStreamSynchronize(stream_), "sync");
+    const uint32_t *hdr = reinterpret_cast<const uint32_t *>(h + off_hdr_);
     if (hdr[2]) throw EngineError("ccj_probe raised status flags " + std::to_string(hdr[2]));
     ChunkProbeResult r;
-    r.round_counts.resize(hdr[1]);
-    r.sel.resize(hdr[0]);
-    r.payload.resize(hdr[0]);
-    if (hdr[1]) hip_check(hipMemcpyAsync(r.round_counts.data(), d_rc_, hdr[1] * 4, hipMemcpyDeviceToHost, stream_), "D2H");
-    if (hdr[0]) {
-      hip_check(hipMemcpyAsync(r.sel.data(), d_osel_, hdr[0] * 4, hipMemcpyDeviceToHost, stream_), "D2H");
-      hip_check(hipMemcpyAsync(r.payload.data(), d_pay_, hdr[0] * 8, hipMemcpyDeviceToHost, stream_), "D2H");
-    }
-    hip_check(hipStreamSynchronize(stream_), "sync");
+    const uint32_t nm = hdr[0], nr = hdr[1] < max_rounds_ ? hdr[1] : max_rounds_;
+    const uint32_t *rc = reinterpret_cast<const uint32_t *>(h + off_rc_);
+    const uint32_t *os = reinterpret_cast<const uint32_t *>(h + off_osel_);
+    const int64_t *op = reinterpret_cast<const int64_t *>(h + off_pay_);
+    r.round_counts.assign(rc, rc + nr);
+    r.sel.assign(os, os + nm);
+    r.payload.assign(op, op + nm);
     return r;
   }
   const ccj_table *handle() const { return t_; }
 
  private:
+  static size_t Align(size_t x) { return (x + 15) & ~(size_t)15; }
   void Ensure() {
     if (sized_for_ == kBlockSize) return;
     Release();
     const size_t n = kBlockSize;
     cap_ = n * std::max<uint64_t>(1, info_.max_dup);
     max_rounds_ = info_.max_rounds + 1;
-    hip_check(hipMalloc(&d_keys_, n * 8), "hipMalloc");
-    hip_check(hipMalloc(&d_sel_, n * 4), "hipMalloc");
-    hip_check(hipMalloc(&d_counts_, 4), "hipMalloc");
-    hip_check(hipMalloc(&d_count_, 4), "hipMalloc");
-    hip_check(hipMalloc(&d_rounds_, 4), "hipMalloc");
-    hip_check(hipMalloc(&d_status_, 4), "hipMalloc");
-    hip_check(hipMalloc(&d_osel_, cap_ * 4), "hipMalloc");
-    hip_check(hipMalloc(&d_pay_, cap_ * 8), "hipMalloc");
-    hip_check(hipMalloc(&d_rc_, max_rounds_ * 4), "hipMalloc");
+    off_keys_ = 0;
+    off_sel_ = Align(n * 8);
+    off_cnt_ = Align(off_sel_ + n * 4);
+    off_hdr_ = Align(off_cnt_ + 4);
+    off_rc_ = off_hdr_ + 16;
+    off_osel_ = Align(off_rc_ + (size_t)max_rounds_ * 4);
+    off_pay_ = Align(off_osel_ + cap_ * 4);
+    end_ = off_pay_ + cap_ * 8;
+    hip_check(hipMalloc(&d_buf_, end_), "hipMalloc");
+    hip_check(hipHostMalloc(&h_buf_, end_, hipHostMallocDefault), "hipHostMalloc");
     sized_for_ = n;
   }
   void Release() {
-    for (void *p : {(void *)d_keys_, (void *)d_sel_, (void *)d_counts_, (void *)d_count_, (void *)d_rounds_,
-                    (void *)d_status_, (void *)d_osel_, (void *)d_pay_, (void *)d_rc_})
-      if (p) (void)hipFree(p);
-    d_keys_ = nullptr;
-    d_sel_ = d_counts_ = d_count_ = d_rounds_ = d_status_ = d_osel_ = d_rc_ = nullptr;
-    d_pay_ = nullptr;
+    if (d_buf_) (void)hipFree(d_buf_);
+    if (h_buf_) (void)hipHostFree(h_buf_);
+    d_buf_ = h_buf_ = nullptr;
     sized_for_ = 0;
   }
 
@@ -151,9 +153,8 @@ class DeviceTable {
   size_t sized_for_ = 0;
   uint64_t cap_ = 0;
   uint32_t max_rounds_ = 0;
-  int64_t *d_keys_ = nullptr, *d_pay_ = nullptr;
-  uint32_t *d_sel_ = nullptr, *d_counts_ = nullptr, *d_count_ = nullptr, *d_rounds_ = nullptr, *d_status_ = nullptr,
-           *d_osel_ = nullptr, *d_rc_ = nullptr;
+  size_t off_keys_ = 0, off_sel_ = 0, off_cnt_ = 0, off_hdr_ = 0, off_rc_ = 0, off_osel_ = 0, off_pay_ = 0, end_ = 0;
+  char *d_buf_ = nullptr, *h_buf_ = nullptr;
 };
 
 // Fills `result` with one Next result: Slice (base.cpp:37-47) + payload column m+1 at the selected
