@@ -15,6 +15,8 @@
 // per probe chunk copies its rows (DataChunk::Append's gather, base.cpp:15-27) -> chunk counts.
 #include <hipcub/hipcub.hpp>
 
+#include <cstdlib>
+
 #include "ccj_internal.h"
 
 namespace ccj {
@@ -128,6 +130,97 @@ __global__ __launch_bounds__(256) void copy_rows(CompactParams p) {
   }
 }
 
+// Flat form of copy_rows for chunks with at most 64 Next results: lane r holds round r's count,
+// its P-stream start, its pass-through index and its source offset (wave prefix sums); every lane
+// then copies matches m = lane, lane + 64, ... of the chunk, finding m's round by a binary search
+// over the lanes.  All 64 lanes stay busy however the matches spread over rounds.
+__global__ __launch_bounds__(256) void copy_rows_flat(CompactParams p) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t c = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= p.a.n_chunks) return;
+  const uint64_t B = p.a.chunk;
+  const uint64_t F = p.totals[1] < p.max_full ? p.totals[1] : p.max_full;
+  const uint64_t cap_rows = p.a.out_cap_rows;
+  const uint32_t rounds = p.a.rounds[c] < p.a.max_rounds ? p.a.rounds[c] : p.a.max_rounds;
+  const uint32_t total = p.a.count[c];
+  if (rounds > 64) {  // rare: the per-round loop of copy_rows handles it
+    uint64_t t = p.nonfull[c], f = p.full[c], src = c * p.a.cap;
+    for (uint32_t r = 0; r < rounds; ++r) {
+      const uint32_t rc = p.a.round_counts[c * p.a.max_rounds + r];
+      const bool is_full = p.bypass(rc);
+      const uint64_t fbase = (e_of(t, B) + f) * B;
+      for (uint32_t j = lane; j < rc; j += 64) {
+        if (src + j >= c * p.a.cap + total) break;
+        uint64_t dest;
+        if (is_full) {
+          dest = fbase + j;
+        } else {
+          const uint64_t u = t + j, k = u / B;
+          dest = (k + (F ? full_before(p, F, k) : 0)) * B + (u - k * B);
+        }
+        if (dest >= cap_rows) continue;
+        const uint64_t row = c * B + p.a.sel[src + j];
+        for (uint32_t q = 0; q < p.a.n_cols; ++q) p.a.out_cols[q][dest] = p.a.cols[q][row];
+        if (p.a.out_payload) p.a.out_payload[dest] = p.a.payload[src + j];
+        if (p.a.out_row) p.a.out_row[dest] = row;
+      }
+      src += rc;
+      if (is_full) ++f;
+      else t += rc;
+    }
+    return;
+  }
+  const uint32_t rc = lane < rounds ? p.a.round_counts[c * p.a.max_rounds + lane] : 0u;
+  const bool byp = lane < rounds && p.bypass(rc);
+  // exclusive prefixes over rounds: source offset, P-stream rows, pass-through results
+  uint32_t src = rc, ps = byp ? 0u : rc, fs = byp ? 1u : 0u;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t a = (uint32_t)__shfl_up((int)src, d), b = (uint32_t)__shfl_up((int)ps, d),
+                   e = (uint32_t)__shfl_up((int)fs, d);
+    if (lane >= (uint32_t)d) {
+      src += a;
+      ps += b;
+      fs += e;
+    }
+  }
+  src -= rc;
+  ps -= byp ? 0u : rc;
+  fs -= byp ? 1u : 0u;
+  const uint64_t t_r = p.nonfull[c] + ps, f_r = p.full[c] + fs;
+  const uint64_t fbase = (e_of(t_r, B) + f_r) * B;  // lane r's pass-through destination
+  const uint64_t obase = c * p.a.cap;
+  // Every lane runs every iteration (cross-lane reads need the source lanes active).
+  for (uint32_t m0 = 0; m0 < total; m0 += 64) {
+    const uint32_t m = m0 + lane;
+    // round of match m: the last r < rounds with src_r <= m (src is non-decreasing, src_0 = 0)
+    uint32_t r = 0;
+#pragma unroll
+    for (uint32_t step = 32; step >= 1; step >>= 1) {
+      const uint32_t cand = r + step;
+      const uint32_t v = (uint32_t)__shfl((int)src, (int)(cand < rounds ? cand : 0u));
+      if (cand < rounds && v <= m) r = cand;
+    }
+    const uint32_t j = m - (uint32_t)__shfl((int)src, (int)r);
+    const bool rb = __shfl((int)byp, (int)r) != 0;
+    const uint64_t fb = (uint64_t)__shfl((long long)fbase, (int)r);
+    const uint64_t tr = (uint64_t)__shfl((long long)t_r, (int)r);
+    if (m >= total) continue;
+    uint64_t dest;
+    if (rb) {
+      dest = fb + j;
+    } else {
+      const uint64_t u = tr + j, k = u / B;
+      dest = (k + (F ? full_before(p, F, k) : 0)) * B + (u - k * B);
+    }
+    if (dest >= cap_rows) continue;
+    const uint64_t row = c * B + p.a.sel[obase + m];
+    for (uint32_t q = 0; q < p.a.n_cols; ++q) p.a.out_cols[q][dest] = p.a.cols[q][row];
+    if (p.a.out_payload) p.a.out_payload[dest] = p.a.payload[obase + m];
+    if (p.a.out_row) p.a.out_row[dest] = row;
+  }
+}
+
 __global__ void chunk_counts(CompactParams p) {
   // P-chunks (compacted): all full except the last; pass-through chunks were counted by full_list.
   const uint64_t T = p.totals[0], B = p.a.chunk;
@@ -196,7 +289,9 @@ hipError_t launch_compact(const ccj_compact_args &a, hipStream_t s) {
   if (e) return e;
   hipLaunchKernelGGL(seg_totals, dim3(1), dim3(1), 0, s, p, nf_raw + a.n_chunks - 1, f_raw + a.n_chunks - 1);
   hipLaunchKernelGGL(full_list, dim3(g), dim3(256), 0, s, p);
-  hipLaunchKernelGGL(copy_rows, dim3((unsigned)((a.n_chunks + 3) / 4)), dim3(256), 0, s, p);
+  static const bool flat = getenv("CCJ_COMPACT_ROUNDWISE") == nullptr;
+  if (flat) hipLaunchKernelGGL(copy_rows_flat, dim3((unsigned)((a.n_chunks + 3) / 4)), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(copy_rows, dim3((unsigned)((a.n_chunks + 3) / 4)), dim3(256), 0, s, p);
   hipLaunchKernelGGL(chunk_counts, dim3(1024), dim3(256), 0, s, p);
   return hipGetLastError();
 }
