@@ -385,12 +385,15 @@ extern "C" int ccj_pipeline_run(ccj_pipeline *pl, const int64_t *const *d_cols, 
       a.workspace_bytes = L.compact_ws.bytes;
       a.status = (uint32_t *)(tot + 3);
       if (T) PL_TRY(ccj::launch_compact(a, s), "pipeline compact");
-      // pass-through chunks add output chunks beyond ceil(T / B); read the true number
-      PL_TRY(hipMemcpyAsync(h, tot, sizeof(h), hipMemcpyDeviceToHost, s), "copy sizes");
-      PL_TRY(hipStreamSynchronize(s), "sync");
-      if (h[3]) return ccj::api_fail(CCJ_ERR_LIMIT, "ccj_pipeline_run: compaction status flags " + std::to_string(h[3]));
-      in_chunks = T ? h[2] : 0;
       gaps = thr != 0 && thr < B;
+      if (gaps) {  // pass-through chunks add output chunks beyond ceil(T / B): read the number
+        PL_TRY(hipMemcpyAsync(h, tot, sizeof(h), hipMemcpyDeviceToHost, s), "copy sizes");
+        PL_TRY(hipStreamSynchronize(s), "sync");
+        if (h[3]) return ccj::api_fail(CCJ_ERR_LIMIT, "ccj_pipeline_run: compaction status flags " + std::to_string(h[3]));
+        in_chunks = T ? h[2] : 0;
+      } else {  // NaiveCompactor: every output chunk is full but the last (status checked later)
+        in_chunks = out_chunks;
+      }
       last_out_chunks = in_chunks;
       in_counts = L.next_counts.as<uint32_t>();
       in_base = in_obase = nullptr;
