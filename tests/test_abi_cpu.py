@@ -51,3 +51,36 @@ def test_built_for_gfx950():
     if out.returncode != 0:
         pytest.skip("roc-obj-ls unavailable")
     assert "gfx950" in out.stdout
+
+
+def test_new_entry_points_fail_loudly_without_device():
+    """Pipeline, tuner-facing and multi-GPU entry points refuse to run without a GPU and report
+    bad arguments before touching the device (no CPU fallback anywhere)."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("GPU present")
+    except ImportError:
+        pass
+    L = ccj.lib()
+    h = C.c_void_p()
+    # no tables -> invalid argument, checked before the device
+    assert L.ccj_pipeline_create(None, 3, 256, 1, C.byref(h)) == -1 and not h.value
+    arr = (C.c_void_p * 1)(None)
+    assert L.ccj_pipeline_create(arr, 1, 256, 1, C.byref(h)) == -1  # null table
+    assert L.ccj_pipeline_set_thresholds(None, None) == -1
+    assert L.ccj_pipeline_free(None) == 0
+    assert L.ccj_pipeline_checksum(None, 1, None, None) == -1
+    # fixed-capacity partition: argument checks
+    assert L.ccj_partition_by_owner_fixed(None, 10, 3, 0, 16, None, None, None, None, None, 0, None) == -1
+    assert L.ccj_segment_chunk_counts(None, 1, 100, 64, None, None, None) == -1  # seg_cap % chunk
+    assert L.ccj_gen_c3_keys(None, 10, 1, 0, 100, 1, 100000, None) == -1
+    assert L.ccj_gen_c3_keys(None, 0, 1, 0, 100, 1, 2000000, None) == -1  # hit_ppm > 1e6
+    assert b"" != L.ccj_last_error()
+
+
+def test_compact_workspace_grows_with_pass_through():
+    L = ccj.lib()
+    naive = L.ccj_compact_workspace_size(1000, 2048, 2048, 33, 0)
+    gated = L.ccj_compact_workspace_size(1000, 2048, 2048, 33, 1)
+    assert gated > naive > 0
