@@ -1,4 +1,4 @@
-// ccj_partition.hip — stable multisplits of a key column by a digit of its murmurhash64 value.
+// ccj_partition.hip — multisplits of a key column by a digit of its murmurhash64 value.
 //
 //  - owner partitioning for the multi-GPU join: digit = h >> (64 - log2 P), the TOP
 //    hash bits, disjoint from the low bits every GPU's local table uses, so shards stay balanced;
@@ -7,10 +7,12 @@
 //
 // Each pass is a multisplit in two kernels: (1) per-tile digit counts, written digit-major;
 // (2) after an exclusive scan of those counts, every tile re-reads its keys, builds an LDS image
-// of itself grouped by digit, and writes each digit segment whole.  The owner split ranks keys
-// stably (ballot + mbcnt), so the send buffers are deterministic; the slot split ranks them with
-// LDS atomics (grouping exact, order inside a tile's segment not), which is all the probe needs:
-// the second LSD pass still leaves every partition contiguous and its table window shared.
+// of itself grouped by digit, and writes each digit segment whole; tiles are dealt to XCDs in
+// contiguous ranges so the lines where neighbouring tiles' segments meet are completed in one L2.
+// The exact-size owner split (build-side sharding, exchange fallback) ranks keys stably (ballot +
+// mbcnt), so its output is deterministic; the fixed-capacity owner split and the slot split rank
+// them with LDS atomics (grouping exact, order inside a tile's segment not), which is all the
+// probe needs — the second LSD pass still leaves every slot partition contiguous.
 #include <hipcub/hipcub.hpp>
 
 #include "ccj_internal.h"
@@ -175,7 +177,8 @@ size_t pass_workspace(uint64_t n, uint32_t parts) {
   return 2 * ((m * 8 + 255) & ~255ull) + scan_bytes(m ? m : 1);
 }
 
-// One stable multisplit pass.  out_counts (digit totals) may be NULL.
+// One multisplit pass (STABLE: ballot ranking; else LDS atomics).  out_counts (digit totals) may be
+// NULL; stride > 0 gives destination d the fixed segment [d*stride, (d+1)*stride).
 template <typename RowT, bool STABLE>
 hipError_t split_pass(const int64_t *keys, const RowT *in_rows, uint64_t n, uint32_t parts, Digit dg,
                       uint64_t row_base, int64_t *out_keys, RowT *out_rows, uint64_t *out_counts, void *ws,
