@@ -131,7 +131,7 @@ def parse(out):
     return res, head
 
 
-@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("name", sorted(k for k in KA if "naive_compact" not in k))  # incl. C1's 16M cases
 def test_batched_engine_matches_reference(name):
     want = KA[name]
     p = run_bin(want["spec"], "batched")
