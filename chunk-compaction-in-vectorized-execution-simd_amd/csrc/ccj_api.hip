@@ -215,6 +215,22 @@ int build_chain_host(const int64_t *keys, uint64_t n, ccj_table **out) {
     return rc;
   }
   t->d_row = (uint32_t *)d;
+  {  // bucket records: the chain's range and first key in one 16-byte load
+    std::vector<int64_t> rec(2 * size);
+    for (uint64_t b = 0; b < size; ++b) {
+      const uint64_t lo = off[b], len = off[b + 1] - off[b];
+      rec[2 * b] = (int64_t)(lo | (len << 32));
+      rec[2 * b + 1] = len ? chain[lo] : -1;
+    }
+    rc = upload(&d, rec.data(), rec.size() * sizeof(int64_t), "chain bucket records");
+    if (rc) {
+      (void)hipFree(t->d_table);
+      (void)hipFree(t->d_off);
+      (void)hipFree(t->d_row);
+      return rc;
+    }
+    t->d_bucket = (int64_t *)d;
+  }
   t->info.d_table = t->d_table;
   t->info.d_bucket_off = t->d_off;
   (void)hipGetDevice(&t->device);
@@ -390,6 +406,7 @@ int ccj_table_free(ccj_table *t) {
   if (!t) return CCJ_OK;
   if (t->d_table) (void)hipFree(t->d_table);
   if (t->d_off) (void)hipFree(t->d_off);
+  if (t->d_bucket) (void)hipFree(t->d_bucket);
   if (t->d_row) (void)hipFree(t->d_row);
   if (t->d_pay) (void)hipFree(t->d_pay);
   delete t;
@@ -406,6 +423,7 @@ int fill_probe_params(const ccj_table *t, const ccj_probe_args *a, ccj::ProbePar
   p = ccj::ProbeParams{};
   p.table = t->d_table;
   p.off = t->d_off;
+  p.bucket = reinterpret_cast<const longlong2 *>(t->d_bucket);
   p.mask = (uint32_t)(t->info.size - 1);
   p.keys = a->keys;
   p.sel = a->sel;

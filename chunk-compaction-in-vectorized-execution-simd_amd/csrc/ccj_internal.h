@@ -12,6 +12,7 @@ struct ccj_table {
   ccj_table_info info;
   int64_t *d_table = nullptr;   // LP slots / chain keys
   uint32_t *d_off = nullptr;    // chain CSR offsets (size + 1)
+  int64_t *d_bucket = nullptr;  // chain: per bucket {start | len << 32, first chain key} (16 B)
   uint32_t *d_row = nullptr;    // table position -> build tuple index (LP: kNoRow for empty slots)
   uint64_t positions = 0;       // allocated positions (LP slots / chain keys, padded)
   int64_t *d_pay = nullptr;     // position-major payload rows [positions][n_pay]
@@ -39,6 +40,9 @@ constexpr uint32_t kMaxParts = 64;  // owner partitions (GPUs) per multisplit
 struct ProbeParams {
   const int64_t *table;
   const uint32_t *off;
+  // chain only, optional: bucket records {start | len << 32, first key} — one 16-byte load gives
+  // the chain's range and its round-0 candidate (most chains at load 1/2 have one key)
+  const longlong2 *bucket;
   uint32_t mask;  // size - 1 (size <= 2^32)
   const int64_t *keys;
   const uint32_t *sel;

@@ -184,8 +184,15 @@ __device__ __forceinline__ bool walk_rows(const ProbeParams &p, const int64_t *s
     for (int g = 0; g < G; ++g) {
       if ((live >> g) & 1u) {
         if (KIND == CCJ_TABLE_CHAIN && ((start >> g) & 1u)) {
-          o0[g] = p.off[cur[g]];  // chaining_ht.cpp:46-49: bucket -> chain (CSR range)
-          o1[g] = p.off[cur[g] + 1];
+          if (p.bucket) {  // {start | len << 32, first key}: range + round-0 candidate, one load
+            const longlong2 rec = p.bucket[cur[g]];
+            o0[g] = (uint32_t)rec.x;
+            o1[g] = (uint32_t)rec.x + (uint32_t)((uint64_t)rec.x >> 32);
+            v[g][0].x = rec.y;
+          } else {
+            o0[g] = p.off[cur[g]];  // chaining_ht.cpp:46-49: bucket -> chain (CSR range)
+            o1[g] = p.off[cur[g] + 1];
+          }
         } else {
           const longlong2 *w = reinterpret_cast<const longlong2 *>(p.table + (cur[g] & ~(uint32_t)(kWin - 1)));
 #pragma unroll
@@ -203,6 +210,15 @@ __device__ __forceinline__ bool walk_rows(const ProbeParams &p, const int64_t *s
           cur[g] = o0[g];
           lim[g] = o1[g];
           done = cur[g] == lim[g];  // empty bucket: not in the active set (chaining_ht.cpp:52-55)
+          if (!done && p.bucket) {  // round 0 from the record's first key
+            if (v[g][0].x == kj[g]) mm[g] |= 1u;
+            r0[g] = 1;
+            cur[g] = o0[g] + 1;
+            if (cur[g] == lim[g]) {  // a one-key chain: one round
+              on_end(row, 1u);
+              done = true;
+            }
+          }
         } else {
           const uint32_t blk = cur[g] & ~(uint32_t)(kWin - 1);
           const uint32_t off = cur[g] - blk;
