@@ -388,14 +388,17 @@ def main():
             del bk, pay
         keys = ccj.gen_uniform_keys(n_probe, SEED, n_build, first_row=rank * n_probe, stream=stream)
         out = table.alloc_outputs(n_probe, chunk, rounds=True, payload_cols=P)
-        part = table.alloc_partitioned(n_probe) if args.path == "partitioned" else None
+        part = out_p = None
+        if args.path == "partitioned" or not c5:  # the headline path, or the one timed beside it
+            part = table.alloc_partitioned(n_probe, chunk)
+            out_p = table.alloc_outputs(part["positions"], chunk, rounds=False)
     stream.synchronize()
     log(f"[setup] table {table.size} slots, max_rounds {table.max_rounds}, keys {n_probe}: "
         f"{time.perf_counter() - t0:.1f} s")
 
     def step(path=args.path):
-        if path == "partitioned":
-            table.probe_partitioned(keys, chunk, out=out, part=part, stream=stream)
+        if path == "partitioned":  # no host check inside the timed region: status is read after it
+            table.probe_partitioned(keys, chunk, out=out_p, part=part, stream=stream, retry=False)
         else:
             table.probe(keys, chunk, out=out, stream=stream)
 
@@ -426,19 +429,21 @@ def main():
     value = total_tuples / (wall / args.steps)
 
     # ---- verification + work accounting (untimed) ----
-    status = int(out["status"].item())
     if args.path == "partitioned":
-        rm = part["row_map"][:n_probe].to(torch.int64) + rank * n_probe
-        matches, l2 = ccj.result_checksum(out, chunk, row_map=rm, stream=stream)
+        status = int(out_p["status"].item())
+        if status & ccj.FLAG_PART_OVERFLOW:
+            raise SystemExit("bench: fixed-capacity partition overflowed on uniform keys")
+        out_p["n_chunks"] = (part["positions"] + chunk - 1) // chunk
+        rm = part["row_map"].to(torch.int64) + rank * n_probe
+        matches, l2 = ccj.result_checksum(out_p, chunk, row_map=rm, stream=stream)
         del rm
     else:
+        status = int(out["status"].item())
         matches, l2 = ccj.result_checksum(out, chunk, row_base=rank * n_probe, stream=stream)
     # the other path, timed the same way (reported beside the headline)
     other = "chunk" if args.path == "partitioned" else "partitioned"
-    other_ms = None
+    other_ms = other_parity = None
     if not c5:
-        if other == "partitioned":
-            part = table.alloc_partitioned(n_probe)
         step(other)
         stream.synchronize()
         ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
@@ -448,6 +453,12 @@ def main():
             b.record(stream)
         stream.synchronize()
         other_ms = sum(a.elapsed_time(b) for a, b in ev2) / len(ev2)
+        if other == "partitioned":  # its L1/L2 against the oracle answer too
+            out_p["n_chunks"] = (part["positions"] + chunk - 1) // chunk
+            rm = part["row_map"].to(torch.int64) + rank * n_probe
+            om, ol2 = ccj.result_checksum(out_p, chunk, row_map=rm, stream=stream)
+            del rm
+            other_parity = {"status_flags": int(out_p["status"].item()), "matches": om, "l2": hex(ol2)}
     examined, cost_matches = table.probe_cost(keys, stream=stream)
     parity = {"status_flags": status, "matches": matches, "l2": hex(l2)}
     if c5:  # every gathered payload column holds the matched build tuple's p_c (key == payload)
@@ -465,6 +476,8 @@ def main():
         want_m, want_l2 = O.count_uniform(SEED, rank * n_probe, (rank + 1) * n_probe, n_build, n_build, 1,
                                           threads=args.cpu_threads)
         parity.update(expected_matches=want_m, l1_ok=(want_m == matches), l2_ok=(want_l2 == l2))
+        if other_parity is not None:
+            other_parity.update(l1_ok=(want_m == other_parity["matches"]), l2_ok=(hex(want_l2) == other_parity["l2"]))
     s_bar = examined / n_probe
     m_bar = matches / n_probe
     alg_bytes_per_tuple = 8 + 8 * s_bar + m_bar * (12 + 16 * P)  # +16 B per payload column
@@ -500,7 +513,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          # measured DRAM bytes (whole 128-B lines per random slot read) per second
                          "traffic_GBps": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
-                         "kernel": ("ccj_probe_partitioned (2 slot-partition passes + probe_chunks)"
+                         "kernel": ("ccj_probe_partitioned (one-pass slot split + probe_pair)"
                                     if args.path == "partitioned" else "probe_chunks<LP,2>"),
                          "kernel_ms": kern_ms,
                          "alg_bytes_per_tuple": alg_bytes_per_tuple, "s_bar": s_bar, "m_bar": m_bar},
@@ -510,7 +523,8 @@ def main():
             "other_path": None if other_ms is None else {
                 "path": other, "ms_per_step": other_ms, "value": n_probe / (other_ms * 1e-3),
                 "frac": alg_bytes / (other_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                "parity": "L3 (reference order)" if other == "chunk" else "L1/L2"},
+                "parity": "L3 (reference order)" if other == "chunk" else "L1/L2",
+                "check": other_parity},
         }
         print(json.dumps(line), flush=True)
     if dist:

@@ -21,7 +21,8 @@ LIB_PATH = os.path.join(HERE, "libccj.so")
 
 LP, CHAIN = 0, 1
 LAYOUT_REFERENCE, LAYOUT_DEVICE = 0, 1
-FLAG_CAP_OVERFLOW, FLAG_ROUND_OVERFLOW, FLAG_BAD_INPUT = 1, 2, 4
+FLAG_CAP_OVERFLOW, FLAG_ROUND_OVERFLOW, FLAG_BAD_INPUT, FLAG_PART_OVERFLOW = 1, 2, 4, 8
+PART_EXACT = 1
 
 _lib = None
 
@@ -60,7 +61,8 @@ EXPORTS = ["ccj_last_error", "ccj_abi_version", "ccj_device_init", "ccj_table_bu
            "ccj_probe", "ccj_gen_uniform_keys", "ccj_probe_cost", "ccj_result_checksum",
            "ccj_compact_workspace_size", "ccj_compact", "ccj_partition_workspace_size", "ccj_partition_by_owner",
            "ccj_result_checksum_mapped", "ccj_gen_reference_keys", "ccj_table_set_payload",
-           "ccj_probe_partitioned_workspace_size", "ccj_probe_partitioned", "ccj_pipeline_create",
+           "ccj_probe_partitioned_workspace_size", "ccj_probe_partitioned", "ccj_probe_partitioned_positions",
+           "ccj_pipeline_create",
            "ccj_pipeline_run", "ccj_pipeline_free", "ccj_pipeline_checksum", "ccj_partition_by_owner_fixed",
            "ccj_segment_chunk_counts", "ccj_pipeline_set_thresholds", "ccj_gen_c3_keys"]
 
@@ -98,8 +100,10 @@ def lib():
         L.ccj_table_free.argtypes = [vp]
         L.ccj_table_set_payload.argtypes = [vp, vp, C.c_uint32, vp]
         L.ccj_probe_partitioned_workspace_size.restype = C.c_size_t
-        L.ccj_probe_partitioned_workspace_size.argtypes = [vp, u64]
-        L.ccj_probe_partitioned.argtypes = [vp, C.POINTER(ProbeArgs), vp, vp, C.c_size_t, vp]
+        L.ccj_probe_partitioned_workspace_size.argtypes = [vp, u64, C.c_uint32]
+        L.ccj_probe_partitioned_positions.restype = u64
+        L.ccj_probe_partitioned_positions.argtypes = [vp, u64, C.c_uint32]
+        L.ccj_probe_partitioned.argtypes = [vp, C.POINTER(ProbeArgs), C.c_uint32, vp, vp, C.c_size_t, vp]
         L.ccj_probe.argtypes = [vp, C.POINTER(ProbeArgs), vp]
         L.ccj_gen_uniform_keys.argtypes = [vp, u64, u64, u64, u64, vp]
         L.ccj_gen_reference_keys.argtypes = [vp, u64, u64, u64, u64, vp]
@@ -274,26 +278,59 @@ class Table:
         )
         return o
 
-    def alloc_partitioned(self, n_rows: int, device=None):
+    def partitioned_positions(self, n_rows: int, chunk: int) -> int:
+        """Positions of the partitioned column layout (row-map entries; outputs hold
+        positions / chunk chunks) — ccj_probe_partitioned_positions."""
+        return int(lib().ccj_probe_partitioned_positions(self._h, n_rows, chunk))
+
+    def alloc_partitioned(self, n_rows: int, chunk: int, device=None):
         """Workspace + row map for probe_partitioned."""
         import torch
         dev = device or torch.device("cuda", torch.cuda.current_device())
-        ws_bytes = lib().ccj_probe_partitioned_workspace_size(self._h, n_rows)
+        ws_bytes = lib().ccj_probe_partitioned_workspace_size(self._h, n_rows, chunk)
+        positions = self.partitioned_positions(n_rows, chunk)
         return dict(ws=torch.empty(max(ws_bytes, 8), dtype=torch.uint8, device=dev), ws_bytes=ws_bytes,
-                    row_map=torch.empty(max(n_rows, 1), dtype=torch.int32, device=dev))
+                    row_map=torch.empty(max(positions, 1), dtype=torch.int32, device=dev), positions=positions,
+                    n_rows=n_rows, chunk=chunk)
 
-    def probe_partitioned(self, keys, chunk: int, out=None, part=None, stream=None, **alloc_kw):
+    def probe_partitioned(self, keys, chunk: int, out=None, part=None, stream=None, exact: bool = False,
+                          retry: bool = True, **alloc_kw):
         """Slot-range-partitioned probe (ccj_probe_partitioned): L1/L2 results of probe(); out_sel
-        indexes the partitioned column and part["row_map"] maps it back to original rows."""
+        indexes the partitioned layout and part["row_map"] maps a live position back to its row.
+        The default one-pass split may overflow a segment under heavy key skew
+        (FLAG_PART_OVERFLOW); with retry=True that is checked (one stream synchronisation) and the
+        probe re-run with the exact split, as the ABI prescribes."""
+        n = keys.numel()
+        if part is None:
+            part = self.alloc_partitioned(n, chunk)
+        if part["n_rows"] != n or part["chunk"] != chunk:
+            raise CCJError("partition workspace was sized for another column / chunk")
         if out is None:
             alloc_kw.setdefault("rounds", False)
-            out = self.alloc_outputs(keys.numel(), chunk, **alloc_kw)
-        if part is None:
-            part = self.alloc_partitioned(keys.numel())
+            out = self.alloc_outputs(part["positions"], chunk, **alloc_kw)
+        n_chunks = (part["positions"] + chunk - 1) // chunk
+        if out["count"].numel() < n_chunks or out["sel"].numel() < n_chunks * out["cap"]:
+            raise CCJError("probe output buffers smaller than the partitioned layout needs")
         a = self._args(keys, chunk, None, None, out)
         a.out_round_counts = None  # no Next boundaries in partition order
-        check(lib().ccj_probe_partitioned(self._h, C.byref(a), _ptr(part["row_map"]), _ptr(part["ws"]),
+        flags = PART_EXACT if exact else 0
+        check(lib().ccj_probe_partitioned(self._h, C.byref(a), flags, _ptr(part["row_map"]), _ptr(part["ws"]),
                                           part["ws_bytes"], _stream(stream)), "ccj_probe_partitioned")
+        if retry and not exact:
+            import torch
+            if stream is not None:
+                stream.synchronize()
+            else:
+                torch.cuda.synchronize()
+            st = int(out["status"].item())
+            if st & FLAG_PART_OVERFLOW:
+                out["status"].fill_(st & ~FLAG_PART_OVERFLOW)
+                torch.cuda.synchronize()  # the fill ran on torch's stream, the re-run goes on `stream`
+                check(lib().ccj_probe_partitioned(self._h, C.byref(a), PART_EXACT, _ptr(part["row_map"]),
+                                                  _ptr(part["ws"]), part["ws_bytes"], _stream(stream)),
+                      "ccj_probe_partitioned")
+                out["exact_retry"] = True
+        out["n_chunks"] = n_chunks
         out["row_map"] = part["row_map"]
         return out
 

@@ -452,13 +452,45 @@ int fill_probe_params(const ccj_table *t, const ccj_probe_args *a, ccj::ProbePar
 }
 }  // namespace
 
-size_t ccj_probe_partitioned_workspace_size(const ccj_table *t, uint64_t n_rows) {
+namespace {
+// Layout of the partitioned column: identity (table = one window), or the fixed-capacity split's
+// parts * 8 segments of seg_cap positions (the exact split uses a prefix of the same positions).
+struct PartLayout {
+  ccj::SlotPlan pl;
+  uint32_t parts;
+  uint64_t seg_cap, positions;
+};
+PartLayout part_layout(const ccj_table *t, uint64_t n_rows, uint32_t chunk) {
+  PartLayout L{};
+  L.pl = ccj::slot_plan(t->info.size);
+  L.parts = 1u << (L.pl.lo_bits + L.pl.hi_bits);
+  if (L.pl.lo_bits == 0 || n_rows == 0 || chunk == 0) {
+    L.positions = n_rows;
+    return L;
+  }
+  L.seg_cap = ccj::slot_seg_cap(n_rows, L.pl, chunk);
+  L.positions = (uint64_t)L.parts * 8 * L.seg_cap;
+  return L;
+}
+uint64_t align256(uint64_t b) { return (b + 255) & ~255ull; }
+}  // namespace
+
+uint64_t ccj_probe_partitioned_positions(const ccj_table *t, uint64_t n_rows, uint32_t chunk) {
   if (!t) return 0;
-  return ((n_rows * 8 + 255) & ~255ull) + ccj::slot_partition_workspace(n_rows, ccj::slot_plan(t->info.size));
+  return part_layout(t, n_rows, chunk).positions;
 }
 
-int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t *out_row_map, void *ws,
-                          size_t ws_bytes, ccj_stream stream) {
+size_t ccj_probe_partitioned_workspace_size(const ccj_table *t, uint64_t n_rows, uint32_t chunk) {
+  if (!t) return 0;
+  const PartLayout L = part_layout(t, n_rows, chunk);
+  // partitioned keys (positions) + the fixed split's cursors, or the exact split's pass scratch
+  const size_t fixed = align256((uint64_t)L.parts * 8 * 4);
+  const size_t exact = ccj::slot_partition_workspace(n_rows, L.pl);
+  return align256(L.positions * 8) + (fixed > exact ? fixed : exact);
+}
+
+int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t flags, uint32_t *out_row_map,
+                          void *ws, size_t ws_bytes, ccj_stream stream) {
   ccj::ProbeParams p;
   if (int rc = fill_probe_params(t, a, p)) return rc;
   if (t->info.kind != CCJ_TABLE_LP) return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: LP tables only");
@@ -466,18 +498,35 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   if (a->out_pos || a->n_payload_cols || a->out_round_counts)
     return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: out_pos/payload columns/round counts not supported");
   if (a->n_rows >= (1ull << 32)) return fail(CCJ_ERR_LIMIT, "ccj_probe_partitioned: n_rows must be < 2^32");
+  if (flags & ~CCJ_PART_EXACT) return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: unknown flags");
   if (a->n_rows == 0) return CCJ_OK;
-  if (!out_row_map || !ws || ws_bytes < ccj_probe_partitioned_workspace_size(t, a->n_rows))
+  if (!out_row_map || !ws || ws_bytes < ccj_probe_partitioned_workspace_size(t, a->n_rows, a->chunk))
     return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: missing row map or workspace too small");
-  const ccj::SlotPlan pl = ccj::slot_plan(t->info.size);
+  const PartLayout L = part_layout(t, a->n_rows, a->chunk);
+  const bool exact = (flags & CCJ_PART_EXACT) != 0;
+  if (L.pl.lo_bits && !exact && !a->status)
+    return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: the fixed-capacity split needs args->status");
   hipStream_t s = (hipStream_t)stream;
   int64_t *pkeys = (int64_t *)ws;
-  void *rest = (char *)ws + ((a->n_rows * 8 + 255) & ~255ull);
-  if (pl.lo_bits == 0) {  // the whole table is one window: identity order
+  void *rest = (char *)ws + align256(L.positions * 8);
+  const uint64_t out_chunks = L.positions / a->chunk + (L.positions % a->chunk ? 1 : 0);
+  if (L.pl.lo_bits == 0) {  // the whole table is one window: identity order
     HIP_TRY(hipMemcpyAsync(pkeys, a->keys, a->n_rows * 8, hipMemcpyDeviceToDevice, s), "copy");
     HIP_TRY(ccj::launch_iota_u32(out_row_map, a->n_rows, s), "iota");
+  } else if (!exact) {
+    uint32_t *cursors = (uint32_t *)rest;
+    HIP_TRY(ccj::launch_slot_split_fixed(a->keys, a->n_rows, L.pl, L.seg_cap, cursors, pkeys, out_row_map, a->status,
+                                         s),
+            "slot split");
+    p.seg_count = cursors;
+    p.seg_parts = L.parts;
+    p.seg_cap = L.seg_cap;
+    p.n_rows = L.positions;
+    p.n_chunks = out_chunks;
   } else {
-    HIP_TRY(ccj::launch_slot_partition(a->keys, a->n_rows, pl, pkeys, out_row_map, rest, s), "slot partition");
+    HIP_TRY(ccj::launch_slot_partition(a->keys, a->n_rows, L.pl, pkeys, out_row_map, rest, s), "slot partition");
+    if (out_chunks > p.n_chunks)  // the layout's trailing chunks are empty in the exact form
+      HIP_TRY(hipMemsetAsync(a->out_count + p.n_chunks, 0, (out_chunks - p.n_chunks) * 4, s), "count tail");
   }
   p.keys = pkeys;
   p.xcd_swizzle = getenv("CCJ_NO_SWIZZLE") ? 0 : 1;

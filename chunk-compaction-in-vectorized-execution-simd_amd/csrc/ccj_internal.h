@@ -67,6 +67,11 @@ struct ProbeParams {
   // `keys` (sel must be NULL, counts required) and its outputs at out_base[c]; NULL = c*chunk, c*cap.
   const uint64_t *chunk_base;
   const uint64_t *out_base;
+  // Fixed-capacity partitioned input (ccj_probe_partitioned): chunk c's live rows are the first
+  // min(seg_count[g*seg_parts + d] - offset, chunk) of it, segment d*8+g = positions / seg_cap.
+  const uint32_t *seg_count;
+  uint32_t seg_parts;
+  uint64_t seg_cap;
   uint32_t xcd_swizzle;  // 1: consecutive chunks go to the same XCD (L2 reuse of partitioned input)
   uint32_t ablate;       // timing-only ablations (CCJ_ABLATE env, never set in product calls)
 };
@@ -110,7 +115,8 @@ hipError_t launch_compact(const ccj_compact_args &a, hipStream_t s);
 size_t partition_workspace(uint64_t n, uint32_t parts);
 // Slot-range partitioning for the L2-resident probe: partition p = slot >> window_bits, with the
 // partition bits split into a low digit (first LSD pass) and a high digit (second pass).
-constexpr uint32_t kWindowBits = 18;  // 2^18 slots = 2 MiB table window per partition
+constexpr uint32_t kWindowBits = 18;    // 2^18 slots = 2 MiB table window per partition
+constexpr uint32_t kSplitPartBits = 10;  // at most 1024 partitions (larger tables: larger windows)
 struct SlotPlan {
   uint32_t window_bits, lo_bits, hi_bits;
 };
@@ -118,6 +124,12 @@ SlotPlan slot_plan(uint64_t table_size);
 size_t slot_partition_workspace(uint64_t n, const SlotPlan &pl);
 hipError_t launch_slot_partition(const int64_t *keys, uint64_t n, const SlotPlan &pl, int64_t *out_keys,
                                  uint32_t *out_rows, void *ws, hipStream_t s);
+// One-pass fixed-capacity form: segment (partition d, XCD group g) = positions [(d*8+g)*cap, +cap);
+// cursors[g*parts + d] = rows that went to it (may exceed cap: CCJ_FLAG_PART_OVERFLOW raised).
+uint64_t slot_seg_cap(uint64_t n, const SlotPlan &pl, uint32_t chunk);
+hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPlan &pl, uint64_t cap,
+                                   uint32_t *cursors, int64_t *out_keys, uint32_t *out_rows, uint32_t *status,
+                                   hipStream_t s);
 hipError_t launch_partition_fixed(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t row_base, uint64_t seg_cap,
                                   int64_t *out_keys, uint32_t *out_rows, uint64_t *out_counts, uint32_t *status,
                                   void *ws, hipStream_t s);

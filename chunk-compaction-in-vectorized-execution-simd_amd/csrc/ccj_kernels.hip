@@ -436,6 +436,21 @@ constexpr int kFlatThreads = 256;
 constexpr int kFlatRows = kMaxChunk / kFlatThreads;  // 8
 constexpr uint32_t kFlatStage = kMaxChunk;          // matches staged in LDS per chunk
 
+// Live rows of the flat chunk starting at position `base`: all of them, or with the fixed-capacity
+// split's layout the part of the chunk below its segment's fill level.
+__device__ __forceinline__ uint32_t flat_phys(const ProbeParams &p, uint64_t base) {
+  const uint64_t rem = p.n_rows - base;
+  uint32_t phys = rem < p.chunk ? (uint32_t)rem : p.chunk;
+  if (p.seg_count) {
+    const uint64_t seg = base / p.seg_cap;
+    const uint64_t off = base - seg * p.seg_cap;
+    uint64_t live = p.seg_count[(seg & 7) * p.seg_parts + (seg >> 3)];
+    live = live < p.seg_cap ? live : p.seg_cap;
+    phys = live > off ? (live - off < phys ? (uint32_t)(live - off) : phys) : 0u;
+  }
+  return phys;
+}
+
 template <int KIND, int W>
 __global__ __launch_bounds__(kFlatThreads) void probe_flat(ProbeParams p) {
   __shared__ uint32_t s_cnt, s_rounds;
@@ -448,8 +463,7 @@ __global__ __launch_bounds__(kFlatThreads) void probe_flat(ProbeParams p) {
     if (c < n8) c = (c & 7) * (n8 >> 3) + (c >> 3);
   }
   const uint64_t base = c * p.chunk;
-  const uint64_t rem = p.n_rows - base;
-  const uint32_t phys = rem < p.chunk ? (uint32_t)rem : p.chunk;
+  const uint32_t phys = flat_phys(p, base);
   const uint64_t obase = c * p.cap;
   if (tid == 0) {
     s_cnt = 0;
@@ -1013,8 +1027,7 @@ __global__ __launch_bounds__(kFlatThreads) void probe_pair(ProbeParams p) {
     if (c < n8) c = (c & 7) * (n8 >> 3) + (c >> 3);
   }
   const uint64_t base = c * p.chunk;
-  const uint64_t rem = p.n_rows - base;
-  const uint32_t phys = rem < p.chunk ? (uint32_t)rem : p.chunk;
+  const uint32_t phys = flat_phys(p, base);
   const uint64_t obase = c * p.cap;
   for (uint32_t i = tid; i < phys; i += kFlatThreads) s_key[i] = __builtin_nontemporal_load(p.keys + base + i);
   if (tid == 0) {

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CCJ_ABI_VERSION 2
+#define CCJ_ABI_VERSION 3
 
 enum ccj_status {
   CCJ_OK = 0,
@@ -40,7 +40,9 @@ enum ccj_status {
 enum ccj_flag {
   CCJ_FLAG_CAP_OVERFLOW = 1u,   /* a chunk produced more than `cap` matches (extra matches dropped) */
   CCJ_FLAG_ROUND_OVERFLOW = 2u, /* a chunk took more than `max_rounds` rounds (counts not recorded) */
-  CCJ_FLAG_BAD_INPUT = 4u       /* count > chunk or a sel entry outside the chunk (rows skipped) */
+  CCJ_FLAG_BAD_INPUT = 4u,      /* count > chunk or a sel entry outside the chunk (rows skipped) */
+  CCJ_FLAG_PART_OVERFLOW = 8u   /* ccj_probe_partitioned: a fixed-capacity partition segment was full
+                                   (rows dropped): re-run with CCJ_PART_EXACT */
 };
 
 enum ccj_table_kind {
@@ -143,17 +145,27 @@ typedef struct ccj_probe_args {
 int ccj_probe(const ccj_table *table, const ccj_probe_args *args, ccj_stream stream);
 
 /* Slot-range-partitioned probe (the throughput path; L1/L2 parity, not L3 order).
- * LP tables only.  The probe column (args->keys, n_rows; sel and counts must be NULL) is first
- * split by its home slot's partition (slot >> 18: 2 MiB of table per partition, two LSD
- * passes), then probed chunk by chunk like ccj_probe with consecutive chunks kept on one XCD, so
- * each partition's table window is read from L2 instead of as random HBM lines.  Outputs are
- * ccj_probe's, over the partitioned column: out_sel indexes partitioned positions, and
- * out_row_map[pos] gives the original row of partitioned position pos.  Same matches, payloads
- * and per-row multiplicities as ccj_probe (L1 + L2); within a chunk the order is unspecified, so
- * out_round_counts, out_pos and payload columns are not produced (must be NULL / 0). */
-size_t ccj_probe_partitioned_workspace_size(const ccj_table *table, uint64_t n_rows);
-int ccj_probe_partitioned(const ccj_table *table, const ccj_probe_args *args, uint32_t *out_row_map,
-                          void *workspace, size_t workspace_bytes, ccj_stream stream);
+ * LP tables only.  The probe column (args->keys, n_rows < 2^32; sel and counts must be NULL) is
+ * first split by its home slot's partition (slot >> 18: 2 MiB of table per partition), then
+ * probed chunk by chunk like ccj_probe with consecutive chunks kept on one XCD, so each
+ * partition's table window is read from L2 instead of as random HBM lines.
+ *
+ * The split lays the column out in `positions` slots (ccj_probe_partitioned_positions):
+ *   - default: one pass into fixed-capacity segments (partition x XCD group), with gaps; a
+ *     segment that overflows (heavy key skew only) drops rows and raises
+ *     CCJ_FLAG_PART_OVERFLOW in *args->status (required): re-run with CCJ_PART_EXACT;
+ *   - flags & CCJ_PART_EXACT: exact-size two-pass LSD split, no gaps, never overflows.
+ * Outputs are ccj_probe's over that layout: args->out_count etc. hold positions / chunk chunks
+ * (chunk c = positions [c*chunk, (c+1)*chunk), empty ones report count 0), out_sel indexes
+ * positions inside the chunk, and out_row_map[pos] (positions entries) is the original row of a
+ * live position.  Same matches, payloads and per-row multiplicities as ccj_probe (L1 + L2);
+ * within a chunk the order is unspecified, so out_round_counts, out_pos and payload columns are
+ * not produced (must be NULL / 0). */
+#define CCJ_PART_EXACT 1u
+uint64_t ccj_probe_partitioned_positions(const ccj_table *table, uint64_t n_rows, uint32_t chunk);
+size_t ccj_probe_partitioned_workspace_size(const ccj_table *table, uint64_t n_rows, uint32_t chunk);
+int ccj_probe_partitioned(const ccj_table *table, const ccj_probe_args *args, uint32_t flags,
+                          uint32_t *out_row_map, void *workspace, size_t workspace_bytes, ccj_stream stream);
 
 /* ---- compaction ------------------------------------------------------------------------- */
 /* Replaces NaiveCompactor::Compact + Flush (compactor.cpp:5-41, compactor.h:23) applied to every

@@ -160,20 +160,48 @@ def test_l1_l2_large_membership(kind):
     assert O.l2_sum(rows, pay) == l2
 
 
+@pytest.mark.parametrize("exact", [False, True])
 @pytest.mark.parametrize("n_build,cf,n_probe,rng", [(1 << 20, 1, 1 << 22, 1 << 20), (1 << 22, 2, 1 << 23, 3 << 21),
                                                     (1 << 16, 1, 100000, 1 << 17), (1000, 1, 5000, 2000),
                                                     (1 << 24, 1, (1 << 24) + 77, 1 << 24)])
-def test_partitioned_probe_l1_l2(n_build, cf, n_probe, rng):
+def test_partitioned_probe_l1_l2(n_build, cf, n_probe, rng, exact):
     table = ccj.Table.reference(ccj.LP, n_build, cf, ccj.LAYOUT_DEVICE)
     keys = ccj.gen_uniform_keys(n_probe, 31, rng)
+    out = table.probe_partitioned(keys, 2048, exact=exact)
+    torch.cuda.synchronize()
+    assert int(out["status"].item()) == 0 and not out.get("exact_retry")
+    m, l2 = ccj.result_checksum(out, 2048, row_map=out["row_map"].to(torch.int64))
+    assert (m, l2) == O.count_uniform(31, 0, n_probe, rng, n_build, cf)
+    if exact or out["row_map"].numel() == n_probe:
+        # exact split (or one window): the row map is a permutation of the probe rows
+        rm = out["row_map"][:n_probe].cpu().numpy().view(np.uint32)
+        assert np.array_equal(np.sort(rm), np.arange(n_probe, dtype=np.uint32))
+
+
+@pytest.mark.parametrize("distinct", [1, 7, 3000])
+def test_partitioned_probe_skew_falls_back_to_exact(distinct):
+    """Heavy skew overflows the one-pass split's fixed segments: the ABI raises
+    FLAG_PART_OVERFLOW (rows dropped) and the wrapper re-runs with the exact split."""
+    n_build, n_probe = 1 << 20, 3 << 20
+    table = ccj.Table.reference(ccj.LP, n_build, 1, ccj.LAYOUT_DEVICE)
+    g = np.random.default_rng(distinct)
+    vals = g.integers(0, 2 * n_build, size=distinct)
+    keys_h = vals[g.integers(0, distinct, size=n_probe)].astype(np.int64)
+    keys = torch.from_numpy(keys_h).cuda()
+    raw = table.probe_partitioned(keys, 2048, retry=False)
+    torch.cuda.synchronize()
+    overflow = bool(int(raw["status"].item()) & ccj.FLAG_PART_OVERFLOW)
     out = table.probe_partitioned(keys, 2048)
     torch.cuda.synchronize()
     assert int(out["status"].item()) == 0
-    m, l2 = ccj.result_checksum(out, 2048, row_map=out["row_map"][:n_probe].to(torch.int64))
-    assert (m, l2) == O.count_uniform(31, 0, n_probe, rng, n_build, cf)
-    # the row map is a permutation of the probe rows, grouped by table window (slot >> 17)
-    rm = out["row_map"][:n_probe].cpu().numpy().view(np.uint32)
-    assert np.array_equal(np.sort(rm), np.arange(n_probe, dtype=np.uint32))
+    assert bool(out.get("exact_retry")) == overflow
+    if distinct <= 7:
+        assert overflow  # a handful of keys cannot spread over 1024 partitions x 8 groups
+    # expected answer by membership (reference generator: every key < n_build matches once)
+    hit = keys_h < n_build
+    rows = np.nonzero(hit)[0].astype(np.uint64)
+    want = (len(rows), O.l2_sum(rows, keys_h[hit]))
+    assert ccj.result_checksum(out, 2048, row_map=out["row_map"].to(torch.int64)) == want
 
 
 def test_partitioned_probe_same_rows_as_chunk_probe():
