@@ -69,7 +69,7 @@ def parse():
     ap.add_argument("--n-probe", type=int, default=1 << 30, help="probe keys per GPU")
     ap.add_argument("--chunk", type=int, default=2048)
     ap.add_argument("--layout", default="device", choices=["device", "reference"])
-    ap.add_argument("--path", default="chunk", choices=["partitioned", "chunk"],
+    ap.add_argument("--path", default="partitioned", choices=["partitioned", "chunk"],
                     help="partitioned: slot-range partition + L2-resident probe (L1/L2 parity); "
                          "chunk: reference-order chunk probe (L3 parity)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -484,12 +484,15 @@ def main():
     alg_bytes = alg_bytes_per_tuple * n_probe
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
+    kernels_ms = None
+    # DRAM bytes per step of THIS path's kernels, from tools/profile.sh + tools/prof_summary.py
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_{args.path}.json")
     if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
             if pmc.get("n_probe") == n_probe and pmc.get("n_build") == n_build:
                 traffic = pmc.get("hbm_bytes_per_launch")
+                kernels_ms = pmc.get("kernels_ms")
         except (OSError, ValueError):
             pass
 
@@ -513,9 +516,9 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          # measured DRAM bytes (whole 128-B lines per random slot read) per second
                          "traffic_GBps": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
-                         "kernel": ("ccj_probe_partitioned (one-pass slot split + probe_pair)"
+                         "kernel": ("ccj_probe_partitioned (slot_split_fixed + probe_win<2,4,4>)"
                                     if args.path == "partitioned" else "probe_chunks<LP,2>"),
-                         "kernel_ms": kern_ms,
+                         "kernel_ms": kern_ms, "rocprof_kernels_ms": kernels_ms,
                          "alg_bytes_per_tuple": alg_bytes_per_tuple, "s_bar": s_bar, "m_bar": m_bar},
             "cpu_baseline": cpu,
             "parity": parity,

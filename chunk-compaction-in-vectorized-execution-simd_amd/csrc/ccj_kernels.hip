@@ -12,6 +12,7 @@
 // result_vector order (L3).  Per-row state lives in VGPRs (key, slot/chain position, chain end);
 // active/match sets are bitmasks over the lane's R rows.
 #include <cstdlib>
+#include <string>
 
 #include "ccj_internal.h"
 
@@ -1175,30 +1176,220 @@ __global__ __launch_bounds__(kFlatThreads) void probe_pair(ProbeParams p) {
   if (p.status && (overflow || total > p.cap)) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
 }
 
+// LP walk for slot-partitioned input (probe_win): LPR lanes per row (1 or 2), windows of WS slots
+// (each lane loads WS / LPR of them as 16-byte pieces), R rows in flight per lane group.  ALIGN:
+// windows aligned to WS slots; otherwise a window starts at the row's next unread slot (clamped so
+// it never passes the table end), which covers WS slots of the run with every load.  Against
+// probe_pair the per-step bookkeeping is bit arithmetic on the window's empty / match masks (one
+// DPP swap for LPR = 2, nothing cross-lane for LPR = 1), the wave prefix of the step's matches is
+// bit-sliced over ballots instead of a shuffle scan, and a finished cursor takes the chunk's next
+// unwalked row from an LDS counter (one atomic per wave and step), so every thread stays busy
+// until the chunk's rows run out instead of draining a fixed share.
+template <int LPR, int WS, int R, bool ALIGN>
+__global__ __launch_bounds__(kFlatThreads) void probe_win(ProbeParams p) {
+  constexpr uint32_t kGroups = kFlatThreads / LPR;  // rows walked side by side
+  constexpr int kSlotsPerLane = WS / LPR;
+  constexpr int kLoads = kSlotsPerLane / 2;  // 16-byte pieces per lane and window
+  static_assert(kLoads >= 1 && WS <= 16 && (LPR == 1 || LPR == 2), "window shape");
+  __shared__ uint32_t s_cnt, s_rounds, s_next;
+  __shared__ int64_t s_key[kMaxChunk];
+  __shared__ uint32_t s_sel[kFlatStage];
+  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1);
+  const uint32_t sub = LPR == 1 ? 0u : (tid & 1u), grp = tid / LPR;
+  const uint32_t last_start = p.mask - (uint32_t)(WS - 1);  // table size - WS (size >= 16)
+  uint64_t c = blockIdx.x;
+  if (p.xcd_swizzle) {
+    const uint64_t n8 = p.n_chunks & ~7ull;
+    if (c < n8) c = (c & 7) * (n8 >> 3) + (c >> 3);
+  }
+  const uint64_t base = c * p.chunk;
+  const uint32_t phys = flat_phys(p, base);
+  const uint64_t obase = c * p.cap;
+  for (uint32_t i = tid; i < phys; i += kFlatThreads) s_key[i] = __builtin_nontemporal_load(p.keys + base + i);
+  if (tid == 0) {
+    s_cnt = 0;
+    s_rounds = 0;
+    s_next = kGroups * R;
+  }
+  __syncthreads();
+  int64_t key[R];
+  uint32_t row[R], cur[R], r0[R];
+  uint32_t need = 0, lane_rounds = 0, overflow = 0;
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    row[k] = (uint32_t)k * kGroups + grp;
+    r0[k] = 0;
+    key[k] = 0;
+    cur[k] = 0;
+    if (row[k] < phys) {
+      key[k] = s_key[row[k]];
+      cur[k] = (uint32_t)murmurhash64((uint64_t)key[k]) & p.mask;
+      need |= 1u << k;
+    }
+  }
+  while (__ballot(need != 0u) != 0ull) {
+    int64_t v[R][kSlotsPerLane];
+    uint32_t st[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      st[k] = ALIGN ? (cur[k] & ~(uint32_t)(WS - 1)) : (cur[k] < last_start ? cur[k] : last_start);
+      if ((need >> k) & 1u) {
+        const int64_t *w = p.table + st[k] + sub * kSlotsPerLane;
+#pragma unroll
+        for (int t = 0; t < kSlotsPerLane; t += 2) {
+          if (p.ablate & 2u) {  // timing only: no table reads
+            v[k][t] = t ? -1 : key[k];
+            v[k][t + 1] = -1;
+          } else if (ALIGN) {
+            const longlong2 x = *reinterpret_cast<const longlong2 *>(w + t);
+            v[k][t] = x.x;
+            v[k][t + 1] = x.y;
+          } else {  // 8-byte aligned pair of slots
+            v[k][t] = w[t];
+            v[k][t + 1] = w[t + 1];
+          }
+        }
+      }
+    }
+    uint32_t hits[R], n = 0, done = 0;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      uint32_t e = 0, m = 0;
+#pragma unroll
+      for (int t = 0; t < kSlotsPerLane; ++t) {
+        const uint32_t b = sub * kSlotsPerLane + t;
+        e |= ((v[k][t] == -1) ? 1u : 0u) << b;
+        m |= ((v[k][t] == key[k]) ? 1u : 0u) << b;
+      }
+      if (LPR == 2) {  // the pair's halves of the window: swap with the partner lane (quad_perm 1,0,3,2)
+        e |= (uint32_t)__builtin_amdgcn_mov_dpp((int)e, 0xB1, 0xF, 0xF, false);
+        m |= (uint32_t)__builtin_amdgcn_mov_dpp((int)m, 0xB1, 0xF, 0xF, false);
+      }
+      hits[k] = 0;
+      if ((need >> k) & 1u) {
+        const uint32_t off = cur[k] - st[k];
+        const uint32_t from = ~0u << off;
+        e &= from;
+        const uint32_t f = e ? (uint32_t)__builtin_ctz(e) : (uint32_t)WS;  // first empty slot: the run's end
+        hits[k] = m & from & ((1u << f) - 1u);
+        if (e) {
+          const uint32_t r = r0[k] + f - off;  // occupied slots walked = the reference's rounds
+          lane_rounds = r > lane_rounds ? r : lane_rounds;
+          done |= 1u << k;
+        } else {
+          r0[k] += (uint32_t)WS - off;
+          cur[k] = (st[k] + (uint32_t)WS) & p.mask;
+        }
+      }
+      if (sub) hits[k] = 0;  // the pair's first lane emits
+      n += (uint32_t)__builtin_popcount(hits[k]);
+    }
+    // Wave prefix of the step's matches, bit-sliced over ballots (n <= R * WS).
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int b = 0; (1 << b) <= R * WS; ++b) {
+      const uint64_t bm = __ballot((n >> b) & 1u);
+      pre += lane_prefix(bm) << b;
+      tot += (uint32_t)__popcll(bm) << b;
+    }
+    if (tot) {
+      uint32_t wb = 0;
+      if (lane == 0) wb = atomicAdd(&s_cnt, tot);
+      wb = (uint32_t)__builtin_amdgcn_readfirstlane((int)wb);
+      if (n && !(p.ablate & 1u)) {
+        uint32_t o = wb + pre;
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          for (uint32_t hm = hits[k]; hm; hm &= hm - 1u, ++o) {
+            if (o < kFlatStage) {
+              s_sel[o] = row[k];  // payload = s_key[row]: the matched table value == probe key
+            } else if (o < p.cap) {
+              p.out_sel[obase + o] = row[k];
+              if (p.out_payload) p.out_payload[obase + o] = key[k];
+            } else {
+              overflow = 1;
+            }
+          }
+        }
+      }
+    }
+    // Finished cursors take the chunk's next rows: one LDS atomic per wave and step.
+    const uint32_t nd = sub ? 0u : (uint32_t)__builtin_popcount(done);
+    uint32_t dpre = 0, dtot = 0;
+#pragma unroll
+    for (int b = 0; (1 << b) <= R; ++b) {
+      const uint64_t bm = __ballot((nd >> b) & 1u);
+      dpre += lane_prefix(bm) << b;
+      dtot += (uint32_t)__popcll(bm) << b;
+    }
+    if (dtot) {
+      uint32_t rb = 0;
+      if (lane == 0) rb = atomicAdd(&s_next, dtot);
+      rb = (uint32_t)__builtin_amdgcn_readfirstlane((int)rb) + dpre;
+      if (LPR == 2) rb = (uint32_t)__builtin_amdgcn_mov_dpp((int)rb, 0xA0, 0xF, 0xF, false);  // quad_perm 0,0,2,2
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        if ((done >> k) & 1u) {
+          need &= ~(1u << k);
+          row[k] = rb++;
+          r0[k] = 0;
+          if (row[k] < phys) {
+            key[k] = s_key[row[k]];
+            cur[k] = (uint32_t)murmurhash64((uint64_t)key[k]) & p.mask;
+            need |= 1u << k;
+          }
+        }
+      }
+    }
+  }
+  {
+    const uint32_t wr = wave_max(lane_rounds);
+    if (lane == 0) atomicMax(&s_rounds, wr);
+  }
+  __syncthreads();
+  const uint32_t total = s_cnt;
+  const uint32_t staged = total < kFlatStage ? total : kFlatStage;
+  if (!(p.ablate & 1u)) {
+    for (uint32_t o = tid; o < staged && o < p.cap; o += kFlatThreads) {
+      __builtin_nontemporal_store(s_sel[o], p.out_sel + obase + o);
+      if (p.out_payload) __builtin_nontemporal_store(s_key[s_sel[o]], p.out_payload + obase + o);
+    }
+  }
+  if (tid == 0) {
+    p.out_count[c] = total < p.cap ? total : (uint32_t)p.cap;
+    if (p.out_rounds) p.out_rounds[c] = s_rounds;
+  }
+  if (p.status && (overflow || total > p.cap)) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
+}
+
 hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
   if (p.n_chunks == 0) return hipSuccess;
   const dim3 g((unsigned)p.n_chunks), b(kFlatThreads);
-  // 16-byte windows: probe_flat<.., 4> (two loads per step) measured 14.3 ms vs 13.2 ms at C2, and a
-  // 4-lane cooperative 64-byte-window walk 23 ms (VALU-bound: 4 lanes per row).
-  static const int pair = [] {
-    const char *e = getenv("CCJ_FLAT_PAIR");  // 0: one lane per row (probe_flat)
-    return e ? atoi(e) : 4;
-  }();
   const uint64_t size = (uint64_t)p.mask + 1;
-  if (pair && (kind != CCJ_TABLE_LP || size >= 4)) {
-    if (kind == CCJ_TABLE_LP) {
-      if (pair == 2) hipLaunchKernelGGL((probe_pair<CCJ_TABLE_LP, 2>), g, b, 0, s, p);
-      else if (pair == 3) hipLaunchKernelGGL((probe_pair<CCJ_TABLE_LP, 3>), g, b, 0, s, p);
-      else if (pair == 6) hipLaunchKernelGGL((probe_pair<CCJ_TABLE_LP, 6>), g, b, 0, s, p);
-      else if (pair == 8) hipLaunchKernelGGL((probe_pair<CCJ_TABLE_LP, 8>), g, b, 0, s, p);
-      else hipLaunchKernelGGL((probe_pair<CCJ_TABLE_LP, 4>), g, b, 0, s, p);
-    } else {
-      hipLaunchKernelGGL((probe_pair<CCJ_TABLE_CHAIN, 4>), g, b, 0, s, p);
-    }
+  if (kind != CCJ_TABLE_LP) {
+    hipLaunchKernelGGL((probe_pair<CCJ_TABLE_CHAIN, 4>), g, b, 0, s, p);
     return hipGetLastError();
   }
-  if (kind == CCJ_TABLE_LP) hipLaunchKernelGGL((probe_flat<CCJ_TABLE_LP, 2>), g, b, 0, s, p);
-  else hipLaunchKernelGGL((probe_flat<CCJ_TABLE_CHAIN, 2>), g, b, 0, s, p);
+  // CCJ_PROBE_VARIANT (tuning override, read per launch): pair4 | flat | wL_Wa_R / wL_Wu_R =
+  // probe_win<L lanes per row, W-slot windows, aligned (a) or from the next slot (u), R rows>.
+  // At C2 (profiles/r1b_*): w2_4a_4 11.6 ms, w1_2u_3 11.6, w1_4u_2 11.8, pair4 12.1; w1_8a_2
+  // 15.5 and w2_8a_* 12.2 (wider windows cost more L2 requests than they save).
+  const char *e = getenv("CCJ_PROBE_VARIANT");
+  const std::string v = e && *e ? e : "w2_4a_4";
+  if (size < 16 || v == "pair4") {
+    if (size >= 4) hipLaunchKernelGGL((probe_pair<CCJ_TABLE_LP, 4>), g, b, 0, s, p);
+    else hipLaunchKernelGGL((probe_flat<CCJ_TABLE_LP, 2>), g, b, 0, s, p);
+  } else if (v == "flat") {
+    hipLaunchKernelGGL((probe_flat<CCJ_TABLE_LP, 2>), g, b, 0, s, p);
+  } else if (v == "w1_2u_3") {
+    hipLaunchKernelGGL((probe_win<1, 2, 3, false>), g, b, 0, s, p);
+  } else if (v == "w2_4a_4") {
+    hipLaunchKernelGGL((probe_win<2, 4, 4, true>), g, b, 0, s, p);
+  } else if (v == "w1_4u_2") {
+    hipLaunchKernelGGL((probe_win<1, 4, 2, false>), g, b, 0, s, p);
+  } else {
+    hipLaunchKernelGGL((probe_win<2, 4, 4, true>), g, b, 0, s, p);  // w2_4a_4
+  }
   return hipGetLastError();
 }
 

@@ -302,7 +302,7 @@ static_assert(kSplitParts <= (uint32_t)kSplitThreads, "one partition per thread 
 __global__ __launch_bounds__(kSplitThreads) void slot_split_fixed(const int64_t *keys, uint64_t n, uint32_t shift,
                                                                  uint32_t parts, uint64_t n_tiles, uint32_t *cur,
                                                                  uint64_t cap, int64_t *out_k, uint32_t *out_r,
-                                                                 uint32_t *status) {
+                                                                 uint32_t *status, uint32_t ablate) {
   __shared__ int64_t s_k[kSplitTile];
   __shared__ uint16_t s_i[kSplitTile];
   __shared__ uint32_t s_hist[kSplitParts], s_loc[kSplitParts], s_lim[kSplitParts];
@@ -321,7 +321,8 @@ __global__ __launch_bounds__(kSplitThreads) void slot_split_fixed(const int64_t 
 #pragma unroll
     for (int it = 0; it < kSplitPer; ++it) {
       const uint32_t li = (uint32_t)it * kSplitThreads + tid;
-      kk[it] = li < tn ? __builtin_nontemporal_load(keys + t0 + li) : 0;
+      if (ablate & 0x20u) kk[it] = (int64_t)((t0 + li) * 0x9E3779B97F4A7C15ull >> 20);  // timing only: no key reads
+      else kk[it] = li < tn ? __builtin_nontemporal_load(keys + t0 + li) : 0;
     }
   };
   if (tile < tend) load(tile);
@@ -348,7 +349,7 @@ __global__ __launch_bounds__(kSplitThreads) void slot_split_fixed(const int64_t 
       if (lane >= (uint32_t)o) incl += v;
     }
     if (lane == 63) s_wsum[wave] = incl;
-    const uint32_t r = h ? atomicAdd(&cur[(uint64_t)g * parts + tid], h) : 0u;  // flies during the image build
+    const uint32_t r = h && !(ablate & 0x40u) ? atomicAdd(&cur[(uint64_t)g * parts + tid], h) : 0u;  // flies during the image build
     __syncthreads();
     uint32_t wpre = 0;
     for (uint32_t w = 0; w < wave; ++w) wpre += s_wsum[w];
@@ -376,7 +377,7 @@ __global__ __launch_bounds__(kSplitThreads) void slot_split_fixed(const int64_t 
       const int64_t k = s_k[q];
       const uint32_t d = (uint32_t)(murmurhash64((uint64_t)k) >> shift) & mask;
       const uint32_t o = q - s_loc[d];
-      if (o < s_lim[d]) {
+      if (o < s_lim[d] && !(ablate & 0x10u)) {  // (0x10: timing only, no stores)
         const uint64_t dest = s_dst[d] + o;
         out_k[dest] = k;
         out_r[dest] = (uint32_t)(t0 + s_i[q]);
@@ -386,6 +387,7 @@ __global__ __launch_bounds__(kSplitThreads) void slot_split_fixed(const int64_t 
   }
   if (dropped && status) atomicOr(status, CCJ_FLAG_PART_OVERFLOW);
 }
+
 }  // namespace
 
 uint64_t slot_seg_cap(uint64_t n, const SlotPlan &pl, uint32_t chunk) {
@@ -410,8 +412,10 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     return (unsigned)(cus >= 8 ? cus / 8 * 8 : 8);
   }();
+  const char *ab = getenv("CCJ_ABLATE");  // timing-only ablations (never set in product calls)
+  const uint32_t ablate = ab ? (uint32_t)atoi(ab) : 0u;
   hipLaunchKernelGGL(slot_split_fixed, dim3(blocks), dim3(kSplitThreads), 0, s, keys, n, pl.window_bits, parts,
-                     n_tiles, cursors, cap, out_keys, out_rows, status);
+                     n_tiles, cursors, cap, out_keys, out_rows, status, ablate);
   return hipGetLastError();
 }
 
