@@ -376,8 +376,6 @@ def main():
     t0 = time.perf_counter()
     c5 = args.workload == "c5"
     P = 8 if c5 else 0
-    if c5:
-        args.path = "chunk"  # the partitioned path does not gather payload columns
     with torch.cuda.stream(stream):
         table = ccj.Table.reference(ccj.LP, n_build, 1, layout, stream=stream)
         if c5:  # C5 payload of build tuple t (key k): p_c = k*(c+1)+c, row-major [n_build, 8]
@@ -387,11 +385,12 @@ def main():
             table.set_payload(pay.reshape(-1), P, stream=stream)
             del bk, pay
         keys = ccj.gen_uniform_keys(n_probe, SEED, n_build, first_row=rank * n_probe, stream=stream)
-        out = table.alloc_outputs(n_probe, chunk, rounds=True, payload_cols=P)
-        part = out_p = None
-        if args.path == "partitioned" or not c5:  # the headline path, or the one timed beside it
+        out = part = out_p = None
+        if args.path == "chunk" or not c5:  # C2: both paths (the headline and the one timed beside it)
+            out = table.alloc_outputs(n_probe, chunk, rounds=True, payload_cols=P)
+        if args.path == "partitioned" or not c5:
             part = table.alloc_partitioned(n_probe, chunk)
-            out_p = table.alloc_outputs(part["positions"], chunk, rounds=False)
+            out_p = table.alloc_outputs(part["positions"], chunk, rounds=False, payload_cols=P)
     stream.synchronize()
     log(f"[setup] table {table.size} slots, max_rounds {table.max_rounds}, keys {n_probe}: "
         f"{time.perf_counter() - t0:.1f} s")
@@ -463,11 +462,13 @@ def main():
     parity = {"status_flags": status, "matches": matches, "l2": hex(l2)}
     if c5:  # every gathered payload column holds the matched build tuple's p_c (key == payload)
         torch.cuda.current_stream().wait_stream(stream)
-        cnt = out["count"].to(torch.int64)
-        valid = torch.arange(out["cap"], device=dev)[None, :] < cnt[:, None]
-        pk = out["payload"].view(-1, out["cap"])
+        res = out_p if args.path == "partitioned" else out
+        nc = res["n_chunks"]
+        cnt = res["count"][:nc].to(torch.int64)
+        valid = torch.arange(res["cap"], device=dev)[None, :] < cnt[:, None]
+        pk = res["payload"][:nc * res["cap"]].view(-1, res["cap"])
         parity["payload_cols_ok"] = all(
-            bool(((out["payload_cols"][c].view(-1, out["cap"]) == pk * (c + 1) + c) | ~valid).all())
+            bool(((res["payload_cols"][c][:nc * res["cap"]].view(-1, res["cap"]) == pk * (c + 1) + c) | ~valid).all())
             for c in range(P))
         del cnt, valid, pk
 
@@ -516,8 +517,10 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          # measured DRAM bytes (whole 128-B lines per random slot read) per second
                          "traffic_GBps": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
-                         "kernel": ("ccj_probe_partitioned (slot_split_fixed + probe_win<2,4,4>)"
-                                    if args.path == "partitioned" else "probe_chunks<LP,2>"),
+                         "kernel": (("ccj_probe_partitioned (slot_split_fixed + probe_win<2,4,4>"
+                                     + (" with positions + gather_payload_quad)" if c5 else ")"))
+                                    if args.path == "partitioned" else "probe_chunks<LP,2>"
+                                    + (" + gather_payload_quad" if c5 else "")),
                          "kernel_ms": kern_ms, "rocprof_kernels_ms": kernels_ms,
                          "alg_bytes_per_tuple": alg_bytes_per_tuple, "s_bar": s_bar, "m_bar": m_bar},
             "cpu_baseline": cpu,

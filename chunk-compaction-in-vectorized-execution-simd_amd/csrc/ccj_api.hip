@@ -495,8 +495,10 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   if (int rc = fill_probe_params(t, a, p)) return rc;
   if (t->info.kind != CCJ_TABLE_LP) return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: LP tables only");
   if (a->sel || a->counts) return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: sel/counts must be NULL");
-  if (a->out_pos || a->n_payload_cols || a->out_round_counts)
-    return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: out_pos/payload columns/round counts not supported");
+  if (a->out_round_counts)
+    return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: no round counts (no Next boundaries in partition order)");
+  if ((a->out_pos || a->n_payload_cols) && t->info.size < 16)
+    return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: positions / payload columns need a table of >= 16 slots");
   if (a->n_rows >= (1ull << 32)) return fail(CCJ_ERR_LIMIT, "ccj_probe_partitioned: n_rows must be < 2^32");
   if (flags & ~CCJ_PART_EXACT) return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: unknown flags");
   if (a->n_rows == 0) return CCJ_OK;
@@ -531,7 +533,21 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   p.keys = pkeys;
   p.xcd_swizzle = getenv("CCJ_NO_SWIZZLE") ? 0 : 1;
   if (const char *ab = getenv("CCJ_ABLATE")) p.ablate = (uint32_t)atoi(ab);
-  HIP_TRY(ccj::launch_probe_flat(t->info.kind, p, s), "probe launch");
+  if (p.n_pay == 0) {
+    HIP_TRY(ccj::launch_probe_flat(t->info.kind, p, s), "probe launch");
+    return CCJ_OK;
+  }
+  // Wide payload (C5): the walk records every match's table position, a second pass gathers rows
+  // (consecutive chunks share a table window, so their payload rows stay in the Infinity Cache).
+  uint32_t *pos = p.out_pos;
+  if (!pos) HIP_TRY(hipMallocAsync((void **)&pos, p.n_chunks * p.cap * sizeof(uint32_t), s), "payload positions");
+  ccj::ProbeParams q = p;
+  q.out_pos = pos;
+  q.n_pay = 0;
+  hipError_t e = ccj::launch_probe_flat(t->info.kind, q, s);
+  if (e == hipSuccess) e = ccj::launch_gather_payload(p, pos, s);
+  if (!p.out_pos) (void)hipFreeAsync(pos, s);
+  HIP_TRY(e, "partitioned probe + payload gather launch");
   return CCJ_OK;
 }
 

@@ -1185,7 +1185,7 @@ __global__ __launch_bounds__(kFlatThreads) void probe_pair(ProbeParams p) {
 // bit-sliced over ballots instead of a shuffle scan, and a finished cursor takes the chunk's next
 // unwalked row from an LDS counter (one atomic per wave and step), so every thread stays busy
 // until the chunk's rows run out instead of draining a fixed share.
-template <int LPR, int WS, int R, bool ALIGN>
+template <int LPR, int WS, int R, bool ALIGN, bool POS = false>
 __global__ __launch_bounds__(kFlatThreads) void probe_win(ProbeParams p) {
   constexpr uint32_t kGroups = kFlatThreads / LPR;  // rows walked side by side
   constexpr int kSlotsPerLane = WS / LPR;
@@ -1194,6 +1194,7 @@ __global__ __launch_bounds__(kFlatThreads) void probe_win(ProbeParams p) {
   __shared__ uint32_t s_cnt, s_rounds, s_next;
   __shared__ int64_t s_key[kMaxChunk];
   __shared__ uint32_t s_sel[kFlatStage];
+  __shared__ uint32_t s_pos[POS ? kFlatStage : 1];  // POS (C5): every match's table position
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1);
   const uint32_t sub = LPR == 1 ? 0u : (tid & 1u), grp = tid / LPR;
   const uint32_t last_start = p.mask - (uint32_t)(WS - 1);  // table size - WS (size >= 16)
@@ -1303,9 +1304,11 @@ __global__ __launch_bounds__(kFlatThreads) void probe_win(ProbeParams p) {
           for (uint32_t hm = hits[k]; hm; hm &= hm - 1u, ++o) {
             if (o < kFlatStage) {
               s_sel[o] = row[k];  // payload = s_key[row]: the matched table value == probe key
+              if (POS) s_pos[o] = st[k] + (uint32_t)__builtin_ctz(hm);
             } else if (o < p.cap) {
               p.out_sel[obase + o] = row[k];
               if (p.out_payload) p.out_payload[obase + o] = key[k];
+              if (POS) p.out_pos[obase + o] = st[k] + (uint32_t)__builtin_ctz(hm);
             } else {
               overflow = 1;
             }
@@ -1353,6 +1356,7 @@ __global__ __launch_bounds__(kFlatThreads) void probe_win(ProbeParams p) {
     for (uint32_t o = tid; o < staged && o < p.cap; o += kFlatThreads) {
       __builtin_nontemporal_store(s_sel[o], p.out_sel + obase + o);
       if (p.out_payload) __builtin_nontemporal_store(s_key[s_sel[o]], p.out_payload + obase + o);
+      if (POS) __builtin_nontemporal_store(s_pos[o], p.out_pos + obase + o);
     }
   }
   if (tid == 0) {
@@ -1376,7 +1380,10 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
   // 15.5 and w2_8a_* 12.2 (wider windows cost more L2 requests than they save).
   const char *e = getenv("CCJ_PROBE_VARIANT");
   const std::string v = e && *e ? e : "w2_4a_4";
-  if (size < 16 || v == "pair4") {
+  if (p.out_pos) {  // C5: table positions of the matches for the payload gather (default walk)
+    if (size < 16) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((probe_win<2, 4, 4, true, true>), g, b, 0, s, p);
+  } else if (size < 16 || v == "pair4") {
     if (size >= 4) hipLaunchKernelGGL((probe_pair<CCJ_TABLE_LP, 4>), g, b, 0, s, p);
     else hipLaunchKernelGGL((probe_flat<CCJ_TABLE_LP, 2>), g, b, 0, s, p);
   } else if (v == "flat") {

@@ -414,7 +414,12 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
   }();
   const char *ab = getenv("CCJ_ABLATE");  // timing-only ablations (never set in product calls)
   const uint32_t ablate = ab ? (uint32_t)atoi(ab) : 0u;
-  hipLaunchKernelGGL(slot_split_fixed, dim3(blocks), dim3(kSplitThreads), 0, s, keys, n, pl.window_bits, parts,
+  unsigned nb = blocks;
+  if (const char *e = getenv("CCJ_SPLIT_BLOCKS")) {  // tuning override: fewer persistent workgroups
+    const unsigned v = (unsigned)atoi(e) / 8 * 8;
+    if (v >= 8 && v <= blocks) nb = v;
+  }
+  hipLaunchKernelGGL(slot_split_fixed, dim3(nb), dim3(kSplitThreads), 0, s, keys, n, pl.window_bits, parts,
                      n_tiles, cursors, cap, out_keys, out_rows, status, ablate);
   return hipGetLastError();
 }

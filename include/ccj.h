@@ -159,8 +159,9 @@ int ccj_probe(const ccj_table *table, const ccj_probe_args *args, ccj_stream str
  * (chunk c = positions [c*chunk, (c+1)*chunk), empty ones report count 0), out_sel indexes
  * positions inside the chunk, and out_row_map[pos] (positions entries) is the original row of a
  * live position.  Same matches, payloads and per-row multiplicities as ccj_probe (L1 + L2);
- * within a chunk the order is unspecified, so out_round_counts, out_pos and payload columns are
- * not produced (must be NULL / 0). */
+ * within a chunk the order is unspecified, so out_round_counts is not produced (must be NULL).
+ * out_pos (table position of every match) and payload columns (C5: gathered after the walk) are
+ * produced as by ccj_probe, for tables of >= 16 slots. */
 #define CCJ_PART_EXACT 1u
 uint64_t ccj_probe_partitioned_positions(const ccj_table *table, uint64_t n_rows, uint32_t chunk);
 size_t ccj_probe_partitioned_workspace_size(const ccj_table *table, uint64_t n_rows, uint32_t chunk);

@@ -81,3 +81,35 @@ def test_c5_device_built_lp():
     assert len(np.unique(pairs)) == len(pairs)  # each build duplicate gathered once per probe row
     m, _ = O.count_uniform(9, 0, n_probe, n_build, n_build, cf)
     assert len(brow) == m
+
+
+@pytest.mark.parametrize("cf", [1, 2])
+def test_c5_partitioned(cf):
+    """C5 on the slot-partitioned path: the walk records every match's table position and the
+    gather pass materialises the 8 payload columns; every gathered row belongs to a build tuple
+    with the probe row's key, each build tuple once per probe row, and the counts are exact."""
+    n_build, n_probe, chunk = 1 << 18, 1 << 20, 2048
+    bkeys = ref_keys(n_build, cf)
+    pay = payload_rows(n_build)
+    table = ccj.Table.on_device(ccj.LP, torch.from_numpy(bkeys).cuda())
+    table.set_payload(torch.from_numpy(pay.reshape(-1)).cuda(), P)
+    keys = O.uniform_keys(21 + cf, 0, n_probe, n_build + n_build // 8)
+    out = table.probe_partitioned(torch.from_numpy(keys).cuda(), chunk, pos=True, payload_cols=P)
+    torch.cuda.synchronize()
+    assert int(out["status"].item()) == 0
+    nc, cap = out["n_chunks"], out["cap"]
+    cnt = out["count"].cpu().numpy()[:nc].astype(np.int64)
+    valid = (np.arange(cap)[None, :] < cnt[:, None]).reshape(-1)
+    sel = out["sel"].cpu().numpy()[:nc * cap].view(np.uint32)[valid].astype(np.int64)
+    chunk_of = np.repeat(np.arange(nc), cnt)
+    prow = out["row_map"].cpu().numpy().view(np.uint32)[chunk_of * chunk + sel].astype(np.int64)
+    col0 = out["payload_cols"][0].cpu().numpy()[:nc * cap][valid]
+    inv = {int(v): r for r, v in enumerate(pay[:, 0])}
+    brow = np.array([inv[int(v)] for v in col0], np.int64)
+    assert np.array_equal(bkeys[brow], keys[prow])
+    for c in range(1, P):
+        assert np.array_equal(out["payload_cols"][c].cpu().numpy()[:nc * cap][valid], pay[brow, c])
+    pairs = prow * n_build + brow
+    assert len(np.unique(pairs)) == len(pairs)
+    m, _ = O.count_uniform(21 + cf, 0, n_probe, n_build + n_build // 8, n_build, cf)
+    assert len(brow) == m

@@ -178,6 +178,22 @@ def test_partitioned_probe_l1_l2(n_build, cf, n_probe, rng, exact):
         assert np.array_equal(np.sort(rm), np.arange(n_probe, dtype=np.uint32))
 
 
+@pytest.mark.parametrize("variant", ["w2_4a_4", "w1_2u_3", "w1_4u_2", "pair4", "flat"])
+@pytest.mark.parametrize("n_build,cf,n_probe,rng", [(1 << 20, 1, 1 << 22, 1 << 20), (1 << 16, 3, 300000, 1 << 17),
+                                                    (5000, 1, 70000, 20000)])
+def test_partitioned_probe_walk_variants(variant, n_build, cf, n_probe, rng, monkeypatch):
+    """Every form of the partitioned walk (CCJ_PROBE_VARIANT, read per launch: probe_win windows,
+    probe_pair, probe_flat) gives the exact L1 + L2 answer, duplicates (cf 3) and misses included."""
+    monkeypatch.setenv("CCJ_PROBE_VARIANT", variant)
+    table = ccj.Table.reference(ccj.LP, n_build, cf, ccj.LAYOUT_DEVICE)
+    keys = ccj.gen_uniform_keys(n_probe, 17, rng)
+    out = table.probe_partitioned(keys, 2048)
+    torch.cuda.synchronize()
+    assert int(out["status"].item()) == 0
+    m, l2 = ccj.result_checksum(out, 2048, row_map=out["row_map"].to(torch.int64))
+    assert (m, l2) == O.count_uniform(17, 0, n_probe, rng, n_build, cf)
+
+
 @pytest.mark.parametrize("distinct", [1, 7, 3000])
 def test_partitioned_probe_skew_falls_back_to_exact(distinct):
     """Heavy skew overflows the one-pass split's fixed segments: the ABI raises

@@ -12,12 +12,12 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 echo "[profile] kernel trace: bench.py $ARGS"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -f csv -d "$OUT/kt" -o kt -- python3 bench.py $ARGS > "$OUT/kt_bench.log" 2>&1 || exit $?
-for grp in FETCH_SIZE WRITE_SIZE "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" \
-           "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum" "TCC_HIT_sum TCC_MISS_sum" \
+for grp in FETCH_SIZE WRITE_SIZE "TCC_REQ_sum TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" \
+           "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum" \
            "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES" "GRBM_GUI_ACTIVE"; do
   name=$(echo "$grp" | tr ' ' '+')
   echo "[profile] pmc $grp"
-  timeout -k 10 600 rocprofv3 --pmc $grp --kernel-include-regex "${PMC_KERNEL:-probe_chunks}" -T -f csv -d "$OUT/pmc_$name" -o pmc \
-      -- python3 bench.py $ARGS --steps 2 --warmup 1 > "$OUT/pmc_$name.log" 2>&1 || { echo "pmc $grp failed rc=$?"; tail -5 "$OUT/pmc_$name.log"; }
+  timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-include-regex "${PMC_KERNEL:-slot_split_fixed|probe_win}" -T -f csv -d "$OUT/pmc_$name" -o pmc \
+      -- python3 bench.py $ARGS --steps 2 --warmup 1 --no-cpu --no-verify > "$OUT/pmc_$name.log" 2>&1 || { echo "pmc $grp failed rc=$?"; tail -5 "$OUT/pmc_$name.log"; }
 done
 echo "[profile] done"
