@@ -387,10 +387,12 @@ def main():
         keys = ccj.gen_uniform_keys(n_probe, SEED, n_build, first_row=rank * n_probe, stream=stream)
         out = part = out_p = None
         if args.path == "chunk" or not c5:  # C2: both paths (the headline and the one timed beside it)
-            out = table.alloc_outputs(n_probe, chunk, rounds=True, payload_cols=P)
+            out = table.alloc_outputs(n_probe, chunk, rounds=True, payload_cols=P, pos=c5)
         if args.path == "partitioned" or not c5:
             part = table.alloc_partitioned(n_probe, chunk)
-            out_p = table.alloc_outputs(part["positions"], chunk, rounds=False, payload_cols=P)
+            # C5: the match positions the payload gather reads are a caller-owned buffer, so no
+            # allocation runs inside the timed step
+            out_p = table.alloc_outputs(part["positions"], chunk, rounds=False, payload_cols=P, pos=c5)
     stream.synchronize()
     log(f"[setup] table {table.size} slots, max_rounds {table.max_rounds}, keys {n_probe}: "
         f"{time.perf_counter() - t0:.1f} s")
