@@ -462,7 +462,7 @@ struct PartLayout {
 };
 PartLayout part_layout(const ccj_table *t, uint64_t n_rows, uint32_t chunk) {
   PartLayout L{};
-  L.pl = ccj::slot_plan(t->info.size);
+  L.pl = ccj::slot_plan(t->info.size, t->info.kind);
   L.parts = 1u << (L.pl.lo_bits + L.pl.hi_bits);
   if (L.pl.lo_bits == 0 || n_rows == 0 || chunk == 0) {
     L.positions = n_rows;
@@ -493,7 +493,8 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
                           void *ws, size_t ws_bytes, ccj_stream stream) {
   ccj::ProbeParams p;
   if (int rc = fill_probe_params(t, a, p)) return rc;
-  if (t->info.kind != CCJ_TABLE_LP) return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: LP tables only");
+  if (t->info.kind == CCJ_TABLE_CHAIN && (a->out_pos || a->n_payload_cols))
+    return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: positions / payload columns need an LP table");
   if (a->sel || a->counts) return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: sel/counts must be NULL");
   if (a->out_round_counts)
     return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: no round counts (no Next boundaries in partition order)");

@@ -120,7 +120,9 @@ constexpr uint32_t kSplitPartBits = 10;  // at most 1024 partitions (larger tabl
 struct SlotPlan {
   uint32_t window_bits, lo_bits, hi_bits;
 };
-SlotPlan slot_plan(uint64_t table_size);
+// kind: LP windows are 2^kWindowBits slots (8 B each); chaining windows 2^(kWindowBits-1) buckets
+// (16-byte bucket records, plus their chains' keys) — 2 MiB of table either way.
+SlotPlan slot_plan(uint64_t table_size, int kind = CCJ_TABLE_LP);
 size_t slot_partition_workspace(uint64_t n, const SlotPlan &pl);
 hipError_t launch_slot_partition(const int64_t *keys, uint64_t n, const SlotPlan &pl, int64_t *out_keys,
                                  uint32_t *out_rows, void *ws, hipStream_t s);

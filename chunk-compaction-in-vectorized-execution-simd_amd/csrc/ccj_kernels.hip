@@ -1366,12 +1366,163 @@ __global__ __launch_bounds__(kFlatThreads) void probe_win(ProbeParams p) {
   if (p.status && (overflow || total > p.cap)) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
 }
 
+// Chaining walk for bucket-partitioned input (probe_chain_win): one lane per row, R rows in
+// flight, the chunk's rows handed out by an LDS counter as in probe_win.  Round 0 comes from the
+// bucket record {start | len << 32, first key} (one 16-byte load); longer chains continue through
+// aligned 2-key windows of the CSR key array.  After the bucket-range split both the records and
+// the chains of a chunk's window (2^17 buckets) are L2-resident.  Rounds per row = chain length
+// (chaining_ht.cpp:60-136 walks the whole chain); matches = chain entries equal to the key.
+template <int R>
+__global__ __launch_bounds__(kFlatThreads) void probe_chain_win(ProbeParams p) {
+  __shared__ uint32_t s_cnt, s_rounds, s_next;
+  __shared__ int64_t s_key[kMaxChunk];
+  __shared__ uint32_t s_sel[kFlatStage];
+  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1);
+  uint64_t c = blockIdx.x;
+  if (p.xcd_swizzle) {
+    const uint64_t n8 = p.n_chunks & ~7ull;
+    if (c < n8) c = (c & 7) * (n8 >> 3) + (c >> 3);
+  }
+  const uint64_t base = c * p.chunk;
+  const uint32_t phys = flat_phys(p, base);
+  const uint64_t obase = c * p.cap;
+  for (uint32_t i = tid; i < phys; i += kFlatThreads) s_key[i] = __builtin_nontemporal_load(p.keys + base + i);
+  if (tid == 0) {
+    s_cnt = 0;
+    s_rounds = 0;
+    s_next = kFlatThreads * R;
+  }
+  __syncthreads();
+  int64_t key[R];
+  uint32_t row[R], cur[R], lim[R];
+  uint32_t need = 0, fresh = 0, lane_rounds = 0, overflow = 0;  // fresh bit k: at the bucket record
+  auto start = [&](int k, uint32_t i) {
+    row[k] = i;
+    if (i < phys) {
+      key[k] = s_key[i];
+      cur[k] = (uint32_t)murmurhash64((uint64_t)key[k]) & p.mask;
+      need |= 1u << k;
+      fresh |= 1u << k;
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    key[k] = 0;
+    cur[k] = lim[k] = 0;
+    start(k, (uint32_t)k * kFlatThreads + tid);
+  }
+  while (__ballot(need != 0u) != 0ull) {
+    longlong2 v[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      if ((need >> k) & 1u) {
+        v[k] = ((fresh >> k) & 1u) ? p.bucket[cur[k]]
+                                   : *reinterpret_cast<const longlong2 *>(p.table + (cur[k] & ~1u));
+      }
+    }
+    uint32_t hits[R], n = 0, done = 0;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      hits[k] = 0;
+      if ((need >> k) & 1u) {
+        if ((fresh >> k) & 1u) {
+          fresh &= ~(1u << k);
+          const uint32_t st = (uint32_t)v[k].x, len = (uint32_t)((uint64_t)v[k].x >> 32);
+          lane_rounds = len > lane_rounds ? len : lane_rounds;
+          if (len == 0) {
+            done |= 1u << k;  // empty bucket: not in the active set (chaining_ht.cpp:52-55)
+          } else {
+            hits[k] = v[k].y == key[k] ? 1u : 0u;  // round 0 from the record's first key
+            cur[k] = st + 1;
+            lim[k] = st + len;
+            if (len == 1) done |= 1u << k;
+          }
+        } else {
+          const uint32_t blk = cur[k] & ~1u;
+          if (cur[k] == blk && v[k].x == key[k]) hits[k] |= 1u;      // entry blk (not yet walked)
+          if (blk + 1 < lim[k] && v[k].y == key[k]) hits[k] |= 2u;  // entry blk + 1 (inside the chain)
+          cur[k] = blk + 2;
+          if (cur[k] >= lim[k]) done |= 1u << k;
+        }
+      }
+      n += (uint32_t)__builtin_popcount(hits[k]);
+    }
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int b = 0; (1 << b) <= 2 * R; ++b) {
+      const uint64_t bm = __ballot((n >> b) & 1u);
+      pre += lane_prefix(bm) << b;
+      tot += (uint32_t)__popcll(bm) << b;
+    }
+    if (tot) {
+      uint32_t wb = 0;
+      if (lane == 0) wb = atomicAdd(&s_cnt, tot);
+      wb = (uint32_t)__builtin_amdgcn_readfirstlane((int)wb);
+      if (n && !(p.ablate & 1u)) {
+        uint32_t o = wb + pre;
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          for (uint32_t hm = hits[k]; hm; hm &= hm - 1u, ++o) {
+            if (o < kFlatStage) {
+              s_sel[o] = row[k];  // payload = s_key[row]: the matched chain key == probe key
+            } else if (o < p.cap) {
+              p.out_sel[obase + o] = row[k];
+              if (p.out_payload) p.out_payload[obase + o] = key[k];
+            } else {
+              overflow = 1;
+            }
+          }
+        }
+      }
+    }
+    const uint32_t nd = (uint32_t)__builtin_popcount(done);
+    uint32_t dpre = 0, dtot = 0;
+#pragma unroll
+    for (int b = 0; (1 << b) <= R; ++b) {
+      const uint64_t bm = __ballot((nd >> b) & 1u);
+      dpre += lane_prefix(bm) << b;
+      dtot += (uint32_t)__popcll(bm) << b;
+    }
+    if (dtot) {
+      uint32_t rb = 0;
+      if (lane == 0) rb = atomicAdd(&s_next, dtot);
+      rb = (uint32_t)__builtin_amdgcn_readfirstlane((int)rb) + dpre;
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        if ((done >> k) & 1u) {
+          need &= ~(1u << k);
+          start(k, rb++);
+        }
+      }
+    }
+  }
+  {
+    const uint32_t wr = wave_max(lane_rounds);
+    if (lane == 0) atomicMax(&s_rounds, wr);
+  }
+  __syncthreads();
+  const uint32_t total = s_cnt;
+  const uint32_t staged = total < kFlatStage ? total : kFlatStage;
+  if (!(p.ablate & 1u)) {
+    for (uint32_t o = tid; o < staged && o < p.cap; o += kFlatThreads) {
+      __builtin_nontemporal_store(s_sel[o], p.out_sel + obase + o);
+      if (p.out_payload) __builtin_nontemporal_store(s_key[s_sel[o]], p.out_payload + obase + o);
+    }
+  }
+  if (tid == 0) {
+    p.out_count[c] = total < p.cap ? total : (uint32_t)p.cap;
+    if (p.out_rounds) p.out_rounds[c] = s_rounds;
+  }
+  if (p.status && (overflow || total > p.cap)) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
+}
+
 hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
   if (p.n_chunks == 0) return hipSuccess;
   const dim3 g((unsigned)p.n_chunks), b(kFlatThreads);
   const uint64_t size = (uint64_t)p.mask + 1;
   if (kind != CCJ_TABLE_LP) {
-    hipLaunchKernelGGL((probe_pair<CCJ_TABLE_CHAIN, 4>), g, b, 0, s, p);
+    if (p.bucket && !getenv("CCJ_CHAIN_PAIR")) hipLaunchKernelGGL((probe_chain_win<3>), g, b, 0, s, p);
+    else hipLaunchKernelGGL((probe_pair<CCJ_TABLE_CHAIN, 4>), g, b, 0, s, p);
     return hipGetLastError();
   }
   // CCJ_PROBE_VARIANT (tuning override, read per launch): pair4 | flat | wL_Wa_R / wL_Wu_R =

@@ -263,7 +263,7 @@ hipError_t launch_segment_chunk_counts(const uint64_t *counts, uint32_t n_segs, 
 }
 
 // ---- slot-range partitioning for the L2-resident probe ------------------------------------------
-SlotPlan slot_plan(uint64_t table_size) {
+SlotPlan slot_plan(uint64_t table_size, int kind) {
   // CCJ_WINDOW_BITS (tuning override): log2 slots of table per partition.
   static const uint32_t wbits = [] {
     const char *e = getenv("CCJ_WINDOW_BITS");
@@ -271,7 +271,8 @@ SlotPlan slot_plan(uint64_t table_size) {
   }();
   SlotPlan pl{};
   const uint32_t sbits = log2u(table_size);  // table_size is a power of two
-  pl.window_bits = wbits < sbits ? wbits : sbits;
+  const uint32_t wb = kind == CCJ_TABLE_CHAIN && wbits > 0 ? wbits - 1 : wbits;
+  pl.window_bits = wb < sbits ? wb : sbits;
   if (sbits - pl.window_bits > kSplitPartBits) pl.window_bits = sbits - kSplitPartBits;
   const uint32_t dbits = sbits - pl.window_bits;
   pl.lo_bits = (dbits + 1) / 2;  // exact form: two balanced LSD passes of <= 32 digits
