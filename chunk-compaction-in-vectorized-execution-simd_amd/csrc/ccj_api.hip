@@ -459,6 +459,7 @@ struct PartLayout {
   ccj::SlotPlan pl;
   uint32_t parts;
   uint64_t seg_cap, positions;
+  uint64_t ovf_base, ovf_cap;  // overflow area after the segments (runs that do not fit: key skew)
 };
 PartLayout part_layout(const ccj_table *t, uint64_t n_rows, uint32_t chunk) {
   PartLayout L{};
@@ -469,7 +470,9 @@ PartLayout part_layout(const ccj_table *t, uint64_t n_rows, uint32_t chunk) {
     return L;
   }
   L.seg_cap = ccj::slot_seg_cap(n_rows, L.pl, chunk);
-  L.positions = (uint64_t)L.parts * 8 * L.seg_cap;
+  L.ovf_base = (uint64_t)L.parts * 8 * L.seg_cap;
+  L.ovf_cap = (n_rows / 16 + chunk + chunk - 1) / chunk * chunk;  // 1/16 of the rows + one chunk
+  L.positions = L.ovf_base + L.ovf_cap;
   return L;
 }
 uint64_t align256(uint64_t b) { return (b + 255) & ~255ull; }
@@ -484,7 +487,7 @@ size_t ccj_probe_partitioned_workspace_size(const ccj_table *t, uint64_t n_rows,
   if (!t) return 0;
   const PartLayout L = part_layout(t, n_rows, chunk);
   // partitioned keys (positions) + the fixed split's cursors, or the exact split's pass scratch
-  const size_t fixed = align256((uint64_t)L.parts * 8 * 4);
+  const size_t fixed = align256(((uint64_t)L.parts * 8 + 1) * 4);
   const size_t exact = ccj::slot_partition_workspace(n_rows, L.pl);
   return align256(L.positions * 8) + (fixed > exact ? fixed : exact);
 }
@@ -518,12 +521,15 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
     HIP_TRY(ccj::launch_iota_u32(out_row_map, a->n_rows, s), "iota");
   } else if (!exact) {
     uint32_t *cursors = (uint32_t *)rest;
-    HIP_TRY(ccj::launch_slot_split_fixed(a->keys, a->n_rows, L.pl, L.seg_cap, cursors, pkeys, out_row_map, a->status,
+    HIP_TRY(ccj::launch_slot_split_fixed(a->keys, a->n_rows, L.pl, L.seg_cap, L.ovf_base, L.ovf_cap, cursors, pkeys,
+                                         out_row_map, a->status,
                                          s),
             "slot split");
     p.seg_count = cursors;
     p.seg_parts = L.parts;
     p.seg_cap = L.seg_cap;
+    p.ovf_base = L.ovf_base;
+    p.swz_chunks = L.ovf_base / a->chunk;
     p.n_rows = L.positions;
     p.n_chunks = out_chunks;
   } else {

@@ -72,6 +72,11 @@ struct ProbeParams {
   const uint32_t *seg_count;
   uint32_t seg_parts;
   uint64_t seg_cap;
+  // shared overflow area [ovf_base, n_rows): runs that did not fit their segment (key skew);
+  // its fill level is seg_count[seg_parts * 8].  0 = no overflow area.
+  uint64_t ovf_base;
+  uint64_t swz_chunks;   // chunks dealt to XCDs in contiguous ranges (0: all); the overflow area's
+                         // chunks follow in plain order so they do not unbalance the XCDs' shares
   uint32_t xcd_swizzle;  // 1: consecutive chunks go to the same XCD (L2 reuse of partitioned input)
   uint32_t ablate;       // timing-only ablations (CCJ_ABLATE env, never set in product calls)
 };
@@ -129,9 +134,10 @@ hipError_t launch_slot_partition(const int64_t *keys, uint64_t n, const SlotPlan
 // One-pass fixed-capacity form: segment (partition d, XCD group g) = positions [(d*8+g)*cap, +cap);
 // cursors[g*parts + d] = rows that went to it (may exceed cap: CCJ_FLAG_PART_OVERFLOW raised).
 uint64_t slot_seg_cap(uint64_t n, const SlotPlan &pl, uint32_t chunk);
+// cursors[parts * 8] = rows that went to the overflow area [ovf_base, ovf_base + ovf_cap).
 hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPlan &pl, uint64_t cap,
-                                   uint32_t *cursors, int64_t *out_keys, uint32_t *out_rows, uint32_t *status,
-                                   hipStream_t s);
+                                   uint64_t ovf_base, uint64_t ovf_cap, uint32_t *cursors, int64_t *out_keys,
+                                   uint32_t *out_rows, uint32_t *status, hipStream_t s);
 hipError_t launch_partition_fixed(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t row_base, uint64_t seg_cap,
                                   int64_t *out_keys, uint32_t *out_rows, uint64_t *out_counts, uint32_t *status,
                                   void *ws, hipStream_t s);

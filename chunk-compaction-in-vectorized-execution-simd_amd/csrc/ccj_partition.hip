@@ -302,9 +302,11 @@ static_assert(kSplitParts <= (uint32_t)kSplitThreads, "one partition per thread 
 
 __global__ __launch_bounds__(kSplitThreads) void slot_split_fixed(const int64_t *keys, uint64_t n, uint32_t shift,
                                                                  uint32_t parts, uint64_t n_tiles, uint32_t *cur,
-                                                                 uint64_t cap, int64_t *out_k, uint32_t *out_r,
-                                                                 uint32_t *status, uint32_t ablate) {
+                                                                 uint64_t cap, uint64_t ovf_base, uint64_t ovf_cap,
+                                                                 int64_t *out_k, uint32_t *out_r, uint32_t *status,
+                                                                 uint32_t ablate) {
   __shared__ int64_t s_k[kSplitTile];
+  __shared__ uint32_t s_ovf[kSplitParts], s_olim[kSplitParts];  // overflow-area run: start, length
   __shared__ uint16_t s_i[kSplitTile];
   __shared__ uint32_t s_hist[kSplitParts], s_loc[kSplitParts], s_lim[kSplitParts];
   __shared__ uint64_t s_dst[kSplitParts];
@@ -370,7 +372,15 @@ __global__ __launch_bounds__(kSplitThreads) void slot_split_fixed(const int64_t 
       const uint32_t lim = r >= cap ? 0u : (uint32_t)(cap - r < h ? cap - r : h);
       s_dst[tid] = seg * cap + r;
       s_lim[tid] = lim;
-      dropped |= lim < h;
+      uint32_t olim = 0, r2 = 0;
+      if (lim < h) {  // the rest of the run goes to the shared overflow area (key skew)
+        const uint32_t extra = h - lim;
+        r2 = atomicAdd(&cur[(uint64_t)parts * 8], extra);
+        olim = r2 >= ovf_cap ? 0u : (uint32_t)(ovf_cap - r2 < extra ? ovf_cap - r2 : extra);
+        dropped |= olim < extra;
+      }
+      s_ovf[tid] = r2;
+      s_olim[tid] = olim;
     }
     __syncthreads();
     if (tile + bpg < tend) load(tile + bpg);  // next tile's keys arrive while this one is written
@@ -378,8 +388,9 @@ __global__ __launch_bounds__(kSplitThreads) void slot_split_fixed(const int64_t 
       const int64_t k = s_k[q];
       const uint32_t d = (uint32_t)(murmurhash64((uint64_t)k) >> shift) & mask;
       const uint32_t o = q - s_loc[d];
-      if (o < s_lim[d] && !(ablate & 0x10u)) {  // (0x10: timing only, no stores)
-        const uint64_t dest = s_dst[d] + o;
+      const uint32_t lim = s_lim[d];
+      if ((o < lim || o - lim < s_olim[d]) && !(ablate & 0x10u)) {  // (0x10: timing only, no stores)
+        const uint64_t dest = o < lim ? s_dst[d] + o : ovf_base + s_ovf[d] + (o - lim);
         out_k[dest] = k;
         out_r[dest] = (uint32_t)(t0 + s_i[q]);
       }
@@ -400,10 +411,10 @@ uint64_t slot_seg_cap(uint64_t n, const SlotPlan &pl, uint32_t chunk) {
 }
 
 hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPlan &pl, uint64_t cap,
-                                   uint32_t *cursors, int64_t *out_keys, uint32_t *out_rows, uint32_t *status,
-                                   hipStream_t s) {
+                                   uint64_t ovf_base, uint64_t ovf_cap, uint32_t *cursors, int64_t *out_keys,
+                                   uint32_t *out_rows, uint32_t *status, hipStream_t s) {
   const uint32_t parts = 1u << (pl.lo_bits + pl.hi_bits);
-  hipError_t e = hipMemsetAsync(cursors, 0, (size_t)parts * 8 * 4, s);
+  hipError_t e = hipMemsetAsync(cursors, 0, ((size_t)parts * 8 + 1) * 4, s);
   if (e || n == 0) return e;
   const uint64_t n_tiles = (n + kSplitTile - 1) / kSplitTile;
   // one persistent workgroup per CU (140 KB of LDS each), a multiple of 8 (one group per XCD)
@@ -421,7 +432,7 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
     if (v >= 8 && v <= blocks) nb = v;
   }
   hipLaunchKernelGGL(slot_split_fixed, dim3(nb), dim3(kSplitThreads), 0, s, keys, n, pl.window_bits, parts,
-                     n_tiles, cursors, cap, out_keys, out_rows, status, ablate);
+                     n_tiles, cursors, cap, ovf_base, ovf_cap, out_keys, out_rows, status, ablate);
   return hipGetLastError();
 }
 

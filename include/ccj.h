@@ -151,9 +151,10 @@ int ccj_probe(const ccj_table *table, const ccj_probe_args *args, ccj_stream str
  * partition's table window is read from L2 instead of as random HBM lines.
  *
  * The split lays the column out in `positions` slots (ccj_probe_partitioned_positions):
- *   - default: one pass into fixed-capacity segments (partition x XCD group), with gaps; a
- *     segment that overflows (heavy key skew only) drops rows and raises
- *     CCJ_FLAG_PART_OVERFLOW in *args->status (required): re-run with CCJ_PART_EXACT;
+ *   - default: one pass into fixed-capacity segments (partition x XCD group), with gaps, then a
+ *     shared overflow area of n_rows / 16 positions for the runs that do not fit their segment
+ *     (key skew); only when that fills too (extreme skew) are rows dropped and
+ *     CCJ_FLAG_PART_OVERFLOW raised in *args->status (required): re-run with CCJ_PART_EXACT;
  *   - flags & CCJ_PART_EXACT: exact-size two-pass LSD split, no gaps, never overflows.
  * Outputs are ccj_probe's over that layout: args->out_count etc. hold positions / chunk chunks
  * (chunk c = positions [c*chunk, (c+1)*chunk), empty ones report count 0), out_sel indexes
