@@ -626,7 +626,7 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
                        "chunk": chunk, "batches": sp.batches, "parallelism": f"dp{world} (owner-partitioned)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "probe_chunks<LP,2> (local probe of received tuples, rank 0)",
+                         "kernel": "ccj_probe_partitioned (local split + probe_win of received tuples, rank 0)",
                          "kernel_ms": probe_ms, "alg_bytes_per_tuple": alg, "s_bar": s_bar, "m_bar": m_bar},
             "cpu_baseline": None,
             "parity": parity,

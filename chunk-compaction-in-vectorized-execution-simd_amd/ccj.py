@@ -294,12 +294,14 @@ class Table:
                     n_rows=n_rows, chunk=chunk)
 
     def probe_partitioned(self, keys, chunk: int, out=None, part=None, stream=None, exact: bool = False,
-                          retry: bool = True, **alloc_kw):
+                          retry: bool = True, counts=None, **alloc_kw):
         """Slot-range-partitioned probe (ccj_probe_partitioned): L1/L2 results of probe(); out_sel
         indexes the partitioned layout and part["row_map"] maps a live position back to its row.
         The default one-pass split may overflow a segment under heavy key skew
         (FLAG_PART_OVERFLOW); with retry=True that is checked (one stream synchronisation) and the
-        probe re-run with the exact split, as the ABI prescribes."""
+        probe re-run with the exact split, as the ABI prescribes.  counts: live rows per input chunk
+        (fixed-capacity segments, e.g. the multi-GPU exchange's receive buffers); with counts an
+        overflow is left to the caller (the exact split takes no counts)."""
         n = keys.numel()
         if part is None:
             part = self.alloc_partitioned(n, chunk)
@@ -311,12 +313,12 @@ class Table:
         n_chunks = (part["positions"] + chunk - 1) // chunk
         if out["count"].numel() < n_chunks or out["sel"].numel() < n_chunks * out["cap"]:
             raise CCJError("probe output buffers smaller than the partitioned layout needs")
-        a = self._args(keys, chunk, None, None, out)
+        a = self._args(keys, chunk, None, counts, out)
         a.out_round_counts = None  # no Next boundaries in partition order
         flags = PART_EXACT if exact else 0
         check(lib().ccj_probe_partitioned(self._h, C.byref(a), flags, _ptr(part["row_map"]), _ptr(part["ws"]),
                                           part["ws_bytes"], _stream(stream)), "ccj_probe_partitioned")
-        if retry and not exact:
+        if retry and not exact and counts is None:
             import torch
             if stream is not None:
                 stream.synchronize()

@@ -7,8 +7,9 @@ HIP streams (partition, comm, probe) with double-buffered send/receive slots:
      row ids in fixed-capacity segment d, true counts beside them;
   2. all-to-all of counts, keys, rows with equal splits (three all_to_all_single calls on the comm
      stream: the tuple shuffle over xGMI, the only data-path collective; no host round trip);
-  3. local probe of batch i's received segments (ccj_segment_chunk_counts + ccj_probe) while the
-     comm stream moves batch i+1 and the compute stream has partitioned it already;
+  3. local probe of the received segments, GROUP batches at a time (ccj_segment_chunk_counts +
+     ccj_probe_partitioned: the live rows split by home-slot window, then walked with the window
+     L2-resident) while the comm stream moves the next group's batches;
   4. (verification only) all-reduce of match counts and of the order-insensitive L2 checksum.
 12 bytes cross xGMI per tuple (the source rank is implied by the receive segment).  A segment
 that overflows its capacity (skewed keys) is detected on the device; that step is then redone
@@ -22,6 +23,7 @@ the gloo backend on CPU tensors.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.distributed as dist
@@ -33,6 +35,8 @@ import ccj
 # corrupts a one-rank all_to_all_single from 1 GiB up (tools/dbg_a2a.py: the first wrong element
 # sits just past 512 MiB), so every exchange here is cut into batches of at most this size.
 MAX_A2A_BYTES = 384 << 20
+# Received batches probed together (one partitioned probe per group): 4 x 2^25 keys at C4.
+GROUP = int(os.environ.get("CCJ_SHARD_GROUP", "4"))
 
 
 def seg_capacity(n: int, world: int, chunk: int) -> int:
@@ -101,9 +105,12 @@ class ShardedProbe:
         self.n_build_local = own_keys.numel()
         self.table = ccj.Table.on_device(ccj.LP, own_keys, stream=self.stream)
         del own_keys
-        # batched, fixed-capacity exchange buffers (two slots each way)
+        # batched, fixed-capacity exchange buffers: two send slots; receive buffers of `group`
+        # batches each, two of them, so one group is probed while the next one arrives
         self.batches = batch_count(n_probe, world, chunk, batches)
         self.bn = -(-n_probe // self.batches)
+        self.group = min(self.batches, GROUP)
+        self.n_groups = -(-self.batches // self.group)
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self._resize(seg_capacity(self.bn, world, chunk))
         ev = lambda: [torch.cuda.Event() for _ in range(2)]  # noqa: E731
@@ -117,22 +124,36 @@ class ShardedProbe:
         assert seg_cap % self.chunk == 0
         dev = torch.device("cuda", torch.cuda.current_device())
         self.seg_cap = seg_cap
-        slots = self.world * seg_cap
+        slots = self.world * seg_cap  # one batch's receive segments
+        self.slots = slots
+        gslots = self.group * slots
         self.fparts = {}
         mk = lambda dt, n: [torch.zeros(n, dtype=dt, device=dev) for _ in range(2)]  # noqa: E731
         self.sk, self.sr, self.sc = mk(torch.int64, slots), mk(torch.int32, slots), mk(torch.int64, self.world)
-        self.rk, self.rr, self.rc = mk(torch.int64, slots), mk(torch.int32, slots), mk(torch.int64, self.world)
-        self.cc = mk(torch.int32, slots // self.chunk)
-        self.outs = [self.table.alloc_outputs(slots, self.chunk, rounds=False) for _ in range(2)]
+        self.rk, self.rr = mk(torch.int64, gslots), mk(torch.int32, gslots)
+        self.rc = mk(torch.int64, self.group * self.world)
+        self.cc = mk(torch.int32, gslots // self.chunk)
+        # local probe on the slot-partitioned path, one call per group of received batches: the
+        # live rows (per-chunk counts) are split by home-slot window, then walked with the table
+        # window L2-resident; a group of batches makes segments long enough to fill chunks
+        self.parts = [self.table.alloc_partitioned(gslots, self.chunk) for _ in range(2)]
+        self.outs = [self.table.alloc_outputs(p["positions"], self.chunk, rounds=False) for p in self.parts]
 
     def _batch(self, i):
         lo = i * self.bn
         return lo, min(self.bn, self.n_probe - lo)
 
+    def _recv(self, i):
+        """Receive views of batch i: (group slot, keys, rows, counts)."""
+        gs, sub = (i // self.group) % 2, i % self.group
+        lo = sub * self.slots
+        return (gs, self.rk[gs][lo:lo + self.slots], self.rr[gs][lo:lo + self.slots],
+                self.rc[gs][sub * self.world:(sub + 1) * self.world])
+
     # ---- pipelined fixed-capacity step ----
-    # Slot s = i % 2 of every buffer serves batches i, i+2, ...; each reuse waits on the event of
-    # the previous user (events of the previous step included: waiting on an unrecorded event
-    # is a no-op).
+    # Send slot s = i % 2 serves batches i, i+2, ...; receive group slot g % 2 serves groups g, g+2;
+    # each reuse waits on the event of the previous user (events of the previous step included:
+    # waiting on an unrecorded event is a no-op).
     def _partition(self, keys, i):
         s = i % 2
         lo, n = self._batch(i)
@@ -144,39 +165,55 @@ class ShardedProbe:
 
     def _exchange(self, i):
         s = i % 2
+        gs, rk, rr, rc = self._recv(i)
         self.comm.wait_event(self.ev_part[s])
-        self.comm.wait_event(self.ev_probe[s])  # the previous probe of receive slot s is done
+        if i % self.group == 0:
+            self.comm.wait_event(self.ev_probe[gs])  # the previous probe of receive group slot gs is done
         with torch.cuda.stream(self.comm):
-            exchange_fixed(self.sk[s], self.sr[s], self.sc[s], self.rk[s], self.rr[s], self.rc[s])
+            exchange_fixed(self.sk[s], self.sr[s], self.sc[s], rk, rr, rc)
         self.ev_comm[s].record(self.comm)
 
-    def _probe(self, i, timing):
-        s = i % 2
-        self.stream.wait_event(self.ev_comm[s])
-        ccj.segment_chunk_counts(self.rc[s], self.seg_cap, self.chunk, self.cc[s], self.status, stream=self.stream)
+    def _probe(self, g, timing):
+        """Probe group g (batches g*group ... its last one, all exchanged in order on comm)."""
+        gs = g % 2
+        first, last = g * self.group, min((g + 1) * self.group, self.batches) - 1
+        self.stream.wait_event(self.ev_comm[last % 2])
+        per = self.slots // self.chunk
+        for i in range(first, last + 1):
+            sub = i % self.group
+            ccj.segment_chunk_counts(self.rc[gs][sub * self.world:(sub + 1) * self.world], self.seg_cap, self.chunk,
+                                     self.cc[gs][sub * per:(sub + 1) * per], self.status, stream=self.stream)
+        if last - first + 1 < self.group:  # a short last group: its missing batches have no live rows
+            with torch.cuda.stream(self.stream):
+                self.cc[gs][(last - first + 1) * per:].zero_()
         if timing:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(self.stream)
-        self.table.probe(self.rk[s], self.chunk, counts=self.cc[s], out=self.outs[s], stream=self.stream)
+        self.table.probe_partitioned(self.rk[gs], self.chunk, counts=self.cc[gs], out=self.outs[gs],
+                                     part=self.parts[gs], stream=self.stream, retry=False)
         if timing:
             b.record(self.stream)
             self.probe_events.append((a, b))
-        self.ev_probe[s].record(self.stream)
+        self.ev_probe[gs].record(self.stream)
 
-    def row_map(self, i):
-        """Global probe row of every receive slot of batch i (valid until slot i % 2 is reused)."""
-        s = i % 2
-        torch.cuda.current_stream().wait_event(self.ev_comm[s])
-        g = torch.arange(self.world * self.seg_cap, device=self.rr[s].device) // self.seg_cap
-        return g * self.n_probe + self.rr[s].to(torch.int64)
+    def group_row_map(self, g):
+        """Global probe row of every position of group g's partitioned layout (gap positions hold
+        arbitrary values: only matched positions are ever looked up)."""
+        gs = g % 2
+        n = self.group * self.slots
+        with torch.cuda.stream(self.stream):  # behind this group's probe, before the slot's next use
+            q = torch.arange(n, device=self.rr[gs].device) % self.slots
+            recv = (q // self.seg_cap) * self.n_probe + self.rr[gs].to(torch.int64)
+            rm = self.parts[gs]["row_map"].to(torch.int64).clamp_(0, n - 1)
+            return recv[rm]
 
     def received_keys(self, i):
         """Batch i's received keys without the segment padding (work accounting)."""
-        s = i % 2
-        torch.cuda.current_stream().wait_event(self.ev_comm[s])
-        pos = torch.arange(self.world * self.seg_cap, device=self.rk[s].device)
-        live = (pos % self.seg_cap) < self.rc[s][pos // self.seg_cap]
-        return self.rk[s][live]
+        gs, rk, rr, rc = self._recv(i)
+        torch.cuda.current_stream().wait_event(self.ev_comm[i % 2])
+        pos = torch.arange(self.slots, device=rk.device)
+        live = (pos % self.seg_cap) < rc[pos // self.seg_cap]
+        return rk[live]
 
     def step(self, keys, row_base: int = 0, timing: bool = False, verify: bool = False):
         """One pass over this rank's keys.  verify=True returns (matches, l2) of this rank's probes
@@ -192,11 +229,13 @@ class ShardedProbe:
             if i + 1 < self.batches:
                 self._partition(keys, i + 1)
                 self._exchange(i + 1)
-            self._probe(i, timing)
-            if verify:
-                bm, bl = ccj.result_checksum(self.outs[i % 2], self.chunk, row_map=self.row_map(i),
-                                             stream=self.stream)
-                m, l2 = m + bm, (l2 + bl) % (1 << 64)
+            if i % self.group == self.group - 1 or i == self.batches - 1:  # group i // group complete
+                g = i // self.group
+                self._probe(g, timing)
+                if verify:
+                    bm, bl = ccj.result_checksum(self.outs[g % 2], self.chunk, row_map=self.group_row_map(g),
+                                                 stream=self.stream)
+                    m, l2 = m + bm, (l2 + bl) % (1 << 64)
         torch.cuda.current_stream().wait_stream(self.stream)
         torch.cuda.current_stream().wait_stream(self.pstream)
         if int(self.status.item()):  # a fixed-capacity segment overflowed: redo with exact sizes

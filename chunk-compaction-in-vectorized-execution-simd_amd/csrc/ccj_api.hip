@@ -498,7 +498,9 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   if (int rc = fill_probe_params(t, a, p)) return rc;
   if (t->info.kind == CCJ_TABLE_CHAIN && (a->out_pos || a->n_payload_cols))
     return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: positions / payload columns need an LP table");
-  if (a->sel || a->counts) return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: sel/counts must be NULL");
+  if (a->sel) return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: sel must be NULL");
+  if (a->counts && (flags & CCJ_PART_EXACT))
+    return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: input chunk counts need the one-pass split (no CCJ_PART_EXACT)");
   if (a->out_round_counts)
     return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: no round counts (no Next boundaries in partition order)");
   if ((a->out_pos || a->n_payload_cols) && t->info.size < 16)
@@ -522,10 +524,10 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   } else if (!exact) {
     uint32_t *cursors = (uint32_t *)rest;
     HIP_TRY(ccj::launch_slot_split_fixed(a->keys, a->n_rows, L.pl, L.seg_cap, L.ovf_base, L.ovf_cap, cursors, pkeys,
-                                         out_row_map, a->status,
-                                         s),
+                                         out_row_map, a->status, s, a->counts, a->chunk),
             "slot split");
     p.seg_count = cursors;
+    p.counts = nullptr;  // the input's chunk counts were applied by the split
     p.seg_parts = L.parts;
     p.seg_cap = L.seg_cap;
     p.ovf_base = L.ovf_base;
@@ -533,6 +535,7 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
     p.n_rows = L.positions;
     p.n_chunks = out_chunks;
   } else {
+    p.counts = nullptr;
     HIP_TRY(ccj::launch_slot_partition(a->keys, a->n_rows, L.pl, pkeys, out_row_map, rest, s), "slot partition");
     if (out_chunks > p.n_chunks)  // the layout's trailing chunks are empty in the exact form
       HIP_TRY(hipMemsetAsync(a->out_count + p.n_chunks, 0, (out_chunks - p.n_chunks) * 4, s), "count tail");

@@ -447,6 +447,9 @@ __device__ __forceinline__ uint32_t flat_phys(const ProbeParams &p, uint64_t bas
     live = live < p.n_rows - p.ovf_base ? live : p.n_rows - p.ovf_base;
     const uint64_t off = base - p.ovf_base;
     phys = live > off ? (live - off < phys ? (uint32_t)(live - off) : phys) : 0u;
+  } else if (p.counts && !p.seg_count) {  // identity layout of a column with per-chunk live counts
+    const uint32_t cn = p.counts[base / p.chunk];
+    phys = cn < phys ? cn : phys;
   } else if (p.seg_count) {
     const uint64_t seg = base / p.seg_cap;
     const uint64_t off = base - seg * p.seg_cap;

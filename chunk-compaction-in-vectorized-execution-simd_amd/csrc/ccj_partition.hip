@@ -300,17 +300,18 @@ constexpr uint32_t kSplitTile = (uint32_t)kSplitThreads * kSplitPer;
 constexpr uint32_t kSplitParts = 1u << kSplitPartBits;
 static_assert(kSplitParts <= (uint32_t)kSplitThreads, "one partition per thread in the scan");
 
+template <bool COUNTS>
 __global__ __launch_bounds__(kSplitThreads) void slot_split_fixed(const int64_t *keys, uint64_t n, uint32_t shift,
                                                                  uint32_t parts, uint64_t n_tiles, uint32_t *cur,
                                                                  uint64_t cap, uint64_t ovf_base, uint64_t ovf_cap,
                                                                  int64_t *out_k, uint32_t *out_r, uint32_t *status,
-                                                                 uint32_t ablate) {
+                                                                 uint32_t ablate, const uint32_t *counts, uint32_t chunk) {
   __shared__ int64_t s_k[kSplitTile];
   __shared__ uint32_t s_ovf[kSplitParts], s_olim[kSplitParts];  // overflow-area run: start, length
   __shared__ uint16_t s_i[kSplitTile];
   __shared__ uint32_t s_hist[kSplitParts], s_loc[kSplitParts], s_lim[kSplitParts];
   __shared__ uint64_t s_dst[kSplitParts];
-  __shared__ uint32_t s_wsum[kSplitThreads / 64];
+  __shared__ uint32_t s_wsum[kSplitThreads / 64], s_tot;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint32_t g = blockIdx.x & 7u, bpg = gridDim.x >> 3;  // gridDim.x is a multiple of 8
   const uint32_t mask = parts - 1;
@@ -318,29 +319,35 @@ __global__ __launch_bounds__(kSplitThreads) void slot_split_fixed(const int64_t 
   const uint64_t tend = (g + 1) * n_tiles / 8;
   uint64_t tile = g * n_tiles / 8 + (blockIdx.x >> 3);
   int64_t kk[kSplitPer];
+  uint32_t live = 0;  // bit it: row it of this thread is in the column (counts: within its chunk's count)
   auto load = [&](uint64_t t) {
     const uint64_t t0 = t * kSplitTile;
     const uint32_t tn = (uint32_t)(n - t0 < kSplitTile ? n - t0 : kSplitTile);
+    live = 0;
 #pragma unroll
     for (int it = 0; it < kSplitPer; ++it) {
       const uint32_t li = (uint32_t)it * kSplitThreads + tid;
+      bool in = li < tn;
+      if (COUNTS && in) {  // fixed-capacity input segments: chunk c's first counts[c] rows are live
+        const uint32_t pos = (uint32_t)(t0 + li), c = pos / chunk;
+        in = pos - c * chunk < counts[c];
+      }
+      live |= (in ? 1u : 0u) << it;
       if (ablate & 0x20u) kk[it] = (int64_t)((t0 + li) * 0x9E3779B97F4A7C15ull >> 20);  // timing only: no key reads
-      else kk[it] = li < tn ? __builtin_nontemporal_load(keys + t0 + li) : 0;
+      else kk[it] = in ? __builtin_nontemporal_load(keys + t0 + li) : 0;
     }
   };
   if (tile < tend) load(tile);
   bool dropped = false;
   for (; tile < tend; tile += bpg) {
     const uint64_t t0 = tile * kSplitTile;
-    const uint32_t tn = (uint32_t)(n - t0 < kSplitTile ? n - t0 : kSplitTile);
     if (tid < kSplitParts) s_hist[tid] = 0;
     __syncthreads();
     uint32_t dd[kSplitPer], rk[kSplitPer];
 #pragma unroll
     for (int it = 0; it < kSplitPer; ++it) {
-      const uint32_t li = (uint32_t)it * kSplitThreads + tid;
       dd[it] = (uint32_t)(murmurhash64((uint64_t)kk[it]) >> shift) & mask;
-      rk[it] = li < tn ? atomicAdd(&s_hist[dd[it]], 1u) : 0u;
+      rk[it] = (live >> it) & 1u ? atomicAdd(&s_hist[dd[it]], 1u) : 0u;
     }
     __syncthreads();
     // thread tid owns partition tid: block-wide exclusive scan + the segment reservation
@@ -357,11 +364,12 @@ __global__ __launch_bounds__(kSplitThreads) void slot_split_fixed(const int64_t 
     uint32_t wpre = 0;
     for (uint32_t w = 0; w < wave; ++w) wpre += s_wsum[w];
     if (tid < parts) s_loc[tid] = wpre + incl - h;
+    if (tid == kSplitThreads - 1) s_tot = wpre + incl;  // rows in the image (live rows of the tile)
     __syncthreads();
 #pragma unroll
     for (int it = 0; it < kSplitPer; ++it) {
       const uint32_t li = (uint32_t)it * kSplitThreads + tid;
-      if (li < tn) {
+      if ((live >> it) & 1u) {
         const uint32_t pos = s_loc[dd[it]] + rk[it];
         s_k[pos] = kk[it];
         s_i[pos] = (uint16_t)li;
@@ -384,7 +392,8 @@ __global__ __launch_bounds__(kSplitThreads) void slot_split_fixed(const int64_t 
     }
     __syncthreads();
     if (tile + bpg < tend) load(tile + bpg);  // next tile's keys arrive while this one is written
-    for (uint32_t q = tid; q < tn; q += kSplitThreads) {
+    const uint32_t tl = s_tot;  // rows in the image
+    for (uint32_t q = tid; q < tl; q += kSplitThreads) {
       const int64_t k = s_k[q];
       const uint32_t d = (uint32_t)(murmurhash64((uint64_t)k) >> shift) & mask;
       const uint32_t o = q - s_loc[d];
@@ -412,7 +421,8 @@ uint64_t slot_seg_cap(uint64_t n, const SlotPlan &pl, uint32_t chunk) {
 
 hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPlan &pl, uint64_t cap,
                                    uint64_t ovf_base, uint64_t ovf_cap, uint32_t *cursors, int64_t *out_keys,
-                                   uint32_t *out_rows, uint32_t *status, hipStream_t s) {
+                                   uint32_t *out_rows, uint32_t *status, hipStream_t s, const uint32_t *counts,
+                                   uint32_t chunk) {
   const uint32_t parts = 1u << (pl.lo_bits + pl.hi_bits);
   hipError_t e = hipMemsetAsync(cursors, 0, ((size_t)parts * 8 + 1) * 4, s);
   if (e || n == 0) return e;
@@ -431,8 +441,12 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
     const unsigned v = (unsigned)atoi(e) / 8 * 8;
     if (v >= 8 && v <= blocks) nb = v;
   }
-  hipLaunchKernelGGL(slot_split_fixed, dim3(nb), dim3(kSplitThreads), 0, s, keys, n, pl.window_bits, parts,
-                     n_tiles, cursors, cap, ovf_base, ovf_cap, out_keys, out_rows, status, ablate);
+  if (counts)
+    hipLaunchKernelGGL(slot_split_fixed<true>, dim3(nb), dim3(kSplitThreads), 0, s, keys, n, pl.window_bits, parts,
+                       n_tiles, cursors, cap, ovf_base, ovf_cap, out_keys, out_rows, status, ablate, counts, chunk);
+  else
+    hipLaunchKernelGGL(slot_split_fixed<false>, dim3(nb), dim3(kSplitThreads), 0, s, keys, n, pl.window_bits, parts,
+                       n_tiles, cursors, cap, ovf_base, ovf_cap, out_keys, out_rows, status, ablate, counts, chunk);
   return hipGetLastError();
 }
 

@@ -278,3 +278,24 @@ def test_partitioned_chaining_c3_skew():
     assert int(out["status"].item()) == 0
     m, l2 = ccj.result_checksum(out, 2048, row_map=out["row_map"].to(torch.int64))
     assert (m, l2) == O.count_c3(42, 0, n_probe, n_build, 1)
+
+
+@pytest.mark.parametrize("n_build", [1 << 20, 5000])
+def test_partitioned_probe_chunk_counts(n_build):
+    """Segmented input (the multi-GPU receive buffers): only the first counts[c] rows of chunk c
+    are live; the dead rows hold keys that WOULD match and must not be probed."""
+    chunk, n_chunks = 2048, 700
+    rng = np.random.default_rng(5)
+    keys_h = rng.integers(0, n_build, size=n_chunks * chunk).astype(np.int64)  # every key a hit
+    counts_h = rng.integers(0, chunk + 1, size=n_chunks).astype(np.uint32)
+    counts_h[::7] = chunk
+    counts_h[3::11] = 0
+    table = ccj.Table.reference(ccj.LP, n_build, 1, ccj.LAYOUT_DEVICE)
+    counts = torch.from_numpy(counts_h.view(np.int32)).cuda()
+    out = table.probe_partitioned(torch.from_numpy(keys_h).cuda(), chunk, counts=counts)
+    torch.cuda.synchronize()
+    assert int(out["status"].item()) == 0
+    pos = np.arange(n_chunks * chunk)
+    live = (pos % chunk) < counts_h[pos // chunk]
+    want = (int(live.sum()), O.l2_sum(pos[live].astype(np.uint64), keys_h[live]))
+    assert ccj.result_checksum(out, chunk, row_map=out["row_map"].to(torch.int64)) == want
