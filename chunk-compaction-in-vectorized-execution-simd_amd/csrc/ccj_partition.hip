@@ -400,8 +400,8 @@ __global__ __launch_bounds__(kSplitThreads) void slot_split_fixed(const int64_t 
       const uint32_t lim = s_lim[d];
       if ((o < lim || o - lim < s_olim[d]) && !(ablate & 0x10u)) {  // (0x10: timing only, no stores)
         const uint64_t dest = o < lim ? s_dst[d] + o : ovf_base + s_ovf[d] + (o - lim);
-        out_k[dest] = k;
-        out_r[dest] = (uint32_t)(t0 + s_i[q]);
+        out_k[dest] = k;  // plain stores: the L2 merges neighbouring runs' partial lines
+        out_r[dest] = (uint32_t)(t0 + s_i[q]);  // (non-temporal stores measured the same)
       }
     }
     __syncthreads();

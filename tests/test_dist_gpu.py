@@ -129,7 +129,7 @@ def pg1():
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("batches", [1, 3, 4])
+@pytest.mark.parametrize("batches", [1, 3, 4, 20])
 def test_sharded_probe_pipelined_one_rank(pg1, batches):
     import ccj_dist
     n_build, n_probe = 1 << 20, 3 << 20
