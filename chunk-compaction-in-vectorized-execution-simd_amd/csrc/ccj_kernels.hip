@@ -1538,13 +1538,14 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
   }
   // CCJ_PROBE_VARIANT (tuning override, read per launch): pair4 | flat | wL_Wa_R / wL_Wu_R =
   // probe_win<L lanes per row, W-slot windows, aligned (a) or from the next slot (u), R rows>.
-  // At C2 (profiles/r1b_*): w2_4a_4 11.6 ms, w1_2u_3 11.6, w1_4u_2 11.8, pair4 12.1; w1_8a_2
-  // 15.5 and w2_8a_* 12.2 (wider windows cost more L2 requests than they save).
+  // At C2 (profiles/r1e_*): w2_4u_3 10.8 ms (a lane pair reads the 4 slots from the row's next
+  // unread slot: 1.1 windows per row instead of 1.43), w2_4a_4 11.6, w1_2u_3 11.6, w1_4u_2 11.8,
+  // pair4 12.1; w1_8a_2 15.5 and w2_8a_* 12.2 (wider windows cost more L2 time than they save).
   const char *e = getenv("CCJ_PROBE_VARIANT");
-  const std::string v = e && *e ? e : "w2_4a_4";
+  const std::string v = e && *e ? e : "w2_4u_3";
   if (p.out_pos) {  // C5: table positions of the matches for the payload gather (default walk)
     if (size < 16) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((probe_win<2, 4, 4, true, true>), g, b, 0, s, p);
+    hipLaunchKernelGGL((probe_win<2, 4, 3, false, true>), g, b, 0, s, p);
   } else if (size < 16 || v == "pair4") {
     if (size >= 4) hipLaunchKernelGGL((probe_pair<CCJ_TABLE_LP, 4>), dim3((unsigned)p.n_chunks), b, 0, s, p);
     else hipLaunchKernelGGL((probe_flat<CCJ_TABLE_LP, 2>), dim3((unsigned)p.n_chunks), b, 0, s, p);
@@ -1556,9 +1557,12 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
     hipLaunchKernelGGL((probe_win<2, 4, 4, true>), g, b, 0, s, p);
   } else if (v == "w1_4u_2") {
     hipLaunchKernelGGL((probe_win<1, 4, 2, false>), g, b, 0, s, p);
+  } else if (v == "w2_4u_4") {
+    hipLaunchKernelGGL((probe_win<2, 4, 4, false>), g, b, 0, s, p);
+
 
   } else {
-    hipLaunchKernelGGL((probe_win<2, 4, 4, true>), g, b, 0, s, p);  // w2_4a_4
+    hipLaunchKernelGGL((probe_win<2, 4, 3, false>), g, b, 0, s, p);  // w2_4u_3
   }
   return hipGetLastError();
 }
