@@ -542,7 +542,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          # measured DRAM bytes (whole 128-B lines per random slot read) per second
                          "traffic_GBps": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
-                         "kernel": (("ccj_probe_partitioned (slot_split_fixed + probe_win<2,4,3,unaligned>"
+                         "kernel": (("ccj_probe_partitioned (slot_split_fixed + probe_win<2,4,3,next-slot windows>"
                                      + (" with positions + gather_payload_quad)" if c5 else ")"))
                                     if args.path == "partitioned" else "probe_chunks<LP,2>"
                                     + (" + gather_payload_quad" if c5 else "")),

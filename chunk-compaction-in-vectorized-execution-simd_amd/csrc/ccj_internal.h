@@ -120,7 +120,10 @@ hipError_t launch_compact(const ccj_compact_args &a, hipStream_t s);
 size_t partition_workspace(uint64_t n, uint32_t parts);
 // Slot-range partitioning for the L2-resident probe: partition p = slot >> window_bits, with the
 // partition bits split into a low digit (first LSD pass) and a high digit (second pass).
-constexpr uint32_t kWindowBits = 18;    // 2^18 slots = 2 MiB table window per partition
+// 2^19 slots = 4 MiB of LP table per partition (chaining: 2^18 buckets of 16-byte records).  At C2
+// windows of 2 / 4 / 8 MiB measured split + walk 7.1 + 10.5 / 6.3 + 10.7 / 5.8 + 12.0 ms: the
+// split's runs grow with fewer partitions, the walk's L2 reuse shrinks with bigger windows.
+constexpr uint32_t kWindowBits = 19;
 constexpr uint32_t kSplitPartBits = 10;  // at most 1024 partitions (larger tables: larger windows)
 struct SlotPlan {
   uint32_t window_bits, lo_bits, hi_bits;

@@ -1193,7 +1193,7 @@ __global__ __launch_bounds__(kFlatThreads) void probe_pair(ProbeParams p) {
 // bit-sliced over ballots instead of a shuffle scan, and a finished cursor takes the chunk's next
 // unwalked row from an LDS counter (one atomic per wave and step), so every thread stays busy
 // until the chunk's rows run out instead of draining a fixed share.
-template <int LPR, int WS, int R, bool ALIGN, bool POS = false>
+template <int LPR, int WS, int R, bool ALIGN, bool POS = false, int LINE = 0>
 __global__ __launch_bounds__(kFlatThreads) void probe_win(ProbeParams p) {
   constexpr uint32_t kGroups = kFlatThreads / LPR;  // rows walked side by side
   constexpr int kSlotsPerLane = WS / LPR;
@@ -1245,6 +1245,10 @@ __global__ __launch_bounds__(kFlatThreads) void probe_win(ProbeParams p) {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       st[k] = ALIGN ? (cur[k] & ~(uint32_t)(WS - 1)) : (cur[k] < last_start ? cur[k] : last_start);
+      if (!ALIGN && LINE) {  // keep the window inside one LINE-slot line: end it at the boundary
+        const uint32_t lim = (st[k] & ~(uint32_t)(LINE - 1)) + (uint32_t)(LINE - WS);
+        st[k] = st[k] < lim ? st[k] : lim;
+      }
       if ((need >> k) & 1u) {
         const int64_t *w = p.table + st[k] + sub * kSlotsPerLane;
 #pragma unroll
@@ -1538,14 +1542,16 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
   }
   // CCJ_PROBE_VARIANT (tuning override, read per launch): pair4 | flat | wL_Wa_R / wL_Wu_R =
   // probe_win<L lanes per row, W-slot windows, aligned (a) or from the next slot (u), R rows>.
-  // At C2 (profiles/r1e_*): w2_4u_3 10.8 ms (a lane pair reads the 4 slots from the row's next
-  // unread slot: 1.1 windows per row instead of 1.43), w2_4a_4 11.6, w1_2u_3 11.6, w1_4u_2 11.8,
+  // At C2 (profiles/r1e_*): w2_4u_3 10.5-10.8 ms (a lane pair reads the 4 slots from the row's next
+  // unread slot: 1.1 windows per row instead of 1.43), w2_4l_3 1 % less (the same, but a window
+  // that would cross a 128-byte line ends at it: one request; w2_4s_3, 64-byte sectors, 3 % more),
+  // w2_4a_4 11.6, w1_2u_3 11.6, w1_4u_2 11.8,
   // pair4 12.1; w1_8a_2 15.5 and w2_8a_* 12.2 (wider windows cost more L2 time than they save).
   const char *e = getenv("CCJ_PROBE_VARIANT");
-  const std::string v = e && *e ? e : "w2_4u_3";
+  const std::string v = e && *e ? e : "w2_4l_3";
   if (p.out_pos) {  // C5: table positions of the matches for the payload gather (default walk)
     if (size < 16) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((probe_win<2, 4, 3, false, true>), g, b, 0, s, p);
+    hipLaunchKernelGGL((probe_win<2, 4, 3, false, true, 16>), g, b, 0, s, p);
   } else if (size < 16 || v == "pair4") {
     if (size >= 4) hipLaunchKernelGGL((probe_pair<CCJ_TABLE_LP, 4>), dim3((unsigned)p.n_chunks), b, 0, s, p);
     else hipLaunchKernelGGL((probe_flat<CCJ_TABLE_LP, 2>), dim3((unsigned)p.n_chunks), b, 0, s, p);
@@ -1557,12 +1563,16 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
     hipLaunchKernelGGL((probe_win<2, 4, 4, true>), g, b, 0, s, p);
   } else if (v == "w1_4u_2") {
     hipLaunchKernelGGL((probe_win<1, 4, 2, false>), g, b, 0, s, p);
+  } else if (v == "w2_4s_3") {
+    hipLaunchKernelGGL((probe_win<2, 4, 3, false, false, 8>), g, b, 0, s, p);
   } else if (v == "w2_4u_4") {
     hipLaunchKernelGGL((probe_win<2, 4, 4, false>), g, b, 0, s, p);
 
 
+  } else if (v == "w2_4u_3") {
+    hipLaunchKernelGGL((probe_win<2, 4, 3, false>), g, b, 0, s, p);
   } else {
-    hipLaunchKernelGGL((probe_win<2, 4, 3, false>), g, b, 0, s, p);  // w2_4u_3
+    hipLaunchKernelGGL((probe_win<2, 4, 3, false, false, 16>), g, b, 0, s, p);  // w2_4l_3
   }
   return hipGetLastError();
 }

@@ -178,7 +178,7 @@ def test_partitioned_probe_l1_l2(n_build, cf, n_probe, rng, exact):
         assert np.array_equal(np.sort(rm), np.arange(n_probe, dtype=np.uint32))
 
 
-@pytest.mark.parametrize("variant", ["w2_4u_3", "w2_4u_4", "w2_4a_4", "w1_2u_3", "w1_4u_2", "pair4", "flat"])
+@pytest.mark.parametrize("variant", ["w2_4l_3", "w2_4s_3", "w2_4u_3", "w2_4u_4", "w2_4a_4", "w1_2u_3", "w1_4u_2", "pair4", "flat"])
 @pytest.mark.parametrize("n_build,cf,n_probe,rng", [(1 << 20, 1, 1 << 22, 1 << 20), (1 << 16, 3, 300000, 1 << 17),
                                                     (5000, 1, 70000, 20000)])
 def test_partitioned_probe_walk_variants(variant, n_build, cf, n_probe, rng, monkeypatch):

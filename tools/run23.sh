@@ -1,0 +1,9 @@
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/r23; mkdir -p $O
+timeout -k 10 300 python3 -u -m pytest tests/test_probe_gpu.py tests/test_c5_gpu.py -x -q -m gpu -k "partitioned or c5" --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { echo "tests failed $?"; tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+CCJ_WINDOW_BITS=19 timeout -k 10 300 rocprofv3 --kernel-trace -T -f csv -d $O/kt19 -o kt -- python3 tools/sweep_part.py w2_4l_3 > $O/c2_19.log 2>&1 || { echo "c2 failed"; tail $O/c2_19.log; exit 1; }
+grep probe $O/c2_19.log
+python3 tools/trace_split.py $O/kt19 w19
