@@ -1193,27 +1193,16 @@ __global__ __launch_bounds__(kFlatThreads) void probe_pair(ProbeParams p) {
 // bit-sliced over ballots instead of a shuffle scan, and a finished cursor takes the chunk's next
 // unwalked row from an LDS counter (one atomic per wave and step), so every thread stays busy
 // until the chunk's rows run out instead of draining a fixed share.
-template <int LPR, int WS, int R, bool ALIGN, bool POS = false, int LINE = 0>
-__global__ __launch_bounds__(kFlatThreads) void probe_win(ProbeParams p) {
+template <int LPR, int WS, int R, bool ALIGN, bool POS, int LINE>
+__device__ __forceinline__ void walk_chunk(const ProbeParams &p, uint64_t c, uint32_t &s_cnt, uint32_t &s_rounds,
+                                           uint32_t &s_next, int64_t *s_key, uint32_t *s_sel, uint32_t *s_pos) {
   constexpr uint32_t kGroups = kFlatThreads / LPR;  // rows walked side by side
   constexpr int kSlotsPerLane = WS / LPR;
   constexpr int kLoads = kSlotsPerLane / 2;  // 16-byte pieces per lane and window
   static_assert(kLoads >= 1 && WS <= 16 && (LPR == 1 || LPR == 2), "window shape");
-  __shared__ uint32_t s_cnt, s_rounds, s_next;
-  __shared__ int64_t s_key[kMaxChunk];
-  // Matches are staged in LDS and written out coalesced at the end: writing each wave step's range
-  // straight to the output (16 KB of LDS, 8 workgroups per CU instead of 6) measured 14.1-15.0 ms
-  // against 11.5 at C2.
-  __shared__ uint32_t s_sel[kFlatStage];
-  __shared__ uint32_t s_pos[POS ? kFlatStage : 1];  // POS (C5): every match's table position
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1);
   const uint32_t sub = LPR == 1 ? 0u : (tid & 1u), grp = tid / LPR;
   const uint32_t last_start = p.mask - (uint32_t)(WS - 1);  // table size - WS (size >= 16)
-  uint64_t c = blockIdx.x;
-  if (p.xcd_swizzle) {
-    const uint64_t n8 = (p.swz_chunks ? p.swz_chunks : p.n_chunks) & ~7ull;
-    if (c < n8) c = (c & 7) * (n8 >> 3) + (c >> 3);
-  }
   const uint64_t base = c * p.chunk;
   const uint32_t phys = flat_phys(p, base);
   const uint64_t obase = c * p.cap;
@@ -1379,6 +1368,23 @@ __global__ __launch_bounds__(kFlatThreads) void probe_win(ProbeParams p) {
     if (p.out_rounds) p.out_rounds[c] = s_rounds;
   }
   if (p.status && (overflow || total > p.cap)) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
+}
+
+template <int LPR, int WS, int R, bool ALIGN, bool POS = false, int LINE = 0>
+__global__ __launch_bounds__(kFlatThreads) void probe_win(ProbeParams p) {
+  __shared__ uint32_t s_cnt, s_rounds, s_next;
+  __shared__ int64_t s_key[kMaxChunk];
+  // Matches are staged in LDS and written out coalesced at the end: writing each wave step's range
+  // straight to the output (16 KB of LDS, 8 workgroups per CU instead of 6) measured 14.1-15.0 ms
+  // against 11.5 at C2.
+  __shared__ uint32_t s_sel[kFlatStage];
+  __shared__ uint32_t s_pos[POS ? kFlatStage : 1];  // POS (C5): every match's table position
+  uint64_t c = blockIdx.x;
+  if (p.xcd_swizzle) {
+    const uint64_t n8 = (p.swz_chunks ? p.swz_chunks : p.n_chunks) & ~7ull;
+    if (c < n8) c = (c & 7) * (n8 >> 3) + (c >> 3);
+  }
+  walk_chunk<LPR, WS, R, ALIGN, POS, LINE>(p, c, s_cnt, s_rounds, s_next, s_key, s_sel, s_pos);
 }
 
 // Chaining walk for bucket-partitioned input (probe_chain_win): one lane per row, R rows in
@@ -1547,6 +1553,9 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
   // that would cross a 128-byte line ends at it: one request; w2_4s_3, 64-byte sectors, 3 % more),
   // w2_4a_4 11.6, w1_2u_3 11.6, w1_4u_2 11.8,
   // pair4 12.1; w1_8a_2 15.5 and w2_8a_* 12.2 (wider windows cost more L2 time than they save).
+  // A persistent form of w2_4l_3 (4-8 workgroups per CU taking chunks from per-XCD atomic queue
+  // heads, walk_chunk in a loop) measured 11.8 ms against 10.6 (84 VGPRs, occupancy 5): the
+  // one-shot grid's workgroup turnover already hides each chunk's store drain.
   const char *e = getenv("CCJ_PROBE_VARIANT");
   const std::string v = e && *e ? e : "w2_4l_3";
   if (p.out_pos) {  // C5: table positions of the matches for the payload gather (default walk)
@@ -1567,8 +1576,6 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
     hipLaunchKernelGGL((probe_win<2, 4, 3, false, false, 8>), g, b, 0, s, p);
   } else if (v == "w2_4u_4") {
     hipLaunchKernelGGL((probe_win<2, 4, 4, false>), g, b, 0, s, p);
-
-
   } else if (v == "w2_4u_3") {
     hipLaunchKernelGGL((probe_win<2, 4, 3, false>), g, b, 0, s, p);
   } else {
