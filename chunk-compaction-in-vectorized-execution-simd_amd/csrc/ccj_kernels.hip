@@ -437,6 +437,22 @@ constexpr int kFlatThreads = 256;
 constexpr int kFlatRows = kMaxChunk / kFlatThreads;  // 8
 constexpr uint32_t kFlatStage = kMaxChunk;          // matches staged in LDS per chunk
 
+// A chunk's live keys into LDS: every thread issues all of its kFlatRows loads before the first
+// LDS write (a rolled loop waits out one memory latency per load).
+__device__ __forceinline__ void stage_keys(int64_t *s_key, const int64_t *keys, uint32_t phys, uint32_t tid) {
+  int64_t v[kFlatRows];
+#pragma unroll
+  for (int j = 0; j < kFlatRows; ++j) {
+    const uint32_t i = tid + (uint32_t)j * kFlatThreads;
+    v[j] = i < phys ? __builtin_nontemporal_load(keys + i) : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < kFlatRows; ++j) {
+    const uint32_t i = tid + (uint32_t)j * kFlatThreads;
+    if (i < phys) s_key[i] = v[j];
+  }
+}
+
 // Live rows of the flat chunk starting at position `base`: all of them, or with the fixed-capacity
 // split's layout the part of the chunk below its segment's fill level.
 __device__ __forceinline__ uint32_t flat_phys(const ProbeParams &p, uint64_t base) {
@@ -1038,7 +1054,7 @@ __global__ __launch_bounds__(kFlatThreads) void probe_pair(ProbeParams p) {
   const uint64_t base = c * p.chunk;
   const uint32_t phys = flat_phys(p, base);
   const uint64_t obase = c * p.cap;
-  for (uint32_t i = tid; i < phys; i += kFlatThreads) s_key[i] = __builtin_nontemporal_load(p.keys + base + i);
+  stage_keys(s_key, p.keys + base, phys, tid);
   if (tid == 0) {
     s_cnt = 0;
     s_rounds = 0;
@@ -1195,7 +1211,7 @@ __global__ __launch_bounds__(kFlatThreads) void probe_pair(ProbeParams p) {
 // until the chunk's rows run out instead of draining a fixed share.
 template <int LPR, int WS, int R, bool ALIGN, bool POS, int LINE>
 __device__ __forceinline__ void walk_chunk(const ProbeParams &p, uint64_t c, uint32_t &s_cnt, uint32_t &s_rounds,
-                                           uint32_t &s_next, int64_t *s_key, uint32_t *s_sel, uint32_t *s_pos) {
+                                           uint32_t &s_next, int64_t *s_key, uint16_t *s_sel, uint32_t *s_pos) {
   constexpr uint32_t kGroups = kFlatThreads / LPR;  // rows walked side by side
   constexpr int kSlotsPerLane = WS / LPR;
   constexpr int kLoads = kSlotsPerLane / 2;  // 16-byte pieces per lane and window
@@ -1206,7 +1222,7 @@ __device__ __forceinline__ void walk_chunk(const ProbeParams &p, uint64_t c, uin
   const uint64_t base = c * p.chunk;
   const uint32_t phys = flat_phys(p, base);
   const uint64_t obase = c * p.cap;
-  for (uint32_t i = tid; i < phys; i += kFlatThreads) s_key[i] = __builtin_nontemporal_load(p.keys + base + i);
+  stage_keys(s_key, p.keys + base, phys, tid);
   if (tid == 0) {
     s_cnt = 0;
     s_rounds = 0;
@@ -1307,7 +1323,7 @@ __device__ __forceinline__ void walk_chunk(const ProbeParams &p, uint64_t c, uin
         for (int k = 0; k < R; ++k) {
           for (uint32_t hm = hits[k]; hm; hm &= hm - 1u, ++o) {
             if (o < kFlatStage) {
-              s_sel[o] = row[k];  // payload = s_key[row]: the matched table value == probe key
+              s_sel[o] = (uint16_t)row[k];  // payload = s_key[row]: the matched table value == probe key
               if (POS) s_pos[o] = st[k] + (uint32_t)__builtin_ctz(hm);
             } else if (o < p.cap) {
               p.out_sel[obase + o] = row[k];
@@ -1358,8 +1374,9 @@ __device__ __forceinline__ void walk_chunk(const ProbeParams &p, uint64_t c, uin
   const uint32_t staged = total < kFlatStage ? total : kFlatStage;
   if (!(p.ablate & 1u)) {
     for (uint32_t o = tid; o < staged && o < p.cap; o += kFlatThreads) {
-      __builtin_nontemporal_store(s_sel[o], p.out_sel + obase + o);
-      if (p.out_payload) __builtin_nontemporal_store(s_key[s_sel[o]], p.out_payload + obase + o);
+      const uint32_t r = s_sel[o];
+      __builtin_nontemporal_store(r, p.out_sel + obase + o);
+      if (p.out_payload) __builtin_nontemporal_store(s_key[r], p.out_payload + obase + o);
       if (POS) __builtin_nontemporal_store(s_pos[o], p.out_pos + obase + o);
     }
   }
@@ -1377,7 +1394,8 @@ __global__ __launch_bounds__(kFlatThreads) void probe_win(ProbeParams p) {
   // Matches are staged in LDS and written out coalesced at the end: writing each wave step's range
   // straight to the output (16 KB of LDS, 8 workgroups per CU instead of 6) measured 14.1-15.0 ms
   // against 11.5 at C2.
-  __shared__ uint32_t s_sel[kFlatStage];
+  // Chunk rows fit 16 bits: 20 KB of LDS per workgroup, 7 per CU (28 KB and 5 with POS).
+  __shared__ uint16_t s_sel[kFlatStage];
   __shared__ uint32_t s_pos[POS ? kFlatStage : 1];  // POS (C5): every match's table position
   uint64_t c = blockIdx.x;
   if (p.xcd_swizzle) {
@@ -1407,7 +1425,7 @@ __global__ __launch_bounds__(kFlatThreads) void probe_chain_win(ProbeParams p) {
   const uint64_t base = c * p.chunk;
   const uint32_t phys = flat_phys(p, base);
   const uint64_t obase = c * p.cap;
-  for (uint32_t i = tid; i < phys; i += kFlatThreads) s_key[i] = __builtin_nontemporal_load(p.keys + base + i);
+  stage_keys(s_key, p.keys + base, phys, tid);
   if (tid == 0) {
     s_cnt = 0;
     s_rounds = 0;
