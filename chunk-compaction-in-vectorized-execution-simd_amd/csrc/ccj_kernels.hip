@@ -1656,12 +1656,16 @@ __global__ __launch_bounds__(256) void gather_payload(GatherParams g) {
 // 8 columns, 64-byte rows: four lanes share a row, each loading 16 bytes of it, so one wave
 // instruction fetches 16 whole rows (one request per row instead of four); lane q then writes
 // columns 2q and 2q+1 of its row (16 consecutive rows per column per instruction).
-template <int U>
+template <int U, bool NT, bool SWZ>
 __global__ __launch_bounds__(256) void gather_payload_quad(GatherParams g) {
   __shared__ int64_t *s_cols[CCJ_MAX_PAYLOAD_COLS];
   if (threadIdx.x < CCJ_MAX_PAYLOAD_COLS) s_cols[threadIdx.x] = g.cols[threadIdx.x];
   __syncthreads();
-  const uint64_t c = blockIdx.x;
+  uint64_t c = blockIdx.x;
+  if (SWZ) {  // the walk's XCD-swizzled chunk order: each XCD gathers its own range of partitions
+    const uint64_t n8 = (uint64_t)gridDim.x & ~7ull;
+    if (c < n8) c = (c & 7) * (n8 >> 3) + (c >> 3);
+  }
   const uint64_t ob = g.out_base ? g.out_base[c] : c * g.cap;
   const uint32_t n = g.count[c];
   const uint32_t q = threadIdx.x & 3u, r0 = threadIdx.x >> 2;  // 64 rows per block step
@@ -1677,8 +1681,13 @@ __global__ __launch_bounds__(256) void gather_payload_quad(GatherParams g) {
     for (int u = 0; u < U; ++u) {
       const uint32_t j = base + u * 64 + r0;
       if (j < n) {
-        __builtin_nontemporal_store(v[u].x, c0 + ob + j);
-        __builtin_nontemporal_store(v[u].y, c1 + ob + j);
+        if (NT) {
+          __builtin_nontemporal_store(v[u].x, c0 + ob + j);
+          __builtin_nontemporal_store(v[u].y, c1 + ob + j);
+        } else {
+          c0[ob + j] = v[u].x;
+          c1[ob + j] = v[u].y;
+        }
       }
     }
   }
@@ -1688,8 +1697,23 @@ template <int NP>
 hipError_t launch_gather_np(const GatherParams &g, uint64_t n_chunks, hipStream_t s) {
   const bool vec = (g.stride % 2 == 0) && ((uintptr_t)g.pay % 16 == 0);
   static const bool quad = getenv("CCJ_GATHER_SCALAR") == nullptr;
-  if (NP == 8 && vec && quad) hipLaunchKernelGGL((gather_payload_quad<4>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
-  else if (vec) hipLaunchKernelGGL((gather_payload<NP, true>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
+  // tuning override (tools/sweep): CCJ_GATHER_VARIANT = U*100 + plain_stores*10 + swizzle
+  static const int gv = [] {
+    const char *e = getenv("CCJ_GATHER_VARIANT");
+    return e ? atoi(e) : 400;
+  }();
+  const dim3 gd((unsigned)n_chunks), bd(256);
+  if (NP == 8 && vec && quad) {
+    switch (gv) {
+      case 200: hipLaunchKernelGGL((gather_payload_quad<2, true, false>), gd, bd, 0, s, g); break;
+      case 800: hipLaunchKernelGGL((gather_payload_quad<8, true, false>), gd, bd, 0, s, g); break;
+      case 410: hipLaunchKernelGGL((gather_payload_quad<4, false, false>), gd, bd, 0, s, g); break;
+      case 401: hipLaunchKernelGGL((gather_payload_quad<4, true, true>), gd, bd, 0, s, g); break;
+      case 411: hipLaunchKernelGGL((gather_payload_quad<4, false, true>), gd, bd, 0, s, g); break;
+      case 801: hipLaunchKernelGGL((gather_payload_quad<8, true, true>), gd, bd, 0, s, g); break;
+      default: hipLaunchKernelGGL((gather_payload_quad<4, true, false>), gd, bd, 0, s, g); break;
+    }
+  } else if (vec) hipLaunchKernelGGL((gather_payload<NP, true>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
   else hipLaunchKernelGGL((gather_payload<NP, false>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
   return hipGetLastError();
 }

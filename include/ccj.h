@@ -146,7 +146,7 @@ int ccj_probe(const ccj_table *table, const ccj_probe_args *args, ccj_stream str
 
 /* Slot-range-partitioned probe (the throughput path; L1/L2 parity, not L3 order).
  * LP tables only.  The probe column (args->keys, n_rows < 2^32; sel and counts must be NULL) is
- * first split by its home slot's partition (slot >> 18: 2 MiB of table per partition), then
+ * first split by its home slot's partition (slot >> 19: 4 MiB of table per partition, at most 1024 partitions), then
  * probed chunk by chunk like ccj_probe with consecutive chunks kept on one XCD, so each
  * partition's table window is read from L2 instead of as random HBM lines.
  *
