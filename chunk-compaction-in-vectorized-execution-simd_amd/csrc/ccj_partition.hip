@@ -285,7 +285,7 @@ SlotPlan slot_plan(uint64_t table_size, int kind) {
 // Every probe key goes to segment (partition d, tile group g) = position range
 // [(d*8 + g) * cap, (d*8 + g + 1) * cap): g = the XCD the tile's workgroup runs on, so each
 // segment is written from one L2 only.  A persistent workgroup per CU walks its group's tiles
-// (12288 keys); per tile it ranks the keys by partition with LDS atomics, reserves every
+// (11264 keys); per tile it ranks the keys by partition with LDS atomics, reserves every
 // partition's run in its segment with ONE device atomic per partition (group-major cursors, so a
 // wave's 64 reservations are 256 contiguous bytes), builds the tile's image grouped by partition in
 // LDS while those atomics fly, loads the next tile's keys into registers, and writes the runs out.
@@ -295,17 +295,17 @@ SlotPlan slot_plan(uint64_t table_size, int kind) {
 // (only heavy key skew does this; cap leaves 8 standard deviations of room).
 namespace {
 constexpr int kSplitThreads = 1024;
-constexpr int kSplitPer = 12;
+constexpr int kSplitPer = 11;  // CCJ_SPLIT_PER sweep at C2: 8-13 keys -> 6.35 6.12 5.98 5.90 6.34 7.11 ms
 constexpr uint32_t kSplitParts = 1u << kSplitPartBits;
 static_assert(kSplitParts <= (uint32_t)kSplitThreads, "one partition per thread in the scan");
 
-template <bool COUNTS, int THREADS, int MAXP>
+template <bool COUNTS, int THREADS, int MAXP, int PER>
 __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys, uint64_t n, uint32_t shift,
                                                                  uint32_t parts, uint64_t n_tiles, uint32_t *cur,
                                                                  uint64_t cap, uint64_t ovf_base, uint64_t ovf_cap,
                                                                  int64_t *out_k, uint32_t *out_r, uint32_t *status,
                                                                  uint32_t ablate, const uint32_t *counts, uint32_t chunk) {
-  constexpr uint32_t kTileKeys = (uint32_t)THREADS * kSplitPer;
+  constexpr uint32_t kTileKeys = (uint32_t)THREADS * PER;
   static_assert(MAXP <= THREADS, "one partition per thread in the scan");
   __shared__ int64_t s_k[kTileKeys];
   __shared__ uint32_t s_ovf[MAXP], s_olim[MAXP];  // overflow-area run: start, length
@@ -319,14 +319,14 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
   // group g's tiles: [g * n_tiles / 8, (g + 1) * n_tiles / 8); this workgroup takes every bpg-th
   const uint64_t tend = (g + 1) * n_tiles / 8;
   uint64_t tile = g * n_tiles / 8 + (blockIdx.x >> 3);
-  int64_t kk[kSplitPer];
+  int64_t kk[PER];
   uint32_t live = 0;  // bit it: row it of this thread is in the column (counts: within its chunk's count)
   auto load = [&](uint64_t t) {
     const uint64_t t0 = t * kTileKeys;
     const uint32_t tn = (uint32_t)(n - t0 < kTileKeys ? n - t0 : kTileKeys);
     live = 0;
 #pragma unroll
-    for (int it = 0; it < kSplitPer; ++it) {
+    for (int it = 0; it < PER; ++it) {
       const uint32_t li = (uint32_t)it * THREADS + tid;
       bool in = li < tn;
       if (COUNTS && in) {  // fixed-capacity input segments: chunk c's first counts[c] rows are live
@@ -344,9 +344,9 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
     const uint64_t t0 = tile * kTileKeys;
     if (tid < MAXP) s_hist[tid] = 0;
     __syncthreads();
-    uint32_t dd[kSplitPer], rk[kSplitPer];
+    uint32_t dd[PER], rk[PER];
 #pragma unroll
-    for (int it = 0; it < kSplitPer; ++it) {
+    for (int it = 0; it < PER; ++it) {
       dd[it] = (uint32_t)(murmurhash64((uint64_t)kk[it]) >> shift) & mask;
       rk[it] = (live >> it) & 1u ? atomicAdd(&s_hist[dd[it]], 1u) : 0u;
     }
@@ -368,7 +368,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
     if (tid == THREADS - 1) s_tot = wpre + incl;  // rows in the image (live rows of the tile)
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < kSplitPer; ++it) {
+    for (int it = 0; it < PER; ++it) {
       const uint32_t li = (uint32_t)it * THREADS + tid;
       if ((live >> it) & 1u) {
         const uint32_t pos = s_loc[dd[it]] + rk[it];
@@ -427,7 +427,7 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
   const uint32_t parts = 1u << (pl.lo_bits + pl.hi_bits);
   hipError_t e = hipMemsetAsync(cursors, 0, ((size_t)parts * 8 + 1) * 4, s);
   if (e || n == 0) return e;
-  // One persistent 1024-thread workgroup per CU (140 KB of LDS), a multiple of 8 (one tile group
+  // One persistent 1024-thread workgroup per CU (141 KB of LDS), a multiple of 8 (one tile group
   // per XCD).  Two 512-thread workgroups per CU on 6144-key tiles (same run length at 512
   // partitions, phases overlapping between the two) measured 7.8 ms against 6.5 at C2.
   static const unsigned cus = [] {
@@ -438,21 +438,43 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
   }();
   const char *ab = getenv("CCJ_ABLATE");  // timing-only ablations (never set in product calls)
   const uint32_t ablate = ab ? (uint32_t)atoi(ab) : 0u;
-  const uint32_t tile = (uint32_t)kSplitThreads * kSplitPer;
+  // keys per thread per tile: 11 (11264-key tiles, 141 KB of LDS); CCJ_SPLIT_PER = 8 ... 13 is a
+  // tuning override (13: longer runs per partition, 162 KB of the CU's 160 KiB, and slower)
+  uint32_t per = kSplitPer;
+  if (const char *e = getenv("CCJ_SPLIT_PER")) {
+    const uint32_t v = (uint32_t)atoi(e);
+    if (v >= 8 && v <= 13) per = v;
+  }
+  const uint32_t tile = (uint32_t)kSplitThreads * per;
   const uint64_t n_tiles = (n + tile - 1) / tile;
   unsigned nb = cus;
   if (const char *e = getenv("CCJ_SPLIT_BLOCKS")) {  // tuning override: fewer persistent workgroups
     const unsigned v = (unsigned)atoi(e) / 8 * 8;
     if (v >= 8 && v <= nb) nb = v;
   }
-  if (counts)
-    hipLaunchKernelGGL((slot_split_fixed<true, kSplitThreads, kSplitParts>), dim3(nb), dim3(kSplitThreads), 0, s, keys, n,
-                       pl.window_bits, parts, n_tiles, cursors, cap, ovf_base, ovf_cap, out_keys, out_rows, status,
-                       ablate, counts, chunk);
-  else
-    hipLaunchKernelGGL((slot_split_fixed<false, kSplitThreads, kSplitParts>), dim3(nb), dim3(kSplitThreads), 0, s, keys,
-                       n, pl.window_bits, parts, n_tiles, cursors, cap, ovf_base, ovf_cap, out_keys, out_rows, status,
-                       ablate, counts, chunk);
+#define CCJ_SPLIT_LAUNCH(C, P)                                                                                      \
+  hipLaunchKernelGGL((slot_split_fixed<C, kSplitThreads, kSplitParts, P>), dim3(nb), dim3(kSplitThreads), 0, s, keys, n, \
+                     pl.window_bits, parts, n_tiles, cursors, cap, ovf_base, ovf_cap, out_keys, out_rows, status, ablate, \
+                     counts, chunk)
+#define CCJ_SPLIT_PER_CASE(P) \
+  case P:                     \
+    if (counts)               \
+      CCJ_SPLIT_LAUNCH(true, P); \
+    else                      \
+      CCJ_SPLIT_LAUNCH(false, P); \
+    break;
+  switch (per) {
+    CCJ_SPLIT_PER_CASE(8)
+    CCJ_SPLIT_PER_CASE(9)
+    CCJ_SPLIT_PER_CASE(10)
+    CCJ_SPLIT_PER_CASE(12)
+    CCJ_SPLIT_PER_CASE(13)
+    default:
+      if (counts) CCJ_SPLIT_LAUNCH(true, kSplitPer);
+      else CCJ_SPLIT_LAUNCH(false, kSplitPer);
+  }
+#undef CCJ_SPLIT_PER_CASE
+#undef CCJ_SPLIT_LAUNCH
   return hipGetLastError();
 }
 
