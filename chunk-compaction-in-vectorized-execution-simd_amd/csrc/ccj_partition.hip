@@ -299,7 +299,7 @@ constexpr int kSplitPer = 11;  // CCJ_SPLIT_PER sweep at C2: 8-13 keys -> 6.35 6
 constexpr uint32_t kSplitParts = 1u << kSplitPartBits;
 static_assert(kSplitParts <= (uint32_t)kSplitThreads, "one partition per thread in the scan");
 
-template <bool COUNTS, int THREADS, int MAXP, int PER>
+template <bool COUNTS, int THREADS, int MAXP, int PER, bool SD = false>
 __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys, uint64_t n, uint32_t shift,
                                                                  uint32_t parts, uint64_t n_tiles, uint32_t *cur,
                                                                  uint64_t cap, uint64_t ovf_base, uint64_t ovf_cap,
@@ -309,7 +309,8 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
   static_assert(MAXP <= THREADS, "one partition per thread in the scan");
   __shared__ int64_t s_k[kTileKeys];
   __shared__ uint32_t s_ovf[MAXP], s_olim[MAXP];  // overflow-area run: start, length
-  __shared__ uint16_t s_i[kTileKeys];
+  // image row: tile-local row (16 bits), with SD also its partition (bits 16+: no second hash)
+  __shared__ std::conditional_t<SD, uint32_t, uint16_t> s_i[kTileKeys];
   __shared__ uint32_t s_hist[MAXP], s_loc[MAXP], s_lim[MAXP];
   __shared__ uint64_t s_dst[MAXP];
   __shared__ uint32_t s_wsum[THREADS / 64], s_tot;
@@ -373,7 +374,8 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
       if ((live >> it) & 1u) {
         const uint32_t pos = s_loc[dd[it]] + rk[it];
         s_k[pos] = kk[it];
-        s_i[pos] = (uint16_t)li;
+        if constexpr (SD) s_i[pos] = li | dd[it] << 16;
+        else s_i[pos] = (uint16_t)li;
       }
     }
     if (tid < parts) {
@@ -396,13 +398,14 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
     const uint32_t tl = s_tot;  // rows in the image
     for (uint32_t q = tid; q < tl; q += THREADS) {
       const int64_t k = s_k[q];
-      const uint32_t d = (uint32_t)(murmurhash64((uint64_t)k) >> shift) & mask;
+      const uint32_t si = s_i[q];
+      const uint32_t d = SD ? si >> 16 : (uint32_t)(murmurhash64((uint64_t)k) >> shift) & mask;
       const uint32_t o = q - s_loc[d];
       const uint32_t lim = s_lim[d];
       if ((o < lim || o - lim < s_olim[d]) && !(ablate & 0x10u)) {  // (0x10: timing only, no stores)
         const uint64_t dest = o < lim ? s_dst[d] + o : ovf_base + s_ovf[d] + (o - lim);
         out_k[dest] = k;  // plain stores: the L2 merges neighbouring runs' partial lines
-        out_r[dest] = (uint32_t)(t0 + s_i[q]);  // (non-temporal stores measured the same)
+        out_r[dest] = (uint32_t)(t0 + (si & 0xFFFFu));  // (non-temporal stores measured the same)
       }
     }
     __syncthreads();
@@ -456,6 +459,10 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
   hipLaunchKernelGGL((slot_split_fixed<C, kSplitThreads, kSplitParts, P>), dim3(nb), dim3(kSplitThreads), 0, s, keys, n, \
                      pl.window_bits, parts, n_tiles, cursors, cap, ovf_base, ovf_cap, out_keys, out_rows, status, ablate, \
                      counts, chunk)
+#define CCJ_SPLIT_LAUNCH_SD(C, P)                                                                                   \
+  hipLaunchKernelGGL((slot_split_fixed<C, kSplitThreads, kSplitParts, P, true>), dim3(nb), dim3(kSplitThreads), 0, s, keys, \
+                     n, pl.window_bits, parts, n_tiles, cursors, cap, ovf_base, ovf_cap, out_keys, out_rows, status,     \
+                     ablate, counts, chunk)
 #define CCJ_SPLIT_PER_CASE(P) \
   case P:                     \
     if (counts)               \
@@ -463,6 +470,17 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
     else                      \
       CCJ_SPLIT_LAUNCH(false, P); \
     break;
+  const char *sd = getenv("CCJ_SPLIT_SD");  // tuning override: partition kept beside the image row
+  if (sd && atoi(sd) && (per == 9 || per == 10)) {
+    if (per == 9) {
+      if (counts) CCJ_SPLIT_LAUNCH_SD(true, 9);
+      else CCJ_SPLIT_LAUNCH_SD(false, 9);
+    } else {
+      if (counts) CCJ_SPLIT_LAUNCH_SD(true, 10);
+      else CCJ_SPLIT_LAUNCH_SD(false, 10);
+    }
+    return hipGetLastError();
+  }
   switch (per) {
     CCJ_SPLIT_PER_CASE(8)
     CCJ_SPLIT_PER_CASE(9)
@@ -475,6 +493,7 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
   }
 #undef CCJ_SPLIT_PER_CASE
 #undef CCJ_SPLIT_LAUNCH
+#undef CCJ_SPLIT_LAUNCH_SD
   return hipGetLastError();
 }
 
