@@ -386,6 +386,27 @@ int ccj_table_set_payload(ccj_table *t, const int64_t *d_payload, uint32_t n_col
   if (!t || n_cols == 0 || n_cols > CCJ_MAX_PAYLOAD_COLS || (!d_payload && t->info.n_keys))
     return fail(CCJ_ERR_INVALID, "ccj_table_set_payload: bad argument");
   if (!t->d_row) return fail(CCJ_ERR_INVALID, "ccj_table_set_payload: table has no row map");
+  // CCJ_PAY_DENSE=1 (LP): rows stored by rank among the occupied slots (4x smaller at load 1/4), found
+  // through per-32-slot rank words — a tuning override for the C5 gather
+  const char *dense_env = getenv("CCJ_PAY_DENSE");
+  if (dense_env && atoi(dense_env) && t->info.kind == CCJ_TABLE_LP && t->positions < (1ull << 32)) {
+    uint2 *rank = nullptr;
+    if (hipMalloc((void **)&rank, (t->positions + 31) / 32 * sizeof(uint2)) != hipSuccess)
+      return fail(CCJ_ERR_OOM, "payload rank: hipMalloc failed");
+    int64_t *dd = nullptr;
+    uint64_t nd = 0;
+    hipError_t e = ccj::launch_dense_payload(d_payload, n_cols, t->d_row, t->positions, rank, &dd, &nd, (hipStream_t)stream);
+    if (e != hipSuccess) {
+      (void)hipFree(rank);
+      return hip_fail(e, "dense payload");
+    }
+    if (t->d_pay) (void)hipFree(t->d_pay);
+    if (t->d_pay_rank) (void)hipFree(t->d_pay_rank);
+    t->d_pay = dd;
+    t->d_pay_rank = rank;
+    t->n_pay = n_cols;
+    return CCJ_OK;
+  }
   void *d = nullptr;
   if (hipMalloc(&d, t->positions * n_cols * sizeof(int64_t)) != hipSuccess)
     return fail(CCJ_ERR_OOM, "payload: hipMalloc failed");
@@ -397,6 +418,8 @@ int ccj_table_set_payload(ccj_table *t, const int64_t *d_payload, uint32_t n_col
     return hip_fail(e, "payload scatter");
   }
   if (t->d_pay) (void)hipFree(t->d_pay);
+  if (t->d_pay_rank) (void)hipFree(t->d_pay_rank);
+  t->d_pay_rank = nullptr;
   t->d_pay = (int64_t *)d;
   t->n_pay = n_cols;
   return CCJ_OK;
@@ -409,6 +432,7 @@ int ccj_table_free(ccj_table *t) {
   if (t->d_bucket) (void)hipFree(t->d_bucket);
   if (t->d_row) (void)hipFree(t->d_row);
   if (t->d_pay) (void)hipFree(t->d_pay);
+  if (t->d_pay_rank) (void)hipFree(t->d_pay_rank);
   delete t;
   return CCJ_OK;
 }
@@ -442,6 +466,7 @@ int fill_probe_params(const ccj_table *t, const ccj_probe_args *a, ccj::ProbePar
   p.out_pos = a->out_pos;
   if (a->n_payload_cols > t->n_pay) return fail(CCJ_ERR_INVALID, "ccj_probe: table has fewer payload columns");
   p.pay = t->d_pay;
+  p.pay_rank = t->d_pay_rank;
   p.n_pay = a->n_payload_cols;
   p.pay_stride = t->n_pay;
   for (uint32_t c = 0; c < a->n_payload_cols; ++c) {

@@ -16,6 +16,7 @@ struct ccj_table {
   uint32_t *d_row = nullptr;    // table position -> build tuple index (LP: kNoRow for empty slots)
   uint64_t positions = 0;       // allocated positions (LP slots / chain keys, padded)
   int64_t *d_pay = nullptr;     // position-major payload rows [positions][n_pay]
+  uint2 *d_pay_rank = nullptr;  // dense payload (LP, CCJ_PAY_DENSE=1): per 32 positions {occupied bits, occupied before}
   uint32_t n_pay = 0;
   int device = 0;
 };
@@ -60,6 +61,7 @@ struct ProbeParams {
   uint32_t *status;
   uint32_t *out_pos;
   const int64_t *pay;  // position-major payload rows
+  const uint2 *pay_rank;  // non-null: payload rows are dense, row of position p = rank of p among occupied
   uint32_t n_pay;      // payload columns gathered (<= CCJ_MAX_PAYLOAD_COLS)
   uint32_t pay_stride; // payload columns stored per position
   int64_t *out_cols[CCJ_MAX_PAYLOAD_COLS];
@@ -93,6 +95,8 @@ hipError_t launch_fill(int64_t *p, uint64_t n, int64_t v, hipStream_t s);
 hipError_t launch_iota_u32(uint32_t *p, uint64_t n, hipStream_t s);
 hipError_t launch_lp_insert(const int64_t *keys, uint64_t n, int64_t *slots, uint32_t *slot_row, uint32_t mask,
                             hipStream_t s);
+hipError_t launch_dense_payload(const int64_t *src, uint32_t n_cols, const uint32_t *row, uint64_t positions,
+                                uint2 *rank, int64_t **dst, uint64_t *n_dense, hipStream_t s);
 hipError_t launch_scatter_payload(const int64_t *src, uint32_t n_cols, const uint32_t *row, uint64_t positions,
                                   int64_t *dst, hipStream_t s);
 // Per-segment run statistics of an LP slot array (segment = 4096 slots): 4 x uint32 per segment:

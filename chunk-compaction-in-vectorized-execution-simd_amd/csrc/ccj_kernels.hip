@@ -11,6 +11,7 @@
 // Emission order is round-major, idx ascending within a round: exactly the reference's
 // result_vector order (L3).  Per-row state lives in VGPRs (key, slot/chain position, chain end);
 // active/match sets are bitmasks over the lane's R rows.
+#include <hipcub/hipcub.hpp>
 #include <cstdlib>
 #include <string>
 
@@ -23,6 +24,14 @@ __device__ __forceinline__ uint32_t lane_prefix(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// Payload row of table position pos: the position itself, or with a dense payload its rank among
+// the occupied positions (one 8-byte read of the position's 32-position rank word).
+__device__ __forceinline__ uint64_t pay_index(const uint2 *rank, uint32_t pos) {
+  if (!rank) return pos;
+  const uint2 w = rank[pos >> 5];
+  return (uint64_t)w.y + (uint32_t)__popc(w.x & ((1u << (pos & 31u)) - 1u));
+}
+
 // Table position of row key k's candidate in round r (LP: home + r; chain: chain start + r) and
 // the wide-payload gather (C5) for a match written at output slot o.
 template <int KIND>
@@ -32,7 +41,7 @@ __device__ __forceinline__ void emit_extra(const ProbeParams &p, uint64_t obase,
   const uint32_t pos = KIND == CCJ_TABLE_LP ? ((h + r) & p.mask) : p.off[h] + r;
   if (p.out_pos) p.out_pos[obase + o] = pos;
   if (p.n_pay) {
-    const int64_t *row = p.pay + (uint64_t)pos * p.pay_stride;
+    const int64_t *row = p.pay + pay_index(p.pay_rank, pos) * p.pay_stride;
     for (uint32_t c = 0; c < p.n_pay; ++c) p.out_cols[c][obase + o] = row[c];
   }
 }
@@ -1612,6 +1621,7 @@ struct GatherParams {
   const uint64_t *out_base;
   uint64_t cap;
   const int64_t *pay;
+  const uint2 *rank;  // dense payload (ProbeParams::pay_rank)
   uint32_t stride;
   int64_t *cols[CCJ_MAX_PAYLOAD_COLS];
 };
@@ -1627,7 +1637,7 @@ __global__ __launch_bounds__(256) void gather_payload(GatherParams g) {
     for (int u = 0; u < 2; ++u) {
       const uint32_t j = j0 + u * 256;
       if (j < n) {
-        const int64_t *row = g.pay + (uint64_t)g.pos[ob + j] * g.stride;
+        const int64_t *row = g.pay + pay_index(g.rank, g.pos[ob + j]) * g.stride;
         if (VEC) {
 #pragma unroll
           for (int q = 0; q + 1 < NP; q += 2) {
@@ -1675,7 +1685,7 @@ __global__ __launch_bounds__(256) void gather_payload_quad(GatherParams g) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t j = base + u * 64 + r0;
-      if (j < n) v[u] = reinterpret_cast<const longlong2 *>(g.pay + (uint64_t)g.pos[ob + j] * g.stride)[q];
+      if (j < n) v[u] = reinterpret_cast<const longlong2 *>(g.pay + pay_index(g.rank, g.pos[ob + j]) * g.stride)[q];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1726,6 +1736,7 @@ hipError_t launch_gather_payload(const ProbeParams &p, const uint32_t *pos, hipS
   g.out_base = p.out_base;
   g.cap = p.cap;
   g.pay = p.pay;
+  g.rank = p.pay_rank;
   g.stride = p.pay_stride;
   for (uint32_t q = 0; q < p.n_pay; ++q) g.cols[q] = p.out_cols[q];
   switch (p.n_pay) {
@@ -1775,6 +1786,72 @@ hipError_t launch_lp_insert(const int64_t *keys, uint64_t n, int64_t *slots, uin
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(lp_insert, dim3(grid_for(n, 256)), dim3(256), 0, s, keys, n, slots, slot_row, mask);
   return hipGetLastError();
+}
+
+// Dense payload (CCJ_PAY_DENSE): rank words over the table positions, then build rows stored by rank.
+__global__ void pay_rank_words(const uint32_t *row, uint64_t positions, uint2 *rank, uint32_t *cnt, uint64_t n_words) {
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < n_words; w += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t bits = 0;
+    for (uint32_t i = 0; i < 32; ++i) {
+      const uint64_t pos = w * 32 + i;
+      if (pos < positions && row[pos] != kNoRow) bits |= 1u << i;
+    }
+    rank[w].x = bits;
+    cnt[w] = (uint32_t)__popc(bits);
+  }
+}
+
+__global__ void pay_rank_fill(uint2 *rank, const uint32_t *pre, uint64_t n_words) {
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < n_words; w += (uint64_t)gridDim.x * blockDim.x)
+    rank[w].y = pre[w];
+}
+
+__global__ void scatter_payload_dense(const int64_t *src, uint32_t n_cols, const uint32_t *row, uint64_t positions,
+                                      const uint2 *rank, int64_t *dst) {
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < positions * n_cols;
+       t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t pos = t / n_cols, c = t - pos * n_cols;
+    const uint32_t r = row[pos];
+    if (r != kNoRow) dst[pay_index(rank, (uint32_t)pos) * n_cols + c] = src[(uint64_t)r * n_cols + c];
+  }
+}
+
+hipError_t launch_dense_payload(const int64_t *src, uint32_t n_cols, const uint32_t *row, uint64_t positions,
+                                uint2 *rank, int64_t **dst, uint64_t *n_dense, hipStream_t s) {
+  *dst = nullptr;
+  *n_dense = 0;
+  const uint64_t n_words = (positions + 31) / 32;
+  if (n_words == 0) return hipSuccess;
+  uint32_t *cnt = nullptr, *pre = nullptr;
+  void *tmp = nullptr;
+  size_t tmp_bytes = 0;
+  hipError_t e = hipMalloc(&cnt, n_words * 4 * 2);
+  if (e) return e;
+  pre = cnt + n_words;
+  hipLaunchKernelGGL(pay_rank_words, dim3(grid_for(n_words, 256)), dim3(256), 0, s, row, positions, rank, cnt, n_words);
+  e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, pre, (int)n_words, s);
+  if (!e) e = hipMalloc(&tmp, tmp_bytes);
+  if (!e) e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, pre, (int)n_words, s);
+  if (!e) hipLaunchKernelGGL(pay_rank_fill, dim3(grid_for(n_words, 256)), dim3(256), 0, s, rank, pre, n_words);
+  uint32_t last[2] = {0, 0};
+  if (!e) e = hipMemcpyAsync(&last[0], pre + n_words - 1, 4, hipMemcpyDeviceToHost, s);
+  if (!e) e = hipMemcpyAsync(&last[1], cnt + n_words - 1, 4, hipMemcpyDeviceToHost, s);
+  if (!e) e = hipStreamSynchronize(s);
+  const uint64_t total = (uint64_t)last[0] + last[1];
+  if (!e && total) e = hipMalloc((void **)dst, total * n_cols * sizeof(int64_t));
+  if (!e && total)
+    hipLaunchKernelGGL(scatter_payload_dense, dim3(grid_for(positions * n_cols, 256)), dim3(256), 0, s, src, n_cols, row,
+                       positions, rank, *dst);
+  if (!e) e = hipGetLastError();
+  if (!e) e = hipStreamSynchronize(s);
+  (void)hipFree(tmp);
+  (void)hipFree(cnt);
+  if (e && *dst) {
+    (void)hipFree(*dst);
+    *dst = nullptr;
+  }
+  *n_dense = e ? 0 : total;
+  return e;
 }
 
 hipError_t launch_scatter_payload(const int64_t *src, uint32_t n_cols, const uint32_t *row, uint64_t positions,
