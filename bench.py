@@ -35,6 +35,7 @@ PKG = os.path.join(ROOT, "chunk-compaction-in-vectorized-execution-simd_amd")
 sys.path.insert(0, PKG)
 sys.path.insert(0, ROOT)
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import ccj  # noqa: E402
@@ -76,7 +77,12 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-sample", type=int, default=1 << 28, help="probe keys in the multi-thread CPU sample")
     ap.add_argument("--no-verify", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--lib", default="product", choices=["product", "tuning"],
+                    help="tuning: libccj_tuning.so (make tuning; A/B sweeps with its env overrides)")
+    a = ap.parse_args()
+    if a.lib == "tuning":
+        ccj.LIB_PATH = os.path.join(PKG, "libccj_tuning.so")
+    return a
 
 
 def cpu_model():
@@ -202,7 +208,7 @@ def bench_c3(args, dev, stream):
             table.probe(keys, chunk, out=out, stream=stream)
         if ev:
             ev[1].record(stream)
-        comp = ccj.compact(out, chunk, cols=[pkeys if part_mode else keys], rows=False, stream=stream)
+        comp = ccj.compact(out, chunk, cols=[pkeys if part_mode else keys], rows=True, stream=stream)
         if ev:
             ev[2].record(stream)
 
@@ -225,10 +231,26 @@ def bench_c3(args, dev, stream):
         matches, l2 = ccj.result_checksum(out, chunk, row_map=part["row_map"].to(torch.int64), stream=stream)
     else:
         matches, l2 = ccj.result_checksum(out, chunk, stream=stream)
-    n_comp = int(comp["counts"][:int(comp["n"].item())].to(torch.int64).sum().item())
+    # the compacted chunks themselves: every (row, payload) pair and the carried key column
+    torch.cuda.synchronize()
+    n_oc = int(comp["n"].item())
+    cnt = comp["counts"][:n_oc].to(torch.int64)
+    valid = (torch.arange(chunk, device=cnt.device)[None, :] < cnt[:, None]).reshape(-1)
+    idx = torch.nonzero(valid).squeeze(1)
+    c_rows, c_pay, c_key = comp["row"][idx], comp["payload"][idx], comp["cols"][0][idx]
+    if part_mode:
+        c_rows = part["row_map"].to(torch.int64)[c_rows]
+    n_comp = int(idx.numel())
+    key_ok = bool(torch.equal(c_key, c_pay))  # the carried key column == the matched key
+    comp_l2 = None
+    if not args.no_verify:  # checker only (the oracle's L2 term), untimed
+        from oracle import oracle as O
+        comp_l2 = O.l2_sum(c_rows.cpu().numpy().astype(np.uint64), c_pay.cpu().numpy())
+    del c_rows, c_pay, c_key, idx, valid
     examined, _ = table.probe_cost(keys, stream=stream)
     parity = {"status_flags": int(out["status"].item()) | int(comp["status"].item()), "matches": matches,
-              "l2": hex(l2), "compacted_rows": n_comp, "compaction_keeps_all": n_comp == matches}
+              "l2": hex(l2), "compacted_rows": n_comp, "compacted_l2": None if comp_l2 is None else hex(comp_l2),
+              "compaction_keeps_all": n_comp == matches and key_ok and comp_l2 in (None, l2)}
     cpu = None
     if not args.no_verify or not args.no_cpu:
         from oracle import oracle as O
@@ -255,7 +277,7 @@ def bench_c3(args, dev, stream):
         "metric": METRIC, "value": n_probe / (wall / args.steps), "unit": "probe tuples/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall * 1e3 / args.steps,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
-        "data": "synthetic (reference key generator build side; C3 stream: ~10 % Zipf-skewed hits, seed 42)",
+        "data": "synthetic (reference key generator build side; C3 stream: 10 % hits, Zipf s = 1 over the 2^26 build ranks (2^16-bucket inverse CDF), seed 42)",
         "config": {"workload": "C3: 1xMI355X chaining_ht + compactor, Zipf-skewed keys, ~10% match rate, "
                                f"{n_build} build / {n_probe} probe, chunk={chunk}", "parallelism": "dp1"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -585,6 +607,7 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
     dist.barrier()
     torch.cuda.synchronize()
     sp.probe_events.clear()
+    exact_before = sp.exact_steps
     t0 = time.perf_counter()
     for _ in range(args.steps):
         sp.step(keys, rank * n_probe, timing=True)
@@ -594,8 +617,13 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
     t = torch.tensor([wall], device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall = float(t.item())
-    probe_ms = sum(a.elapsed_time(b) for a, b in sp.probe_events) / args.steps
-    exact_fallback = sp.last_exact
+    # local probe time per step: the slowest rank's (the roofline's kernel time)
+    pm = torch.tensor([sum(a.elapsed_time(b) for a, b in sp.probe_events) / args.steps], device=dev)
+    dist.all_reduce(pm, op=dist.ReduceOp.MAX)
+    probe_ms = float(pm.item())
+    # timed steps redone with the exact-size protocol (every rank takes the same branch: the status
+    # word is all-reduced before it, so this count is the same on all ranks)
+    exact_fallback = sp.exact_steps - exact_before
     # verification (untimed): global L1 / L2 against the exact membership answer
     m, l2 = sp.step(keys, rank * n_probe, verify=True)
     rk = sp.received_keys(sp.batches - 1)
@@ -604,7 +632,7 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
     tot = torch.tensor([m, l2 - (1 << 64) if l2 >= (1 << 63) else l2], dtype=torch.int64, device=dev)
     dist.all_reduce(tot)
     m_all, l2_all = int(tot[0].item()), int(tot[1].item()) % (1 << 64)
-    parity = {"matches": m_all, "l2": hex(l2_all), "exact_size_fallback": exact_fallback}
+    parity = {"matches": m_all, "l2": hex(l2_all), "exact_size_fallback_steps": exact_fallback}
     if not args.no_verify and rank == 0:
         from oracle import oracle as O
         want_m, want_l2 = O.count_uniform(SEED, 0, world * n_probe, n_build_total, n_build_total, 1,
@@ -626,7 +654,7 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
                        "chunk": chunk, "batches": sp.batches, "parallelism": f"dp{world} (owner-partitioned)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "ccj_probe_partitioned (local split + probe_win of received tuples, rank 0)",
+                         "kernel": "ccj_probe_partitioned (local split + walk of received tuples, slowest rank)",
                          "kernel_ms": probe_ms, "alg_bytes_per_tuple": alg, "s_bar": s_bar, "m_bar": m_bar},
             "cpu_baseline": None,
             "parity": parity,

@@ -11,33 +11,36 @@ HIP streams (partition, comm, probe) with double-buffered send/receive slots:
      ccj_probe_partitioned: the live rows split by home-slot window, then walked with the window
      L2-resident) while the comm stream moves the next group's batches;
   4. (verification only) all-reduce of match counts and of the order-insensitive L2 checksum.
-12 bytes cross xGMI per tuple (the source rank is implied by the receive segment).  A segment
-that overflows its capacity (skewed keys) is detected on the device; that step is then redone
-with the exact-size protocol (exchange(): host-side split sizes, 16 B per tuple).
-The build side is sharded the same way once, before timing: every rank keeps the reference
-generator's keys it owns and builds its local table on the device.
+12 bytes cross xGMI per tuple (the source rank is implied by the receive segment).
 
-The exchange helpers are backend-agnostic, so tests/test_dist_cpu.py drives the same protocol with
-the gloo backend on CPU tensors.
+Overflow.  Three things can overflow under key skew, each raising a flag in the rank's status
+word: a send segment of the owner split, a receive segment's count, and the local probe's own
+one-pass slot split or output capacity (its args->status IS the same word).  At the end of a step
+the word is all-reduced with MAX, so every rank sees the same value and takes the same branch:
+either all return, or all redo the step with the exact-size protocol (exchange(): host-side split
+sizes, 16 B per tuple) — the ranks' collective sequences never diverge.
+
+The step's control flow is written against an `ops` object: DeviceOps (below) runs the HIP kernels
+on torch.cuda streams; tests/test_dist_cpu.py drives the SAME ShardedProbe with gloo on CPU
+tensors and an oracle-backed ops object (batching, receive-group slots, group_row_map, the
+overflow fallback on one rank only).
 """
 from __future__ import annotations
 
+import contextlib
 import math
-import os
 
 import torch
 import torch.distributed as dist
 
-import ccj
-
 
 # Largest buffer one all_to_all_single moves.  The RCCL in this image's torch wheel (2.26.6)
-# corrupts a one-rank all_to_all_single from 1 GiB up (tools/dbg_a2a.py: the first wrong element
-# sits just past 512 MiB), so every exchange here is cut into batches of at most this size.
+# corrupts a one-rank all_to_all_single from 1 GiB up (the first wrong element sits just past
+# 512 MiB), so every exchange here is cut into batches of at most this size.
 MAX_A2A_BYTES = 384 << 20
 # Received batches probed together (one partitioned probe per group): 8 x 2^25 keys at C4.
 # One-rank rehearsal, local probe per step: groups of 2 / 4 / 8 batches 30.6 / 25.6 / 23.9 ms.
-GROUP = int(os.environ.get("CCJ_SHARD_GROUP", "8"))
+GROUP = 8
 
 
 def seg_capacity(n: int, world: int, chunk: int) -> int:
@@ -79,66 +82,151 @@ def exchange(send_keys, send_rows, send_counts, group=None):
     return recv_keys, recv_rows, rc
 
 
-class ShardedProbe:
-    """One rank's part of the multi-GPU probe of the C4 configuration."""
+def agree_status(status, group=None) -> int:
+    """MAX of every rank's status word: the one value all ranks branch on."""
+    st = status.to(torch.int64) if status.dtype != torch.int64 else status.clone()
+    dist.all_reduce(st, op=dist.ReduceOp.MAX, group=group)
+    return int(st.item())
 
-    def __init__(self, n_build_total: int, cf: int, n_probe: int, chunk: int, world: int, rank: int,
-                 stream=None, batches: int = 4):
-        self.world, self.rank, self.chunk, self.n_probe = world, rank, chunk, n_probe
-        dev = torch.device("cuda", torch.cuda.current_device())
-        self.stream = stream or torch.cuda.Stream(device=dev)
-        self.comm = torch.cuda.Stream(device=dev)
-        self.pstream = torch.cuda.Stream(device=dev)  # partitions run beside the previous probe
-        # build side: reference generator keys (linear_probing_ht.cpp:14-25) of the whole table,
-        # generated in slices, each slice split by owner; this rank keeps its own part.
+
+class DeviceOps:
+    """The HIP kernels (libccj.so) and torch.cuda streams/events one rank's step runs on."""
+
+    def __init__(self):
+        import ccj
+        self.ccj = ccj
+        self.device = torch.device("cuda", torch.cuda.current_device())
+
+    # streams and events
+    def stream(self):
+        return torch.cuda.Stream(device=self.device)
+
+    def event(self, timing=False):
+        return torch.cuda.Event(enable_timing=timing)
+
+    def current(self):
+        return torch.cuda.current_stream()
+
+    def on(self, stream):
+        return torch.cuda.stream(stream)
+
+    def synchronize(self):
+        torch.cuda.synchronize()
+
+    # buffers
+    def zeros(self, n, dtype):
+        return torch.zeros(n, dtype=dtype, device=self.device)
+
+    # build side: this rank's part of the reference generator's keys, built into a local LP table
+    def build_local(self, n_build_total, cf, world, rank, stream):
+        ccj = self.ccj
         own = []
         step = 1 << 26
         for b in range(0, n_build_total, step):
             n = min(step, n_build_total - b)
-            keys = ccj.gen_reference_keys(b, n, n_build_total, cf, stream=self.stream)
-            part = ccj.OwnerPartitioner(n, world, device=dev)
-            k, _, cnt = part(keys, 0, stream=self.stream)
+            keys = ccj.gen_reference_keys(b, n, n_build_total, cf, stream=stream)
+            part = ccj.OwnerPartitioner(n, world, device=self.device)
+            k, _, cnt = part(keys, 0, stream=stream)
             torch.cuda.synchronize()
             c = cnt.tolist()
             lo = sum(c[:rank])
             own.append(k[lo:lo + c[rank]].clone())
-        own_keys = torch.cat(own) if own else torch.empty(0, dtype=torch.int64, device=dev)
-        self.n_build_local = own_keys.numel()
-        self.table = ccj.Table.on_device(ccj.LP, own_keys, stream=self.stream)
-        del own_keys
+        own_keys = torch.cat(own) if own else torch.empty(0, dtype=torch.int64, device=self.device)
+        self.table = ccj.Table.on_device(ccj.LP, own_keys, stream=stream)
+        return own_keys.numel()
+
+    # pipelined protocol
+    def fixed_partitioner(self, n, world, seg_cap):
+        p = self.ccj.FixedOwnerPartitioner(n, world, seg_cap, device=self.device)
+        return lambda keys, row_base, sk, sr, sc, status, stream: p(keys, row_base, sk, sr, sc, status, stream=stream)
+
+    def segment_chunk_counts(self, seg_counts, seg_cap, chunk, out, status, stream):
+        self.ccj.segment_chunk_counts(seg_counts, seg_cap, chunk, out, status, stream=stream)
+
+    def alloc_group(self, gslots, chunk, status):
+        """Partition workspace + outputs of one receive group; the probe reports into `status`."""
+        part = self.table.alloc_partitioned(gslots, chunk)
+        out = self.table.alloc_outputs(part["positions"], chunk, rounds=False)
+        out["status"] = status
+        return part, out
+
+    def probe_group(self, keys, counts, part, out, chunk, stream):
+        self.table.probe_partitioned(keys, chunk, counts=counts, out=out, part=part, stream=stream, retry=False)
+
+    def group_rows(self, part, recv_rows, n_probe, seg_cap, slots, stream):
+        """Global probe row of every position of a group's partitioned layout (gap positions hold
+        arbitrary values: only matched positions are ever looked up)."""
+        n = recv_rows.numel()
+        with torch.cuda.stream(stream):
+            q = torch.arange(n, device=recv_rows.device) % slots
+            recv = (q // seg_cap) * n_probe + recv_rows.to(torch.int64)
+            rm = part["row_map"].to(torch.int64).clamp_(0, n - 1)
+            return recv[rm]
+
+    def checksum(self, out, chunk, row_map, stream):
+        return self.ccj.result_checksum(out, chunk, row_map=row_map, stream=stream)
+
+    # exact-size protocol
+    def owner_partitioner(self, n, world):
+        p = self.ccj.OwnerPartitioner(n, world, device=self.device)
+        return lambda keys, row_base, stream: p(keys, row_base, stream=stream)
+
+    def probe_exact(self, keys, chunk, stream):
+        return self.table.probe(keys, chunk, stream=stream, rounds=False)
+
+    def probe_cost(self, keys, stream):
+        return self.table.probe_cost(keys, stream=stream)
+
+
+class ShardedProbe:
+    """One rank's part of the multi-GPU probe of the C4 configuration."""
+
+    def __init__(self, n_build_total: int, cf: int, n_probe: int, chunk: int, world: int, rank: int,
+                 stream=None, batches: int = 4, ops=None, group=GROUP):
+        self.ops = ops or DeviceOps()
+        o = self.ops
+        self.world, self.rank, self.chunk, self.n_probe = world, rank, chunk, n_probe
+        self.stream = stream or o.stream()
+        self.comm = o.stream()
+        self.pstream = o.stream()  # partitions run beside the previous probe
+        self.n_build_local = o.build_local(n_build_total, cf, world, rank, self.stream)
         # batched, fixed-capacity exchange buffers: two send slots; receive buffers of `group`
         # batches each, two of them, so one group is probed while the next one arrives
         self.batches = batch_count(n_probe, world, chunk, batches)
         self.bn = -(-n_probe // self.batches)
-        self.group = min(self.batches, GROUP)
+        self.group = min(self.batches, group)
         self.n_groups = -(-self.batches // self.group)
-        self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+        # the rank's status word: owner-split overflow, receive-count overflow and the local
+        # probe's own flags (slot-split overflow, output capacity) all land here
+        self.status = o.zeros(1, torch.int32)
         self._resize(seg_capacity(self.bn, world, chunk))
-        ev = lambda: [torch.cuda.Event() for _ in range(2)]  # noqa: E731
+        ev = lambda: [o.event() for _ in range(2)]  # noqa: E731
         self.ev_part, self.ev_comm, self.ev_probe = ev(), ev(), ev()
         self.probe_events = []
         self.parts_exact = {}  # exact-size partitioners (fallback), by batch size
         self.last_exact = False
+        self.exact_steps = 0  # steps redone with the exact-size protocol (on every rank alike)
 
     def _resize(self, seg_cap: int):
         """(Re)allocate the exchange buffers for receive segments of seg_cap slots."""
         assert seg_cap % self.chunk == 0
-        dev = torch.device("cuda", torch.cuda.current_device())
+        o = self.ops
         self.seg_cap = seg_cap
         slots = self.world * seg_cap  # one batch's receive segments
         self.slots = slots
         gslots = self.group * slots
         self.fparts = {}
-        mk = lambda dt, n: [torch.zeros(n, dtype=dt, device=dev) for _ in range(2)]  # noqa: E731
+        mk = lambda dt, n: [o.zeros(n, dt) for _ in range(2)]  # noqa: E731
         self.sk, self.sr, self.sc = mk(torch.int64, slots), mk(torch.int32, slots), mk(torch.int64, self.world)
         self.rk, self.rr = mk(torch.int64, gslots), mk(torch.int32, gslots)
         self.rc = mk(torch.int64, self.group * self.world)
         self.cc = mk(torch.int32, gslots // self.chunk)
-        # local probe on the slot-partitioned path, one call per group of received batches: the
-        # live rows (per-chunk counts) are split by home-slot window, then walked with the table
-        # window L2-resident; a group of batches makes segments long enough to fill chunks
-        self.parts = [self.table.alloc_partitioned(gslots, self.chunk) for _ in range(2)]
-        self.outs = [self.table.alloc_outputs(p["positions"], self.chunk, rounds=False) for p in self.parts]
+        # local probe on the slot-partitioned path, one call per group of received batches
+        self.parts, self.outs = [], []
+        for _ in range(2):
+            part, out = o.alloc_group(gslots, self.chunk, self.status)
+            self.parts.append(part)
+            self.outs.append(out)
 
     def _batch(self, i):
         lo = i * self.bn
@@ -159,9 +247,9 @@ class ShardedProbe:
         s = i % 2
         lo, n = self._batch(i)
         if n not in self.fparts:
-            self.fparts[n] = ccj.FixedOwnerPartitioner(n, self.world, self.seg_cap, device=keys.device)
+            self.fparts[n] = self.ops.fixed_partitioner(n, self.world, self.seg_cap)
         self.pstream.wait_event(self.ev_comm[s])  # the previous all-to-all from send slot s is done
-        self.fparts[n](keys[lo:lo + n], lo, self.sk[s], self.sr[s], self.sc[s], self.status, stream=self.pstream)
+        self.fparts[n](keys[lo:lo + n], lo, self.sk[s], self.sr[s], self.sc[s], self.status, self.pstream)
         self.ev_part[s].record(self.pstream)
 
     def _exchange(self, i):
@@ -170,48 +258,44 @@ class ShardedProbe:
         self.comm.wait_event(self.ev_part[s])
         if i % self.group == 0:
             self.comm.wait_event(self.ev_probe[gs])  # the previous probe of receive group slot gs is done
-        with torch.cuda.stream(self.comm):
+        with self.ops.on(self.comm):
             exchange_fixed(self.sk[s], self.sr[s], self.sc[s], rk, rr, rc)
         self.ev_comm[s].record(self.comm)
 
+    def _group_range(self, g):
+        return g * self.group, min((g + 1) * self.group, self.batches) - 1
+
     def _probe(self, g, timing):
         """Probe group g (batches g*group ... its last one, all exchanged in order on comm)."""
+        o = self.ops
         gs = g % 2
-        first, last = g * self.group, min((g + 1) * self.group, self.batches) - 1
+        first, last = self._group_range(g)
         self.stream.wait_event(self.ev_comm[last % 2])
         per = self.slots // self.chunk
         for i in range(first, last + 1):
             sub = i % self.group
-            ccj.segment_chunk_counts(self.rc[gs][sub * self.world:(sub + 1) * self.world], self.seg_cap, self.chunk,
-                                     self.cc[gs][sub * per:(sub + 1) * per], self.status, stream=self.stream)
+            o.segment_chunk_counts(self.rc[gs][sub * self.world:(sub + 1) * self.world], self.seg_cap, self.chunk,
+                                   self.cc[gs][sub * per:(sub + 1) * per], self.status, self.stream)
         if last - first + 1 < self.group:  # a short last group: its missing batches have no live rows
-            with torch.cuda.stream(self.stream):
+            with o.on(self.stream):
                 self.cc[gs][(last - first + 1) * per:].zero_()
         if timing:
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a, b = o.event(True), o.event(True)
             a.record(self.stream)
-        self.table.probe_partitioned(self.rk[gs], self.chunk, counts=self.cc[gs], out=self.outs[gs],
-                                     part=self.parts[gs], stream=self.stream, retry=False)
+        o.probe_group(self.rk[gs], self.cc[gs], self.parts[gs], self.outs[gs], self.chunk, self.stream)
         if timing:
             b.record(self.stream)
             self.probe_events.append((a, b))
         self.ev_probe[gs].record(self.stream)
 
     def group_row_map(self, g):
-        """Global probe row of every position of group g's partitioned layout (gap positions hold
-        arbitrary values: only matched positions are ever looked up)."""
         gs = g % 2
-        n = self.group * self.slots
-        with torch.cuda.stream(self.stream):  # behind this group's probe, before the slot's next use
-            q = torch.arange(n, device=self.rr[gs].device) % self.slots
-            recv = (q // self.seg_cap) * self.n_probe + self.rr[gs].to(torch.int64)
-            rm = self.parts[gs]["row_map"].to(torch.int64).clamp_(0, n - 1)
-            return recv[rm]
+        return self.ops.group_rows(self.parts[gs], self.rr[gs], self.n_probe, self.seg_cap, self.slots, self.stream)
 
     def received_keys(self, i):
         """Batch i's received keys without the segment padding (work accounting)."""
         gs, rk, rr, rc = self._recv(i)
-        torch.cuda.current_stream().wait_event(self.ev_comm[i % 2])
+        self.ops.current().wait_event(self.ev_comm[i % 2])
         pos = torch.arange(self.slots, device=rk.device)
         live = (pos % self.seg_cap) < rc[pos // self.seg_cap]
         return rk[live]
@@ -219,10 +303,13 @@ class ShardedProbe:
     def step(self, keys, row_base: int = 0, timing: bool = False, verify: bool = False):
         """One pass over this rank's keys.  verify=True returns (matches, l2) of this rank's probes
         (global rows: source rank * n_probe + local row)."""
+        o = self.ops
         assert keys.numel() == self.n_probe and row_base == self.rank * self.n_probe
-        self.status.zero_()
-        self.stream.wait_stream(torch.cuda.current_stream())
-        self.pstream.wait_stream(torch.cuda.current_stream())
+        cur = o.current()
+        with o.on(cur):
+            self.status.zero_()
+        self.stream.wait_stream(cur)
+        self.pstream.wait_stream(cur)
         self._partition(keys, 0)
         self._exchange(0)
         m, l2 = 0, 0
@@ -234,33 +321,82 @@ class ShardedProbe:
                 g = i // self.group
                 self._probe(g, timing)
                 if verify:
-                    bm, bl = ccj.result_checksum(self.outs[g % 2], self.chunk, row_map=self.group_row_map(g),
-                                                 stream=self.stream)
+                    bm, bl = o.checksum(self.outs[g % 2], self.chunk, self.group_row_map(g), self.stream)
                     m, l2 = m + bm, (l2 + bl) % (1 << 64)
-        torch.cuda.current_stream().wait_stream(self.stream)
-        torch.cuda.current_stream().wait_stream(self.pstream)
-        if int(self.status.item()):  # a fixed-capacity segment overflowed: redo with exact sizes
+        cur.wait_stream(self.stream)
+        cur.wait_stream(self.pstream)
+        cur.wait_stream(self.comm)
+        # Every rank branches on the same value: the MAX of all ranks' status words.
+        if agree_status(self.status):
             self.last_exact = True
+            self.exact_steps += 1
             return self.step_exact(keys, row_base, verify)
         self.last_exact = False
         return (m, l2) if verify else None
 
     # ---- exact-size protocol (fallback for skewed keys), batch by batch, not overlapped ----
     def step_exact(self, keys, row_base: int, verify: bool = False):
-        torch.cuda.synchronize()
+        o = self.ops
+        o.synchronize()
         m, l2 = 0, 0
         for i in range(self.batches):
             lo, n = self._batch(i)
             if n not in self.parts_exact:
-                self.parts_exact[n] = ccj.OwnerPartitioner(n, self.world, device=keys.device)
-            k, r, cnt = self.parts_exact[n](keys[lo:lo + n], row_base + lo, stream=self.stream)
-            cur = torch.cuda.current_stream()
+                self.parts_exact[n] = o.owner_partitioner(n, self.world)
+            k, r, cnt = self.parts_exact[n](keys[lo:lo + n], row_base + lo, self.stream)
+            cur = o.current()
             cur.wait_stream(self.stream)  # RCCL runs behind the current stream
             recv_keys, recv_rows, rc = exchange(k, r, cnt)
             self.stream.wait_stream(cur)  # the probe runs behind the exchange
-            out = self.table.probe(recv_keys, self.chunk, stream=self.stream, rounds=False)
+            out = o.probe_exact(recv_keys, self.chunk, self.stream)
             if verify:
-                bm, bl = ccj.result_checksum(out, self.chunk, row_map=recv_rows, stream=self.stream)
+                bm, bl = o.checksum(out, self.chunk, recv_rows, self.stream)
                 m, l2 = m + bm, (l2 + bl) % (1 << 64)
-            torch.cuda.synchronize()
+            o.synchronize()
         return (m, l2) if verify else None
+
+
+class HostStream:
+    """Stand-in for a HIP stream on CPU tensors: work runs in program order, so ordering is trivial."""
+
+    def wait_event(self, ev):
+        pass
+
+    def wait_stream(self, other):
+        pass
+
+    def synchronize(self):
+        pass
+
+
+class HostEvent:
+    def record(self, stream=None):
+        pass
+
+    def elapsed_time(self, other):
+        return 0.0
+
+
+class HostOpsBase:
+    """Stream/event/buffer half of a CPU ops object (tests/test_dist_cpu.py supplies the kernels'
+    stand-ins on top of it)."""
+
+    device = torch.device("cpu")
+
+    def stream(self):
+        return HostStream()
+
+    def event(self, timing=False):
+        return HostEvent()
+
+    def current(self):
+        return HostStream()
+
+    def on(self, stream):
+        return contextlib.nullcontext()
+
+    def synchronize(self):
+        pass
+
+    def zeros(self, n, dtype):
+        return torch.zeros(n, dtype=dtype)

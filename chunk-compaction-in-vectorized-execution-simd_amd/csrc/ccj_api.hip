@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "ccj_internal.h"
+#include "ccj_tuning.h"
 
 namespace {
 
@@ -310,6 +311,22 @@ int build_lp_device(const int64_t *d_keys, uint64_t n, hipStream_t s, uint64_t k
   return CCJ_OK;
 }
 
+// Zipf s = 1 over ranks 1..n as a 2^16-bucket inverse CDF: t[j] = the smallest rank whose CDF
+// H_r / H_n exceeds j / 2^16, t[2^16] = n + 1 (the same IEEE-double construction as the test
+// oracle's ccj_zipf_table, so host and device streams agree bit for bit).
+void zipf_table(uint64_t n, uint32_t *t) {
+  double hn = 0.0;
+  for (uint64_t r = 1; r <= n; ++r) hn += 1.0 / (double)r;
+  uint32_t j = 0;
+  double h = 0.0;
+  for (uint64_t r = 1; r <= n && j < ccj::kZipfBuckets; ++r) {
+    h += 1.0 / (double)r;
+    while (j < ccj::kZipfBuckets && h * (double)ccj::kZipfBuckets > (double)j * hn) t[j++] = (uint32_t)r;
+  }
+  while (j < ccj::kZipfBuckets) t[j++] = (uint32_t)(n ? n : 1);
+  t[ccj::kZipfBuckets] = (uint32_t)(n + 1);
+}
+
 }  // namespace
 
 extern "C" {
@@ -386,27 +403,6 @@ int ccj_table_set_payload(ccj_table *t, const int64_t *d_payload, uint32_t n_col
   if (!t || n_cols == 0 || n_cols > CCJ_MAX_PAYLOAD_COLS || (!d_payload && t->info.n_keys))
     return fail(CCJ_ERR_INVALID, "ccj_table_set_payload: bad argument");
   if (!t->d_row) return fail(CCJ_ERR_INVALID, "ccj_table_set_payload: table has no row map");
-  // CCJ_PAY_DENSE=1 (LP): rows stored by rank among the occupied slots (4x smaller at load 1/4), found
-  // through per-32-slot rank words — a tuning override for the C5 gather
-  const char *dense_env = getenv("CCJ_PAY_DENSE");
-  if (dense_env && atoi(dense_env) && t->info.kind == CCJ_TABLE_LP && t->positions < (1ull << 32)) {
-    uint2 *rank = nullptr;
-    if (hipMalloc((void **)&rank, (t->positions + 31) / 32 * sizeof(uint2)) != hipSuccess)
-      return fail(CCJ_ERR_OOM, "payload rank: hipMalloc failed");
-    int64_t *dd = nullptr;
-    uint64_t nd = 0;
-    hipError_t e = ccj::launch_dense_payload(d_payload, n_cols, t->d_row, t->positions, rank, &dd, &nd, (hipStream_t)stream);
-    if (e != hipSuccess) {
-      (void)hipFree(rank);
-      return hip_fail(e, "dense payload");
-    }
-    if (t->d_pay) (void)hipFree(t->d_pay);
-    if (t->d_pay_rank) (void)hipFree(t->d_pay_rank);
-    t->d_pay = dd;
-    t->d_pay_rank = rank;
-    t->n_pay = n_cols;
-    return CCJ_OK;
-  }
   void *d = nullptr;
   if (hipMalloc(&d, t->positions * n_cols * sizeof(int64_t)) != hipSuccess)
     return fail(CCJ_ERR_OOM, "payload: hipMalloc failed");
@@ -418,8 +414,6 @@ int ccj_table_set_payload(ccj_table *t, const int64_t *d_payload, uint32_t n_col
     return hip_fail(e, "payload scatter");
   }
   if (t->d_pay) (void)hipFree(t->d_pay);
-  if (t->d_pay_rank) (void)hipFree(t->d_pay_rank);
-  t->d_pay_rank = nullptr;
   t->d_pay = (int64_t *)d;
   t->n_pay = n_cols;
   return CCJ_OK;
@@ -432,7 +426,6 @@ int ccj_table_free(ccj_table *t) {
   if (t->d_bucket) (void)hipFree(t->d_bucket);
   if (t->d_row) (void)hipFree(t->d_row);
   if (t->d_pay) (void)hipFree(t->d_pay);
-  if (t->d_pay_rank) (void)hipFree(t->d_pay_rank);
   delete t;
   return CCJ_OK;
 }
@@ -466,7 +459,6 @@ int fill_probe_params(const ccj_table *t, const ccj_probe_args *a, ccj::ProbePar
   p.out_pos = a->out_pos;
   if (a->n_payload_cols > t->n_pay) return fail(CCJ_ERR_INVALID, "ccj_probe: table has fewer payload columns");
   p.pay = t->d_pay;
-  p.pay_rank = t->d_pay_rank;
   p.n_pay = a->n_payload_cols;
   p.pay_stride = t->n_pay;
   for (uint32_t c = 0; c < a->n_payload_cols; ++c) {
@@ -566,10 +558,31 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
       HIP_TRY(hipMemsetAsync(a->out_count + p.n_chunks, 0, (out_chunks - p.n_chunks) * 4, s), "count tail");
   }
   p.keys = pkeys;
-  p.xcd_swizzle = getenv("CCJ_NO_SWIZZLE") ? 0 : 1;
-  if (const char *ab = getenv("CCJ_ABLATE")) p.ablate = (uint32_t)atoi(ab);
+  p.xcd_swizzle = 1;  // consecutive chunks (one partition's rows) go to one XCD: its L2 holds the window
+#ifdef CCJ_TUNING
+  p.ablate = (uint32_t)ccj_tune_int("CCJ_ABLATE", 0);
+#endif
   if (p.n_pay == 0) {
+#ifdef CCJ_TUNING
+    // CCJ_STATS: per-phase cycle sums of the walk's waves, printed per launch (tuning only)
+    static unsigned long long *stats = nullptr;
+    if (ccj_tune_env("CCJ_STATS")) {
+      if (!stats) HIP_TRY(hipMalloc((void **)&stats, 8 * sizeof(unsigned long long)), "stats");
+      HIP_TRY(hipMemsetAsync(stats, 0, 8 * sizeof(unsigned long long), s), "stats");
+      p.stats = stats;
+    }
+#endif
     HIP_TRY(ccj::launch_probe_flat(t->info.kind, p, s), "probe launch");
+#ifdef CCJ_TUNING
+    if (p.stats) {
+      unsigned long long h[8];
+      HIP_TRY(hipMemcpyAsync(h, p.stats, sizeof(h), hipMemcpyDeviceToHost, s), "stats");
+      HIP_TRY(hipStreamSynchronize(s), "stats");
+      const double w = h[4] ? (double)h[4] : 1.0;
+      fprintf(stderr, "[walk stats] waves %llu  per wave: stage %.0f  walk %.0f  emit %.0f cycles, %.2f steps\n",
+              h[4], h[0] / w, h[1] / w, h[2] / w, h[3] / w);
+    }
+#endif
     return CCJ_OK;
   }
   // Wide payload (C5): the walk records every match's table position, a second pass gathers rows
@@ -693,7 +706,20 @@ int ccj_gen_c3_keys(int64_t *d_out, uint64_t n, uint64_t seed, uint64_t first_ro
                     uint32_t hit_ppm, ccj_stream stream) {
   if ((!d_out && n) || cf == 0 || n_build == 0 || n_build >= (1ull << 62) || hit_ppm > 1000000)
     return fail(CCJ_ERR_INVALID, "ccj_gen_c3_keys: bad argument");
-  HIP_TRY(ccj::launch_gen_c3(d_out, n, seed, first_row, n_build, cf, hit_ppm, (hipStream_t)stream), "gen c3 keys");
+  const uint64_t n_unique = n_build / cf + (n_build % cf != 0);
+  if (n_unique >= (1ull << 32)) return fail(CCJ_ERR_LIMIT, "ccj_gen_c3_keys: more than 2^32 distinct build keys");
+  // Zipf s = 1 rank table over the n_unique build keys, built once per table size (host, untimed)
+  static uint64_t cached_n = 0;
+  static uint32_t *d_zipf = nullptr;
+  if (!d_zipf || cached_n != n_unique) {
+    std::vector<uint32_t> t(ccj::kZipfBuckets + 1);
+    zipf_table(n_unique, t.data());
+    if (!d_zipf) HIP_TRY(hipMalloc((void **)&d_zipf, t.size() * sizeof(uint32_t)), "zipf table");
+    HIP_TRY(hipMemcpy(d_zipf, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "zipf table");
+    cached_n = n_unique;
+  }
+  HIP_TRY(ccj::launch_gen_c3(d_out, n, seed, first_row, n_build, cf, hit_ppm, d_zipf, (hipStream_t)stream),
+          "gen c3 keys");
   return CCJ_OK;
 }
 

@@ -91,46 +91,7 @@ __device__ __forceinline__ uint64_t full_before(const CompactParams &p, uint64_t
   return lo;
 }
 
-__global__ __launch_bounds__(256) void copy_rows(CompactParams p) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t c = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (c >= p.a.n_chunks) return;
-  const uint64_t B = p.a.chunk;
-  const uint64_t F = p.totals[1] < p.max_full ? p.totals[1] : p.max_full;
-  const uint64_t cap_rows = p.a.out_cap_rows;
-  uint64_t t = p.nonfull[c], f = p.full[c];
-  uint64_t src = c * p.a.cap;  // rows of this chunk's result, round-major
-  const uint32_t rounds = p.a.rounds[c];
-  const uint32_t total = p.a.count[c];
-  for (uint32_t r = 0; r < rounds && r < p.a.max_rounds; ++r) {
-    const uint32_t rc = p.a.round_counts[c * p.a.max_rounds + r];
-    const bool is_full = p.bypass(rc);
-    const uint64_t fbase = (e_of(t, B) + f) * B;
-    for (uint32_t j = lane; j < rc; j += 64) {
-      if (src + j >= c * p.a.cap + total) break;  // probe capped this chunk (flagged there)
-      uint64_t dest;
-      if (is_full) {
-        dest = fbase + j;
-      } else {
-        const uint64_t u = t + j;
-        const uint64_t k = u / B;
-        dest = (k + (F ? full_before(p, F, k) : 0)) * B + (u - k * B);
-      }
-      if (dest >= cap_rows) continue;
-      const uint32_t s = p.a.sel[src + j];
-      const uint64_t row = c * B + s;
-#pragma unroll 4
-      for (uint32_t q = 0; q < p.a.n_cols; ++q) p.a.out_cols[q][dest] = p.a.cols[q][row];
-      if (p.a.out_payload) p.a.out_payload[dest] = p.a.payload[src + j];
-      if (p.a.out_row) p.a.out_row[dest] = row;
-    }
-    src += rc;
-    if (is_full) ++f;
-    else t += rc;
-  }
-}
-
-// Flat form of copy_rows for chunks with at most 64 Next results: lane r holds round r's count,
+// One wave per probe chunk with at most 64 Next results: lane r holds round r's count,
 // its P-stream start, its pass-through index and its source offset (wave prefix sums); every lane
 // then copies matches m = lane, lane + 64, ... of the chunk, finding m's round by a binary search
 // over the lanes.  All 64 lanes stay busy however the matches spread over rounds.
@@ -143,7 +104,7 @@ __global__ __launch_bounds__(256) void copy_rows_flat(CompactParams p) {
   const uint64_t cap_rows = p.a.out_cap_rows;
   const uint32_t rounds = p.a.rounds[c] < p.a.max_rounds ? p.a.rounds[c] : p.a.max_rounds;
   const uint32_t total = p.a.count[c];
-  if (rounds > 64) {  // rare: the per-round loop of copy_rows handles it
+  if (rounds > 64) {  // rare: a per-round loop (the round-wise form measured 4.20 vs 3.83 ms, main.cpp pipeline)
     uint64_t t = p.nonfull[c], f = p.full[c], src = c * p.a.cap;
     for (uint32_t r = 0; r < rounds; ++r) {
       const uint32_t rc = p.a.round_counts[c * p.a.max_rounds + r];
@@ -289,9 +250,7 @@ hipError_t launch_compact(const ccj_compact_args &a, hipStream_t s) {
   if (e) return e;
   hipLaunchKernelGGL(seg_totals, dim3(1), dim3(1), 0, s, p, nf_raw + a.n_chunks - 1, f_raw + a.n_chunks - 1);
   hipLaunchKernelGGL(full_list, dim3(g), dim3(256), 0, s, p);
-  static const bool flat = getenv("CCJ_COMPACT_ROUNDWISE") == nullptr;
-  if (flat) hipLaunchKernelGGL(copy_rows_flat, dim3((unsigned)((a.n_chunks + 3) / 4)), dim3(256), 0, s, p);
-  else hipLaunchKernelGGL(copy_rows, dim3((unsigned)((a.n_chunks + 3) / 4)), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(copy_rows_flat, dim3((unsigned)((a.n_chunks + 3) / 4)), dim3(256), 0, s, p);
   hipLaunchKernelGGL(chunk_counts, dim3(1024), dim3(256), 0, s, p);
   return hipGetLastError();
 }

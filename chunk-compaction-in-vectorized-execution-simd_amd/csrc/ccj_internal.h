@@ -16,7 +16,6 @@ struct ccj_table {
   uint32_t *d_row = nullptr;    // table position -> build tuple index (LP: kNoRow for empty slots)
   uint64_t positions = 0;       // allocated positions (LP slots / chain keys, padded)
   int64_t *d_pay = nullptr;     // position-major payload rows [positions][n_pay]
-  uint2 *d_pay_rank = nullptr;  // dense payload (LP, CCJ_PAY_DENSE=1): per 32 positions {occupied bits, occupied before}
   uint32_t n_pay = 0;
   int device = 0;
 };
@@ -61,7 +60,6 @@ struct ProbeParams {
   uint32_t *status;
   uint32_t *out_pos;
   const int64_t *pay;  // position-major payload rows
-  const uint2 *pay_rank;  // non-null: payload rows are dense, row of position p = rank of p among occupied
   uint32_t n_pay;      // payload columns gathered (<= CCJ_MAX_PAYLOAD_COLS)
   uint32_t pay_stride; // payload columns stored per position
   int64_t *out_cols[CCJ_MAX_PAYLOAD_COLS];
@@ -80,7 +78,8 @@ struct ProbeParams {
   uint64_t swz_chunks;   // chunks dealt to XCDs in contiguous ranges (0: all); the overflow area's
                          // chunks follow in plain order so they do not unbalance the XCDs' shares
   uint32_t xcd_swizzle;  // 1: consecutive chunks go to the same XCD (L2 reuse of partitioned input)
-  uint32_t ablate;       // timing-only ablations (CCJ_ABLATE env, never set in product calls)
+  uint32_t ablate;       // timing-only ablations (tuning build only: CCJ_ABLATE)
+  unsigned long long *stats;  // tuning build only (CCJ_STATS): per-phase cycle sums of the walk
 };
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 
@@ -95,8 +94,6 @@ hipError_t launch_fill(int64_t *p, uint64_t n, int64_t v, hipStream_t s);
 hipError_t launch_iota_u32(uint32_t *p, uint64_t n, hipStream_t s);
 hipError_t launch_lp_insert(const int64_t *keys, uint64_t n, int64_t *slots, uint32_t *slot_row, uint32_t mask,
                             hipStream_t s);
-hipError_t launch_dense_payload(const int64_t *src, uint32_t n_cols, const uint32_t *row, uint64_t positions,
-                                uint2 *rank, int64_t **dst, uint64_t *n_dense, hipStream_t s);
 hipError_t launch_scatter_payload(const int64_t *src, uint32_t n_cols, const uint32_t *row, uint64_t positions,
                                   int64_t *dst, hipStream_t s);
 // Per-segment run statistics of an LP slot array (segment = 4096 slots): 4 x uint32 per segment:
@@ -105,8 +102,10 @@ hipError_t launch_scatter_payload(const int64_t *src, uint32_t n_cols, const uin
 hipError_t launch_lp_max_dup(const int64_t *slots, uint64_t n_slots, uint32_t max_run, uint32_t *out, hipStream_t s);
 hipError_t launch_lp_runs(const int64_t *slots, uint64_t n_slots, uint32_t *seg_stats, hipStream_t s);
 constexpr uint64_t kRunSegment = 4096;
+// C3 probe stream; zipf: device copy of the rank table (kZipfBuckets + 1 entries, zipf_table()).
 hipError_t launch_gen_c3(int64_t *out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t n_build, uint64_t cf,
-                         uint32_t hit_ppm, hipStream_t s);
+                         uint32_t hit_ppm, const uint32_t *zipf, hipStream_t s);
+constexpr uint32_t kZipfBits = 16, kZipfBuckets = 1u << kZipfBits;
 hipError_t launch_gen_uniform(int64_t *out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t range,
                               hipStream_t s);
 hipError_t launch_probe_cost(int kind, const int64_t *table, const uint32_t *off, uint32_t mask,

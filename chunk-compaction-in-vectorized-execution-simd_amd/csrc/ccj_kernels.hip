@@ -16,20 +16,13 @@
 #include <string>
 
 #include "ccj_internal.h"
+#include "ccj_tuning.h"
 
 namespace ccj {
 namespace {
 
 __device__ __forceinline__ uint32_t lane_prefix(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-// Payload row of table position pos: the position itself, or with a dense payload its rank among
-// the occupied positions (one 8-byte read of the position's 32-position rank word).
-__device__ __forceinline__ uint64_t pay_index(const uint2 *rank, uint32_t pos) {
-  if (!rank) return pos;
-  const uint2 w = rank[pos >> 5];
-  return (uint64_t)w.y + (uint32_t)__popc(w.x & ((1u << (pos & 31u)) - 1u));
 }
 
 // Table position of row key k's candidate in round r (LP: home + r; chain: chain start + r) and
@@ -41,7 +34,7 @@ __device__ __forceinline__ void emit_extra(const ProbeParams &p, uint64_t obase,
   const uint32_t pos = KIND == CCJ_TABLE_LP ? ((h + r) & p.mask) : p.off[h] + r;
   if (p.out_pos) p.out_pos[obase + o] = pos;
   if (p.n_pay) {
-    const int64_t *row = p.pay + pay_index(p.pay_rank, pos) * p.pay_stride;
+    const int64_t *row = p.pay + (uint64_t)pos * p.pay_stride;
     for (uint32_t c = 0; c < p.n_pay; ++c) p.out_cols[c][obase + o] = row[c];
   }
 }
@@ -130,10 +123,7 @@ __device__ void rounds_generic(const ProbeParams &p, uint64_t c, uint64_t base, 
 
 constexpr int kWin = 4;             // slots (LP) / chain keys per window load: 32 B, one aligned sector
 constexpr int kMaxFastRounds = 32;  // rounds recorded by the windowed path (bits of a u32)
-#ifndef CCJ_WALK_ROWS
-#define CCJ_WALK_ROWS 2
-#endif
-constexpr int kWalkRows = CCJ_WALK_ROWS;  // rows per lane walked concurrently (loads in flight)
+constexpr int kWalkRows = 2;  // rows per lane walked concurrently (loads in flight)
 
 constexpr int kEmitRows = 4;    // row groups per lane whose sel loads are issued together in the emit
 constexpr int kChunkWaves = 4;  // waves cooperating on one chunk
@@ -436,12 +426,8 @@ __global__ __launch_bounds__(kBlock) void probe_chunks(ProbeParams p) {
   }
 }
 
-// Flat probe for slot-partitioned input (ccj_probe_partitioned): the output order inside a chunk
-// is free (L1/L2 parity), so every row walks its run and writes its matches as soon as they are
-// found — one phase, no per-round bookkeeping.  256 threads per 2048-row chunk, row i = k*256 +
-// tid (coalesced key loads), all of a lane's rows walked concurrently through aligned 32-byte
-// windows that the slot partitioning keeps L2-resident.  Matches are placed with one LDS atomic
-// per wave and step (wave prefix sum of the lanes' match counts).
+// Walks of slot-partitioned input (ccj_probe_partitioned): the output order inside a chunk is
+// free (L1/L2 parity), so there is no per-round bookkeeping; 256 threads per 2048-row chunk.
 constexpr int kFlatThreads = 256;
 constexpr int kFlatRows = kMaxChunk / kFlatThreads;  // 8
 constexpr uint32_t kFlatStage = kMaxChunk;          // matches staged in LDS per chunk
@@ -483,158 +469,6 @@ __device__ __forceinline__ uint32_t flat_phys(const ProbeParams &p, uint64_t bas
     phys = live > off ? (live - off < phys ? (uint32_t)(live - off) : phys) : 0u;
   }
   return phys;
-}
-
-template <int KIND, int W>
-__global__ __launch_bounds__(kFlatThreads) void probe_flat(ProbeParams p) {
-  __shared__ uint32_t s_cnt, s_rounds;
-  __shared__ uint32_t s_sel[kFlatStage];
-  __shared__ int64_t s_pay[kFlatStage];
-  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1);
-  uint64_t c = blockIdx.x;
-  if (p.xcd_swizzle) {
-    const uint64_t n8 = (p.swz_chunks ? p.swz_chunks : p.n_chunks) & ~7ull;
-    if (c < n8) c = (c & 7) * (n8 >> 3) + (c >> 3);
-  }
-  const uint64_t base = c * p.chunk;
-  const uint32_t phys = flat_phys(p, base);
-  const uint64_t obase = c * p.cap;
-  if (tid == 0) {
-    s_cnt = 0;
-    s_rounds = 0;
-  }
-  __syncthreads();
-  int64_t key[kFlatRows];
-  uint32_t cur[kFlatRows], r0[kFlatRows], lim[kFlatRows];
-  uint32_t need = 0, lane_rounds = 0;
-#pragma unroll
-  for (int k = 0; k < kFlatRows; ++k) {
-    const uint32_t i = k * kFlatThreads + tid;
-    key[k] = 0;
-    cur[k] = r0[k] = lim[k] = 0;
-    if (i < phys) {
-      key[k] = p.keys[base + i];
-      const uint32_t h = (uint32_t)murmurhash64((uint64_t)key[k]) & p.mask;
-      if (KIND == CCJ_TABLE_LP) {
-        cur[k] = h;
-        need |= 1u << k;
-      } else {
-        cur[k] = p.off[h];
-        lim[k] = p.off[h + 1];
-        if (cur[k] != lim[k]) need |= 1u << k;
-      }
-    }
-  }
-  uint32_t overflow = 0;
-  while (__ballot(need != 0u) != 0ull) {
-    int64_t v[kFlatRows][W];
-#pragma unroll
-    for (int k = 0; k < kFlatRows; ++k) {
-      if ((need >> k) & 1u) {
-        const int64_t *w = p.table + (cur[k] & ~(uint32_t)(W - 1));
-        if (p.ablate & 2u) {  // timing only: no table reads
-#pragma unroll
-          for (int t = 0; t < W; ++t) v[k][t] = t ? -1 : key[k];
-        } else if (W == 2) {
-          const longlong2 x = *reinterpret_cast<const longlong2 *>(w);
-          v[k][0] = x.x;
-          v[k][W - 1] = x.y;
-        } else {
-#pragma unroll
-          for (int t = 0; t < W; t += 2) {
-            const longlong2 x = reinterpret_cast<const longlong2 *>(w)[t / 2];
-            v[k][t] = x.x;
-            v[k][t + 1] = x.y;
-          }
-        }
-      }
-    }
-    uint32_t hits[kFlatRows];  // bit t: window position t matched
-    uint32_t n_hits = 0;
-#pragma unroll
-    for (int k = 0; k < kFlatRows; ++k) {
-      hits[k] = 0;
-      if ((need >> k) & 1u) {
-        const uint32_t blk = cur[k] & ~(uint32_t)(W - 1);
-        const uint32_t off = cur[k] - blk;
-        bool go = true;
-#pragma unroll
-        for (int t = 0; t < W; ++t) {
-          if (go && (uint32_t)t >= off) {
-            const int64_t val = v[k][t];
-            const bool stop = KIND == CCJ_TABLE_LP ? (val == -1) : (blk + (uint32_t)t == lim[k]);
-            if (stop) {
-              go = false;
-              const uint32_t r = r0[k] + (uint32_t)t - off;
-              lane_rounds = r > lane_rounds ? r : lane_rounds;
-            } else if (val == key[k]) {
-              hits[k] |= 1u << t;
-            }
-          }
-        }
-        n_hits += (uint32_t)__builtin_popcount(hits[k]);
-        if (go) {
-          r0[k] += (uint32_t)W - off;
-          cur[k] = KIND == CCJ_TABLE_LP ? ((blk + W) & p.mask) : blk + W;
-          if (KIND == CCJ_TABLE_CHAIN && cur[k] == lim[k]) {
-            lane_rounds = r0[k] > lane_rounds ? r0[k] : lane_rounds;
-            go = false;
-          }
-        }
-        if (!go) need &= ~(1u << k);
-      }
-    }
-    // place this step's matches: wave prefix of n_hits, one LDS atomic per wave
-    uint32_t incl = n_hits;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-      const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
-      if (lane >= (uint32_t)d) incl += o;
-    }
-    const uint32_t wave_total = (uint32_t)__shfl((int)incl, kWave - 1);
-    uint32_t wbase = 0;
-    if (wave_total) {
-      if (lane == 0) wbase = atomicAdd(&s_cnt, wave_total);
-      wbase = (uint32_t)__shfl((int)wbase, 0);
-    }
-    if (n_hits) {
-      uint32_t o = wbase + incl - n_hits;
-#pragma unroll
-      for (int k = 0; k < kFlatRows; ++k) {
-        for (uint32_t hm = hits[k]; hm; hm &= hm - 1u, ++o) {
-          if (p.ablate & 1u) continue;  // timing only: no output stores
-          const uint32_t i = k * kFlatThreads + tid;
-          if (o < kFlatStage) {  // staged in LDS, written out coalesced below
-            s_sel[o] = i;
-            s_pay[o] = key[k];  // matched table value == probe key
-          } else if (o < p.cap) {
-            p.out_sel[obase + o] = i;
-            if (p.out_payload) p.out_payload[obase + o] = key[k];
-          } else {
-            overflow = 1;
-          }
-        }
-      }
-    }
-  }
-  {
-    const uint32_t wr = wave_max(lane_rounds);
-    if (lane == 0) atomicMax(&s_rounds, wr);
-  }
-  __syncthreads();
-  const uint32_t total = s_cnt;
-  const uint32_t staged = total < kFlatStage ? total : kFlatStage;
-  if (!(p.ablate & 1u)) {
-    for (uint32_t q = tid; q < staged && q < p.cap; q += kFlatThreads) {
-      p.out_sel[obase + q] = s_sel[q];
-      if (p.out_payload) p.out_payload[obase + q] = s_pay[q];
-    }
-  }
-  if (tid == 0) {
-    p.out_count[c] = total < p.cap ? total : (uint32_t)p.cap;
-    if (p.out_rounds) p.out_rounds[c] = s_rounds;  // rounds the reference would run on this chunk
-  }
-  if (p.status && (overflow || total > p.cap)) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
 }
 
 // Several small chunks per workgroup (chunk B a multiple of 64, B <= 512: the reference's default
@@ -816,22 +650,15 @@ __global__ __launch_bounds__(kBlock) void probe_multi(ProbeParams p) {
 
 template <int KIND>
 hipError_t launch_kind(const ProbeParams &p, hipStream_t s) {
-  // CCJ_WALK_ROWS (tuning override): rows per lane walked concurrently.
-  static const int walk = [] {
-    const char *e = getenv("CCJ_WALK_ROWS");
-    return e ? atoi(e) : kWalkRows;
-  }();
-  static const bool multi = getenv("CCJ_NO_MULTI") == nullptr;
-  if (multi && p.chunk % kWave == 0 && p.chunk <= 512 && !p.xcd_swizzle) {
+  // Chunks of <= 512 rows (the reference's default kBlockSize 256, base.h:42) share a workgroup.
+  if (p.chunk % kWave == 0 && p.chunk <= 512 && !p.xcd_swizzle) {
     const uint64_t per = kMaxChunk / p.chunk;
-    hipLaunchKernelGGL((probe_multi<KIND, 2>), dim3((unsigned)((p.n_chunks + per - 1) / per)), dim3(kBlock), 0, s, p);
+    hipLaunchKernelGGL((probe_multi<KIND, kWalkRows>), dim3((unsigned)((p.n_chunks + per - 1) / per)), dim3(kBlock), 0,
+                       s, p);
     return hipGetLastError();
   }
-  const dim3 g((unsigned)p.n_chunks), b(kBlock);
-  if (walk <= 2) hipLaunchKernelGGL((probe_chunks<KIND, 2>), g, b, 0, s, p);
-  else if (walk <= 4) hipLaunchKernelGGL((probe_chunks<KIND, 4>), g, b, 0, s, p);
-  else if (walk <= 6) hipLaunchKernelGGL((probe_chunks<KIND, 6>), g, b, 0, s, p);
-  else hipLaunchKernelGGL((probe_chunks<KIND, 8>), g, b, 0, s, p);
+  // G = 2 cursors per lane (G = 4 / 6 / 8 measured 34.2 / 33.3 / 22.5 G tuples/s vs 35.3 at C2)
+  hipLaunchKernelGGL((probe_chunks<KIND, kWalkRows>), dim3((unsigned)p.n_chunks), dim3(kBlock), 0, s, p);
   return hipGetLastError();
 }
 
@@ -942,19 +769,17 @@ __device__ __forceinline__ uint64_t perm_n(uint64_t x, uint64_t n, uint64_t seed
 }
 
 __global__ void gen_c3(int64_t *out, uint64_t n, uint64_t seed, uint64_t first, uint64_t n_build, uint64_t cf,
-                       uint32_t hit_ppm) {
+                       uint32_t hit_ppm, const uint32_t *zipf) {
   const uint64_t n_unique = n_build / cf + (n_build % cf != 0);
   const uint64_t step = n_unique ? n_build / n_unique : 1;
-  const uint32_t levels = bitlen64(n_unique);
   for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t i = first + t;
     const uint64_t z1 = splitmix_at(seed, 3 * i), z2 = splitmix_at(seed, 3 * i + 1);
     const uint64_t z3 = splitmix_at(seed, 3 * i + 2);
     int64_t key;
-    if (z1 % 1000000ull < hit_ppm && n_unique) {
-      const uint32_t b = (uint32_t)((z2 >> 32) % levels);
-      const uint64_t lo = 1ull << b;
-      const uint64_t hi = (b + 1 < 64 && (2ull << b) - 1 < n_unique) ? (2ull << b) - 1 : n_unique;
+    if (z1 % 1000000ull < hit_ppm && n_unique) {  // Zipf s = 1 rank: bucket = top 16 bits of z2
+      const uint32_t j = (uint32_t)(z2 >> (64 - kZipfBits));
+      const uint64_t lo = zipf[j], hi = zipf[j + 1] > zipf[j] ? (uint64_t)zipf[j + 1] - 1 : lo;
       const uint64_t r = lo + (z2 & 0xffffffffull) % (hi - lo + 1);
       key = (int64_t)(perm_n(r - 1, n_unique, seed) * step);
     } else {
@@ -1040,187 +865,18 @@ unsigned grid_for(uint64_t n, unsigned block) {
 
 }  // namespace
 
-// Pair variant of probe_flat: two lanes walk one row together through aligned 32-byte windows,
-// each loading 16 bytes of it, so the pair's two loads of one window are one L2 request (the
-// single-lane walk needs ~2.1 16-byte requests per row, this ~1.4).  The pair agrees on where the
-// run ends with one lane swap.  Keys are staged in LDS; R rows per pair are in flight, a finished
-// row's cursor takes the pair's next row at once.
-template <int KIND, int R>
-__global__ __launch_bounds__(kFlatThreads) void probe_pair(ProbeParams p) {
-  constexpr uint32_t WS = 4;                       // slots per window
-  constexpr uint32_t kPairs = kFlatThreads / 2;    // 128 rows walked side by side per step
-  constexpr uint32_t kStride = kPairs * R;         // row step of a refilled cursor
-  __shared__ uint32_t s_cnt, s_rounds;
-  __shared__ int64_t s_key[kMaxChunk];
-  __shared__ uint32_t s_sel[kFlatStage];
-  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1);
-  const uint32_t h = tid & 1u, pr = tid >> 1;
-  uint64_t c = blockIdx.x;
-  if (p.xcd_swizzle) {
-    const uint64_t n8 = (p.swz_chunks ? p.swz_chunks : p.n_chunks) & ~7ull;
-    if (c < n8) c = (c & 7) * (n8 >> 3) + (c >> 3);
-  }
-  const uint64_t base = c * p.chunk;
-  const uint32_t phys = flat_phys(p, base);
-  const uint64_t obase = c * p.cap;
-  stage_keys(s_key, p.keys + base, phys, tid);
-  if (tid == 0) {
-    s_cnt = 0;
-    s_rounds = 0;
-  }
-  __syncthreads();
-  int64_t key[R];
-  uint32_t row[R], cur[R], lim[R], r0[R];
-  uint32_t need = 0, lane_rounds = 0, overflow = 0;
-  auto start = [&](int k, uint32_t i) {
-    row[k] = i;
-    r0[k] = 0;
-    while (i < phys) {
-      key[k] = s_key[i];
-      const uint32_t hh = (uint32_t)murmurhash64((uint64_t)key[k]) & p.mask;
-      if (KIND == CCJ_TABLE_LP) {
-        cur[k] = hh;
-        need |= 1u << k;
-        return;
-      }
-      cur[k] = p.off[hh];
-      lim[k] = p.off[hh + 1];
-      if (cur[k] != lim[k]) {
-        need |= 1u << k;
-        return;
-      }
-      i += kStride;  // empty bucket: no round
-      row[k] = i;
-    }
-  };
-#pragma unroll
-  for (int k = 0; k < R; ++k) {
-    key[k] = 0;
-    cur[k] = lim[k] = 0;
-    start(k, k * kPairs + pr);
-  }
-  while (__ballot(need != 0u) != 0ull) {
-    longlong2 v[R];
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-      v[k].x = v[k].y = 0;
-      const uint32_t s0 = (cur[k] & ~(WS - 1)) + 2 * h;
-      if (((need >> k) & 1u) && (KIND == CCJ_TABLE_LP || s0 < lim[k])) {
-        if (p.ablate & 2u) {
-          v[k].x = key[k];
-          v[k].y = -1;
-        } else {
-          v[k] = *reinterpret_cast<const longlong2 *>(p.table + s0);
-        }
-      }
-    }
-    uint32_t hits[R];
-    uint32_t n_hits = 0, done = 0;
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-      const bool act = (need >> k) & 1u;
-      const uint32_t blk = cur[k] & ~(WS - 1);
-      const uint32_t off = cur[k] - blk;
-      const uint32_t p0 = 2 * h, p1 = 2 * h + 1;
-      uint32_t f;  // first window position ending the run (WS: none)
-      if (KIND == CCJ_TABLE_LP) {
-        uint32_t fl = WS;
-        if (act && p1 >= off && v[k].y == -1) fl = p1;
-        if (act && p0 >= off && v[k].x == -1) fl = p0;
-        const uint32_t fo = (uint32_t)__shfl_xor((int)fl, 1);
-        f = fl < fo ? fl : fo;
-      } else {
-        const uint32_t d = lim[k] - blk;
-        f = d < WS ? d : WS;
-      }
-      hits[k] = 0;
-      if (act) {
-        if (p0 >= off && p0 < f && v[k].x == key[k]) hits[k] |= 1u;
-        if (p1 >= off && p1 < f && v[k].y == key[k]) hits[k] |= 2u;
-        n_hits += (uint32_t)__builtin_popcount(hits[k]);
-        if (f < WS) {
-          const uint32_t r = r0[k] + f - off;
-          lane_rounds = r > lane_rounds ? r : lane_rounds;
-          done |= 1u << k;
-        } else {
-          r0[k] += WS - off;
-          cur[k] = KIND == CCJ_TABLE_LP ? ((blk + WS) & p.mask) : blk + WS;
-          if (KIND == CCJ_TABLE_CHAIN && cur[k] == lim[k]) {
-            lane_rounds = r0[k] > lane_rounds ? r0[k] : lane_rounds;
-            done |= 1u << k;
-          }
-        }
-      }
-    }
-    uint32_t incl = n_hits;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-      const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
-      if (lane >= (uint32_t)d) incl += o;
-    }
-    const uint32_t wave_total = (uint32_t)__shfl((int)incl, kWave - 1);
-    uint32_t wbase = 0;
-    if (wave_total) {
-      if (lane == 0) wbase = atomicAdd(&s_cnt, wave_total);
-      wbase = (uint32_t)__shfl((int)wbase, 0);
-    }
-    if (n_hits && !(p.ablate & 1u)) {
-      uint32_t o = wbase + incl - n_hits;
-#pragma unroll
-      for (int k = 0; k < R; ++k) {
-        for (uint32_t hm = hits[k]; hm; hm &= hm - 1u, ++o) {
-          if (o < kFlatStage) {
-            s_sel[o] = row[k];  // payload = s_key[row]: the matched table value == probe key
-          } else if (o < p.cap) {
-            p.out_sel[obase + o] = row[k];
-            if (p.out_payload) p.out_payload[obase + o] = key[k];
-          } else {
-            overflow = 1;
-          }
-        }
-      }
-    }
-    if (done) {
-#pragma unroll
-      for (int k = 0; k < R; ++k)
-        if ((done >> k) & 1u) {
-          need &= ~(1u << k);
-          start(k, row[k] + kStride);
-        }
-    }
-  }
-  {
-    const uint32_t wr = wave_max(lane_rounds);
-    if (lane == 0) atomicMax(&s_rounds, wr);
-  }
-  __syncthreads();
-  const uint32_t total = s_cnt;
-  const uint32_t staged = total < kFlatStage ? total : kFlatStage;
-  if (!(p.ablate & 1u)) {
-    for (uint32_t o = tid; o < staged && o < p.cap; o += kFlatThreads) {
-      __builtin_nontemporal_store(s_sel[o], p.out_sel + obase + o);
-      if (p.out_payload) __builtin_nontemporal_store(s_key[s_sel[o]], p.out_payload + obase + o);
-    }
-  }
-  if (tid == 0) {
-    p.out_count[c] = total < p.cap ? total : (uint32_t)p.cap;
-    if (p.out_rounds) p.out_rounds[c] = s_rounds;
-  }
-  if (p.status && (overflow || total > p.cap)) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
-}
-
-// LP walk for slot-partitioned input (probe_win): LPR lanes per row (1 or 2), windows of WS slots
-// (each lane loads WS / LPR of them as 16-byte pieces), R rows in flight per lane group.  ALIGN:
-// windows aligned to WS slots; otherwise a window starts at the row's next unread slot (clamped so
-// it never passes the table end), which covers WS slots of the run with every load.  Against
-// probe_pair the per-step bookkeeping is bit arithmetic on the window's empty / match masks (one
-// DPP swap for LPR = 2, nothing cross-lane for LPR = 1), the wave prefix of the step's matches is
-// bit-sliced over ballots instead of a shuffle scan, and a finished cursor takes the chunk's next
-// unwalked row from an LDS counter (one atomic per wave and step), so every thread stays busy
-// until the chunk's rows run out instead of draining a fixed share.
-template <int LPR, int WS, int R, bool ALIGN, bool POS, int LINE>
+// probe_win<R>: the LP walk of slot-partitioned input that also records every match's table
+// position (C5: the payload gather reads the rows by position).  Two lanes per row, each loading
+// 16 B of a 32-byte window that starts at the row's next unread slot (clamped to the table end and
+// to the window's 128-byte line), R rows in flight per pair.  The step's matches are placed with a
+// bit-sliced wave prefix (<= 5 ballots + mbcnt) and one LDS atomic per wave, staged in LDS with
+// their positions and written out coalesced; a finished pair takes the chunk's next unwalked row
+// from an LDS counter.
+template <int R>
 __device__ __forceinline__ void walk_chunk(const ProbeParams &p, uint64_t c, uint32_t &s_cnt, uint32_t &s_rounds,
                                            uint32_t &s_next, int64_t *s_key, uint16_t *s_sel, uint32_t *s_pos) {
+  constexpr int LPR = 2, WS = 4, LINE = 16;  // lanes per row, window slots, slots per 128-B line
+  constexpr bool ALIGN = false, POS = true;
   constexpr uint32_t kGroups = kFlatThreads / LPR;  // rows walked side by side
   constexpr int kSlotsPerLane = WS / LPR;
   constexpr int kLoads = kSlotsPerLane / 2;  // 16-byte pieces per lane and window
@@ -1267,7 +923,7 @@ __device__ __forceinline__ void walk_chunk(const ProbeParams &p, uint64_t c, uin
         const int64_t *w = p.table + st[k] + sub * kSlotsPerLane;
 #pragma unroll
         for (int t = 0; t < kSlotsPerLane; t += 2) {
-          if (p.ablate & 2u) {  // timing only: no table reads
+          if (CCJ_ABLATED(p.ablate, 2u)) {  // timing only: no table reads
             v[k][t] = t ? -1 : key[k];
             v[k][t + 1] = -1;
           } else if (ALIGN) {
@@ -1326,7 +982,7 @@ __device__ __forceinline__ void walk_chunk(const ProbeParams &p, uint64_t c, uin
       uint32_t wb = 0;
       if (lane == 0) wb = atomicAdd(&s_cnt, tot);
       wb = (uint32_t)__builtin_amdgcn_readfirstlane((int)wb);
-      if (n && !(p.ablate & 1u)) {
+      if (n && !(CCJ_ABLATED(p.ablate, 1u))) {
         uint32_t o = wb + pre;
 #pragma unroll
         for (int k = 0; k < R; ++k) {
@@ -1381,7 +1037,7 @@ __device__ __forceinline__ void walk_chunk(const ProbeParams &p, uint64_t c, uin
   __syncthreads();
   const uint32_t total = s_cnt;
   const uint32_t staged = total < kFlatStage ? total : kFlatStage;
-  if (!(p.ablate & 1u)) {
+  if (!(CCJ_ABLATED(p.ablate, 1u))) {
     for (uint32_t o = tid; o < staged && o < p.cap; o += kFlatThreads) {
       const uint32_t r = s_sel[o];
       __builtin_nontemporal_store(r, p.out_sel + obase + o);
@@ -1396,22 +1052,18 @@ __device__ __forceinline__ void walk_chunk(const ProbeParams &p, uint64_t c, uin
   if (p.status && (overflow || total > p.cap)) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
 }
 
-template <int LPR, int WS, int R, bool ALIGN, bool POS = false, int LINE = 0>
+template <int R>
 __global__ __launch_bounds__(kFlatThreads) void probe_win(ProbeParams p) {
   __shared__ uint32_t s_cnt, s_rounds, s_next;
   __shared__ int64_t s_key[kMaxChunk];
-  // Matches are staged in LDS and written out coalesced at the end: writing each wave step's range
-  // straight to the output (16 KB of LDS, 8 workgroups per CU instead of 6) measured 14.1-15.0 ms
-  // against 11.5 at C2.
-  // Chunk rows fit 16 bits: 20 KB of LDS per workgroup, 7 per CU (28 KB and 5 with POS).
-  __shared__ uint16_t s_sel[kFlatStage];
-  __shared__ uint32_t s_pos[POS ? kFlatStage : 1];  // POS (C5): every match's table position
+  __shared__ uint16_t s_sel[kFlatStage];  // chunk rows fit 16 bits
+  __shared__ uint32_t s_pos[kFlatStage];  // every match's table position
   uint64_t c = blockIdx.x;
   if (p.xcd_swizzle) {
     const uint64_t n8 = (p.swz_chunks ? p.swz_chunks : p.n_chunks) & ~7ull;
     if (c < n8) c = (c & 7) * (n8 >> 3) + (c >> 3);
   }
-  walk_chunk<LPR, WS, R, ALIGN, POS, LINE>(p, c, s_cnt, s_rounds, s_next, s_key, s_sel, s_pos);
+  walk_chunk<R>(p, c, s_cnt, s_rounds, s_next, s_key, s_sel, s_pos);
 }
 
 // Chaining walk for bucket-partitioned input (probe_chain_win): one lane per row, R rows in
@@ -1506,7 +1158,7 @@ __global__ __launch_bounds__(kFlatThreads) void probe_chain_win(ProbeParams p) {
       uint32_t wb = 0;
       if (lane == 0) wb = atomicAdd(&s_cnt, tot);
       wb = (uint32_t)__builtin_amdgcn_readfirstlane((int)wb);
-      if (n && !(p.ablate & 1u)) {
+      if (n && !(CCJ_ABLATED(p.ablate, 1u))) {
         uint32_t o = wb + pre;
 #pragma unroll
         for (int k = 0; k < R; ++k) {
@@ -1551,7 +1203,7 @@ __global__ __launch_bounds__(kFlatThreads) void probe_chain_win(ProbeParams p) {
   __syncthreads();
   const uint32_t total = s_cnt;
   const uint32_t staged = total < kFlatStage ? total : kFlatStage;
-  if (!(p.ablate & 1u)) {
+  if (!(CCJ_ABLATED(p.ablate, 1u))) {
     for (uint32_t o = tid; o < staged && o < p.cap; o += kFlatThreads) {
       __builtin_nontemporal_store(s_sel[o], p.out_sel + obase + o);
       if (p.out_payload) __builtin_nontemporal_store(s_key[s_sel[o]], p.out_payload + obase + o);
@@ -1564,50 +1216,270 @@ __global__ __launch_bounds__(kFlatThreads) void probe_chain_win(ProbeParams p) {
   if (p.status && (overflow || total > p.cap)) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
 }
 
+// probe_walk: the LP walk of slot-partitioned input, one wave per 512-row quarter of a chunk,
+// no per-step output bookkeeping.  Each wave stages its own rows' keys (and, with
+// HOME, their home slots) in LDS; its lanes walk rows through 32-byte windows from the row's next
+// unread slot (a window never crosses a 128-byte line: one L2 request); a finished row only
+// leaves its match count in LDS and takes the wave's next row (a wave-uniform cursor, ballot
+// prefix, no LDS atomic).  After the walk the wave reserves its output range with one LDS atomic
+// and writes its rows' matches in row order, coalesced (payload = the probe key, sel = the row's
+// position).  A lane pair walks a row, 16 B each (one DPP swap joins the halves), R rows per pair
+// in flight.
+constexpr uint32_t kWaveRows = kMaxChunk / (kFlatThreads / kWave);  // 512
+
+template <bool HOME>
+struct WalkShared {
+  int64_t key[kMaxChunk];
+  // HOME: the row's home slot, then its match count; else only the count (16 bits: a row's
+  // matches are at most max_dup; 20 KB of LDS in all, 8 workgroups per CU)
+  std::conditional_t<HOME, uint32_t, uint16_t> hc[kMaxChunk];
+  uint32_t total, rounds;
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+  // Rows move between lanes of one wave only: its LDS writes must land before other lanes read.
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool HOME>
+__device__ __forceinline__ void walk_stage(const ProbeParams &p, WalkShared<HOME> &sm, uint64_t base, uint32_t w0,
+                                           uint32_t wend, uint32_t lane) {
+  int64_t v[kWaveRows / kWave];  // all loads in flight before the first LDS write
+#pragma unroll
+  for (int j = 0; j < (int)(kWaveRows / kWave); ++j) {
+    const uint32_t i = w0 + (uint32_t)j * kWave + lane;
+    v[j] = i < wend ? __builtin_nontemporal_load(p.keys + base + i) : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < (int)(kWaveRows / kWave); ++j) {
+    const uint32_t i = w0 + (uint32_t)j * kWave + lane;
+    sm.key[i] = v[j];
+    if (HOME) sm.hc[i] = (uint32_t)murmurhash64((uint64_t)v[j]) & p.mask;
+  }
+  wave_lds_sync();
+}
+
+// Emit the wave's rows [w0, wend): counts in sm.hc; returns 1 on output overflow.
+template <typename SM>
+__device__ __forceinline__ uint32_t walk_emit(const ProbeParams &p, SM &sm, uint64_t c, uint32_t w0,
+                                              uint32_t wend, uint32_t lane) {
+  wave_lds_sync();
+  uint32_t lsum = 0;
+#pragma unroll
+  for (int j = 0; j < (int)(kWaveRows / kWave); ++j) {
+    const uint32_t i = w0 + (uint32_t)j * kWave + lane;
+    lsum += i < wend ? sm.hc[i] : 0u;
+  }
+  uint32_t wsum = lsum;
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) wsum += (uint32_t)__shfl_xor((int)wsum, d);
+  uint32_t ob = 0;
+  if (lane == 0 && wsum) ob = atomicAdd(&sm.total, wsum);
+  ob = (uint32_t)__builtin_amdgcn_readfirstlane((int)ob);
+  const uint64_t obase = c * p.cap;
+  uint32_t overflow = 0;
+#pragma unroll 2
+  for (int j = 0; j < (int)(kWaveRows / kWave); ++j) {
+    const uint32_t i = w0 + (uint32_t)j * kWave + lane;
+    const uint32_t n = i < wend ? sm.hc[i] : 0u;
+    uint32_t pre, tot;
+    if (!__ballot(n > 1u)) {  // every row 0 or 1 match: one ballot
+      const uint64_t bm = __ballot(n != 0u);
+      pre = lane_prefix(bm);
+      tot = (uint32_t)__popcll(bm);
+    } else {
+      uint32_t incl = n;
+#pragma unroll
+      for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
+        if (lane >= (uint32_t)d) incl += o;
+      }
+      pre = incl - n;
+      tot = (uint32_t)__shfl((int)incl, kWave - 1);
+    }
+    if (n && !CCJ_ABLATED(p.ablate, 1u)) {
+      const int64_t k = sm.key[i];
+      for (uint32_t t = 0; t < n; ++t) {
+        const uint64_t o = (uint64_t)ob + pre + t;
+        if (o < p.cap) {
+          __builtin_nontemporal_store(i, p.out_sel + obase + o);
+          if (p.out_payload) __builtin_nontemporal_store(k, p.out_payload + obase + o);
+        } else {
+          overflow = 1;
+        }
+      }
+    }
+    ob += tot;
+  }
+  return overflow;
+}
+
+__device__ __forceinline__ uint64_t walk_chunk_index(const ProbeParams &p) {
+  uint64_t c = blockIdx.x;
+  if (p.xcd_swizzle) {
+    const uint64_t n8 = (p.swz_chunks ? p.swz_chunks : p.n_chunks) & ~7ull;
+    if (c < n8) c = (c & 7) * (n8 >> 3) + (c >> 3);
+  }
+  return c;
+}
+
+template <typename SM>
+__device__ __forceinline__ void walk_finish(const ProbeParams &p, SM &sm, uint64_t c, uint32_t lane,
+                                            uint32_t lane_rounds, uint32_t overflow, unsigned long long t0,
+                                            unsigned long long t1, unsigned long long t2, uint32_t steps) {
+  if (p.out_rounds) {
+    const uint32_t wr = wave_max(lane_rounds);
+    if (lane == 0) atomicMax(&sm.rounds, wr);
+  }
+  unsigned long long t3;
+  CCJ_STAMP(t3);
+  if (p.stats && lane == 0) {
+    atomicAdd(&p.stats[0], t1 - t0);
+    atomicAdd(&p.stats[1], t2 - t1);
+    atomicAdd(&p.stats[2], t3 - t2);
+    atomicAdd(&p.stats[3], (unsigned long long)steps);
+    atomicAdd(&p.stats[4], 1ull);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t total = sm.total;
+    p.out_count[c] = total < p.cap ? total : (uint32_t)p.cap;
+    if (p.out_rounds) p.out_rounds[c] = sm.rounds;
+  }
+  if (p.status && overflow) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
+}
+
+template <int R, bool HOME>
+__global__ __launch_bounds__(kFlatThreads) void probe_walk(ProbeParams p) {
+  __shared__ WalkShared<HOME> sm;
+  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  const uint32_t sub = lane & 1u;
+  unsigned long long t0, t1, t2;
+  uint32_t steps = 0;
+  CCJ_STAMP(t0);
+  const uint64_t c = walk_chunk_index(p);
+  const uint64_t base = c * p.chunk;
+  const uint32_t phys = flat_phys(p, base);
+  const uint32_t w0 = wave * kWaveRows;
+  const uint32_t wend = phys > w0 ? (phys - w0 < kWaveRows ? phys : w0 + kWaveRows) : w0;  // wave's rows [w0, wend)
+  if (tid == 0) {
+    sm.total = 0;
+    sm.rounds = 0;
+  }
+  walk_stage<HOME>(p, sm, base, w0, wend, lane);
+  CCJ_STAMP(t1);
+  const uint32_t last_start = p.mask - 3u;  // table size - 4 (size >= 16)
+  const uint32_t pair = lane >> 1;
+  int64_t key[R];
+  uint32_t row[R], cur[R], cnt[R], r0[R];
+  uint32_t need = 0, lane_rounds = 0;
+  auto start = [&](int k, uint32_t i) {
+    row[k] = i;
+    cnt[k] = 0;
+    r0[k] = 0;
+    if (i < wend) {
+      key[k] = sm.key[i];
+      cur[k] = HOME ? sm.hc[i] : (uint32_t)murmurhash64((uint64_t)key[k]) & p.mask;
+      need |= 1u << k;
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    key[k] = 0;
+    cur[k] = 0;
+    start(k, w0 + (uint32_t)k * (kWave / 2) + pair);
+  }
+  uint32_t next = w0 + (uint32_t)R * (kWave / 2);  // wave-uniform: the wave's next unwalked row
+  while (__ballot(need != 0u) != 0ull) {
+    ++steps;
+    int64_t v0[R], v1[R];
+    uint32_t st[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      uint32_t s = cur[k] < last_start ? cur[k] : last_start;
+      const uint32_t lim = (s & ~15u) + 12u;  // the window ends at its 128-byte line
+      s = s < lim ? s : lim;
+      st[k] = s;
+      v0[k] = -1;
+      v1[k] = -1;
+      if ((need >> k) & 1u) {
+        if (CCJ_ABLATED(p.ablate, 2u)) {  // timing only: no table reads
+          v0[k] = sub ? -1 : key[k];
+        } else {
+          const longlong2 x = *reinterpret_cast<const longlong2 *>(p.table + s + 2 * sub);
+          v0[k] = x.x;
+          v1[k] = x.y;
+        }
+      }
+    }
+    uint32_t done = 0;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      uint32_t e = ((v0[k] == -1) ? 1u : 0u) | ((v1[k] == -1) ? 2u : 0u);
+      uint32_t m = ((v0[k] == key[k]) ? 1u : 0u) | ((v1[k] == key[k]) ? 2u : 0u);
+      uint32_t em = (e | m << 4) << (2 * sub);
+      em |= (uint32_t)__builtin_amdgcn_mov_dpp((int)em, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+      if ((need >> k) & 1u) {
+        const uint32_t off = cur[k] - st[k];
+        const uint32_t ee = (em & 15u) >> off;
+        const uint32_t f = (uint32_t)__builtin_ctz(ee | (16u >> off));  // run end (or window end) past cur
+        cnt[k] += (uint32_t)__builtin_popcount(((em >> 4) >> off) & ((1u << f) - 1u));
+        if (ee) {
+          const uint32_t r = r0[k] + f;  // occupied slots walked = the reference's rounds
+          lane_rounds = r > lane_rounds ? r : lane_rounds;
+          done |= 1u << k;
+        } else {
+          r0[k] += 4u - off;
+          cur[k] = (st[k] + 4u) & p.mask;
+        }
+      }
+    }
+    // Finished rows leave their count and take the wave's next rows (pairs in lane order).
+    const uint32_t nd = (uint32_t)__builtin_popcount(done);
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int b = 0; (1 << b) <= R; ++b) {
+      const uint64_t bm = __ballot(((nd >> b) & 1u) && !sub);
+      pre += lane_prefix(bm) << b;
+      tot += (uint32_t)__popcll(bm) << b;
+    }
+    if (tot) {
+      pre = (uint32_t)__builtin_amdgcn_mov_dpp((int)pre, 0xA0, 0xF, 0xF, false);  // the pair's even lane's
+      uint32_t rb = next + pre;
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        if ((done >> k) & 1u) {
+          need &= ~(1u << k);
+          if (!sub) sm.hc[row[k]] = (std::remove_reference_t<decltype(sm.hc[0])>)cnt[k];
+          start(k, rb++);
+        }
+      }
+      next += tot;
+    }
+  }
+  CCJ_STAMP(t2);
+  const uint32_t overflow = walk_emit(p, sm, c, w0, wend, lane);
+  walk_finish(p, sm, c, lane, lane_rounds, overflow, t0, t1, t2, steps);
+}
+
 hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
   if (p.n_chunks == 0) return hipSuccess;
   const dim3 g((unsigned)p.n_chunks), b(kFlatThreads);
   const uint64_t size = (uint64_t)p.mask + 1;
   if (kind != CCJ_TABLE_LP) {
-    if (p.bucket && !getenv("CCJ_CHAIN_PAIR")) hipLaunchKernelGGL((probe_chain_win<3>), g, b, 0, s, p);
-    else hipLaunchKernelGGL((probe_pair<CCJ_TABLE_CHAIN, 4>), g, b, 0, s, p);
+    if (!p.bucket) return hipErrorInvalidValue;  // every chaining table carries bucket records
+    hipLaunchKernelGGL((probe_chain_win<3>), g, b, 0, s, p);
     return hipGetLastError();
   }
-  // CCJ_PROBE_VARIANT (tuning override, read per launch): pair4 | flat | wL_Wa_R / wL_Wu_R =
-  // probe_win<L lanes per row, W-slot windows, aligned (a) or from the next slot (u), R rows>.
-  // At C2 (profiles/r1e_*): w2_4u_3 10.5-10.8 ms (a lane pair reads the 4 slots from the row's next
-  // unread slot: 1.1 windows per row instead of 1.43), w2_4l_3 1 % less (the same, but a window
-  // that would cross a 128-byte line ends at it: one request; w2_4s_3, 64-byte sectors, 3 % more),
-  // w2_4a_4 11.6, w1_2u_3 11.6, w1_4u_2 11.8,
-  // pair4 12.1; w1_8a_2 15.5 and w2_8a_* 12.2 (wider windows cost more L2 time than they save).
-  // A persistent form of w2_4l_3 (4-8 workgroups per CU taking chunks from per-XCD atomic queue
-  // heads, walk_chunk in a loop) measured 11.8 ms against 10.6 (84 VGPRs, occupancy 5): the
-  // one-shot grid's workgroup turnover already hides each chunk's store drain.
-  const char *e = getenv("CCJ_PROBE_VARIANT");
-  const std::string v = e && *e ? e : "w2_4l_3";
-  if (p.out_pos) {  // C5: table positions of the matches for the payload gather (default walk)
-    if (size < 16) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((probe_win<2, 4, 3, false, true, 16>), g, b, 0, s, p);
-  } else if (size < 16 || v == "pair4") {
-    if (size >= 4) hipLaunchKernelGGL((probe_pair<CCJ_TABLE_LP, 4>), dim3((unsigned)p.n_chunks), b, 0, s, p);
-    else hipLaunchKernelGGL((probe_flat<CCJ_TABLE_LP, 2>), dim3((unsigned)p.n_chunks), b, 0, s, p);
-  } else if (v == "flat") {
-    hipLaunchKernelGGL((probe_flat<CCJ_TABLE_LP, 2>), dim3((unsigned)p.n_chunks), b, 0, s, p);
-  } else if (v == "w1_2u_3") {
-    hipLaunchKernelGGL((probe_win<1, 2, 3, false>), g, b, 0, s, p);
-  } else if (v == "w2_4a_4") {
-    hipLaunchKernelGGL((probe_win<2, 4, 4, true>), g, b, 0, s, p);
-  } else if (v == "w1_4u_2") {
-    hipLaunchKernelGGL((probe_win<1, 4, 2, false>), g, b, 0, s, p);
-  } else if (v == "w2_4s_3") {
-    hipLaunchKernelGGL((probe_win<2, 4, 3, false, false, 8>), g, b, 0, s, p);
-  } else if (v == "w2_4u_4") {
-    hipLaunchKernelGGL((probe_win<2, 4, 4, false>), g, b, 0, s, p);
-  } else if (v == "w2_4u_3") {
-    hipLaunchKernelGGL((probe_win<2, 4, 3, false>), g, b, 0, s, p);
-  } else {
-    hipLaunchKernelGGL((probe_win<2, 4, 3, false, false, 16>), g, b, 0, s, p);  // w2_4l_3
-  }
+  if (size < 16) return launch_probe(kind, p, s);  // a table of < 16 slots is one identity window
+  // At C2 (profiles/r2_*): probe_walk 9.4 ms against 9.9-10.1 for probe_win's per-step output
+  // placement; R = 2 / 3 / 4 / 6 rows per pair 9.65 / 9.4 / 9.7 / 10.9 ms, home slots staged in
+  // LDS 9.4 vs hashed at row start 9.6 ms; one lane per row with two 16-B loads (twice the L2
+  // requests) 11.0-12.3 ms; write-through (sc1) or plain output stores 10.2 ms vs non-temporal.
+  if (p.out_pos) hipLaunchKernelGGL((probe_win<3>), g, b, 0, s, p);  // C5: match positions too
+  else hipLaunchKernelGGL((probe_walk<3, true>), g, b, 0, s, p);
   return hipGetLastError();
 }
 
@@ -1621,7 +1493,6 @@ struct GatherParams {
   const uint64_t *out_base;
   uint64_t cap;
   const int64_t *pay;
-  const uint2 *rank;  // dense payload (ProbeParams::pay_rank)
   uint32_t stride;
   int64_t *cols[CCJ_MAX_PAYLOAD_COLS];
 };
@@ -1637,7 +1508,7 @@ __global__ __launch_bounds__(256) void gather_payload(GatherParams g) {
     for (int u = 0; u < 2; ++u) {
       const uint32_t j = j0 + u * 256;
       if (j < n) {
-        const int64_t *row = g.pay + pay_index(g.rank, g.pos[ob + j]) * g.stride;
+        const int64_t *row = g.pay + (uint64_t)g.pos[ob + j] * g.stride;
         if (VEC) {
 #pragma unroll
           for (int q = 0; q + 1 < NP; q += 2) {
@@ -1666,16 +1537,12 @@ __global__ __launch_bounds__(256) void gather_payload(GatherParams g) {
 // 8 columns, 64-byte rows: four lanes share a row, each loading 16 bytes of it, so one wave
 // instruction fetches 16 whole rows (one request per row instead of four); lane q then writes
 // columns 2q and 2q+1 of its row (16 consecutive rows per column per instruction).
-template <int U, bool NT, bool SWZ>
+template <int U>
 __global__ __launch_bounds__(256) void gather_payload_quad(GatherParams g) {
   __shared__ int64_t *s_cols[CCJ_MAX_PAYLOAD_COLS];
   if (threadIdx.x < CCJ_MAX_PAYLOAD_COLS) s_cols[threadIdx.x] = g.cols[threadIdx.x];
   __syncthreads();
-  uint64_t c = blockIdx.x;
-  if (SWZ) {  // the walk's XCD-swizzled chunk order: each XCD gathers its own range of partitions
-    const uint64_t n8 = (uint64_t)gridDim.x & ~7ull;
-    if (c < n8) c = (c & 7) * (n8 >> 3) + (c >> 3);
-  }
+  const uint64_t c = blockIdx.x;
   const uint64_t ob = g.out_base ? g.out_base[c] : c * g.cap;
   const uint32_t n = g.count[c];
   const uint32_t q = threadIdx.x & 3u, r0 = threadIdx.x >> 2;  // 64 rows per block step
@@ -1685,19 +1552,14 @@ __global__ __launch_bounds__(256) void gather_payload_quad(GatherParams g) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t j = base + u * 64 + r0;
-      if (j < n) v[u] = reinterpret_cast<const longlong2 *>(g.pay + pay_index(g.rank, g.pos[ob + j]) * g.stride)[q];
+      if (j < n) v[u] = reinterpret_cast<const longlong2 *>(g.pay + (uint64_t)g.pos[ob + j] * g.stride)[q];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t j = base + u * 64 + r0;
       if (j < n) {
-        if (NT) {
-          __builtin_nontemporal_store(v[u].x, c0 + ob + j);
-          __builtin_nontemporal_store(v[u].y, c1 + ob + j);
-        } else {
-          c0[ob + j] = v[u].x;
-          c1[ob + j] = v[u].y;
-        }
+        __builtin_nontemporal_store(v[u].x, c0 + ob + j);
+        __builtin_nontemporal_store(v[u].y, c1 + ob + j);
       }
     }
   }
@@ -1706,24 +1568,10 @@ __global__ __launch_bounds__(256) void gather_payload_quad(GatherParams g) {
 template <int NP>
 hipError_t launch_gather_np(const GatherParams &g, uint64_t n_chunks, hipStream_t s) {
   const bool vec = (g.stride % 2 == 0) && ((uintptr_t)g.pay % 16 == 0);
-  static const bool quad = getenv("CCJ_GATHER_SCALAR") == nullptr;
-  // tuning override (tools/sweep): CCJ_GATHER_VARIANT = U*100 + plain_stores*10 + swizzle
-  static const int gv = [] {
-    const char *e = getenv("CCJ_GATHER_VARIANT");
-    return e ? atoi(e) : 400;
-  }();
-  const dim3 gd((unsigned)n_chunks), bd(256);
-  if (NP == 8 && vec && quad) {
-    switch (gv) {
-      case 200: hipLaunchKernelGGL((gather_payload_quad<2, true, false>), gd, bd, 0, s, g); break;
-      case 800: hipLaunchKernelGGL((gather_payload_quad<8, true, false>), gd, bd, 0, s, g); break;
-      case 410: hipLaunchKernelGGL((gather_payload_quad<4, false, false>), gd, bd, 0, s, g); break;
-      case 401: hipLaunchKernelGGL((gather_payload_quad<4, true, true>), gd, bd, 0, s, g); break;
-      case 411: hipLaunchKernelGGL((gather_payload_quad<4, false, true>), gd, bd, 0, s, g); break;
-      case 801: hipLaunchKernelGGL((gather_payload_quad<8, true, true>), gd, bd, 0, s, g); break;
-      default: hipLaunchKernelGGL((gather_payload_quad<4, true, false>), gd, bd, 0, s, g); break;
-    }
-  } else if (vec) hipLaunchKernelGGL((gather_payload<NP, true>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
+  // 8 columns: 2 / 4 / 8 rows in flight per lane group 26.9 ms each at C5, the walk's XCD order
+  // 27.0, plain instead of non-temporal stores 27.8-28.9 (profiles/r1g_*)
+  if (NP == 8 && vec) hipLaunchKernelGGL((gather_payload_quad<4>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
+  else if (vec) hipLaunchKernelGGL((gather_payload<NP, true>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
   else hipLaunchKernelGGL((gather_payload<NP, false>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
   return hipGetLastError();
 }
@@ -1736,7 +1584,6 @@ hipError_t launch_gather_payload(const ProbeParams &p, const uint32_t *pos, hipS
   g.out_base = p.out_base;
   g.cap = p.cap;
   g.pay = p.pay;
-  g.rank = p.pay_rank;
   g.stride = p.pay_stride;
   for (uint32_t q = 0; q < p.n_pay; ++q) g.cols[q] = p.out_cols[q];
   switch (p.n_pay) {
@@ -1788,72 +1635,6 @@ hipError_t launch_lp_insert(const int64_t *keys, uint64_t n, int64_t *slots, uin
   return hipGetLastError();
 }
 
-// Dense payload (CCJ_PAY_DENSE): rank words over the table positions, then build rows stored by rank.
-__global__ void pay_rank_words(const uint32_t *row, uint64_t positions, uint2 *rank, uint32_t *cnt, uint64_t n_words) {
-  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < n_words; w += (uint64_t)gridDim.x * blockDim.x) {
-    uint32_t bits = 0;
-    for (uint32_t i = 0; i < 32; ++i) {
-      const uint64_t pos = w * 32 + i;
-      if (pos < positions && row[pos] != kNoRow) bits |= 1u << i;
-    }
-    rank[w].x = bits;
-    cnt[w] = (uint32_t)__popc(bits);
-  }
-}
-
-__global__ void pay_rank_fill(uint2 *rank, const uint32_t *pre, uint64_t n_words) {
-  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < n_words; w += (uint64_t)gridDim.x * blockDim.x)
-    rank[w].y = pre[w];
-}
-
-__global__ void scatter_payload_dense(const int64_t *src, uint32_t n_cols, const uint32_t *row, uint64_t positions,
-                                      const uint2 *rank, int64_t *dst) {
-  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < positions * n_cols;
-       t += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t pos = t / n_cols, c = t - pos * n_cols;
-    const uint32_t r = row[pos];
-    if (r != kNoRow) dst[pay_index(rank, (uint32_t)pos) * n_cols + c] = src[(uint64_t)r * n_cols + c];
-  }
-}
-
-hipError_t launch_dense_payload(const int64_t *src, uint32_t n_cols, const uint32_t *row, uint64_t positions,
-                                uint2 *rank, int64_t **dst, uint64_t *n_dense, hipStream_t s) {
-  *dst = nullptr;
-  *n_dense = 0;
-  const uint64_t n_words = (positions + 31) / 32;
-  if (n_words == 0) return hipSuccess;
-  uint32_t *cnt = nullptr, *pre = nullptr;
-  void *tmp = nullptr;
-  size_t tmp_bytes = 0;
-  hipError_t e = hipMalloc(&cnt, n_words * 4 * 2);
-  if (e) return e;
-  pre = cnt + n_words;
-  hipLaunchKernelGGL(pay_rank_words, dim3(grid_for(n_words, 256)), dim3(256), 0, s, row, positions, rank, cnt, n_words);
-  e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, pre, (int)n_words, s);
-  if (!e) e = hipMalloc(&tmp, tmp_bytes);
-  if (!e) e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, pre, (int)n_words, s);
-  if (!e) hipLaunchKernelGGL(pay_rank_fill, dim3(grid_for(n_words, 256)), dim3(256), 0, s, rank, pre, n_words);
-  uint32_t last[2] = {0, 0};
-  if (!e) e = hipMemcpyAsync(&last[0], pre + n_words - 1, 4, hipMemcpyDeviceToHost, s);
-  if (!e) e = hipMemcpyAsync(&last[1], cnt + n_words - 1, 4, hipMemcpyDeviceToHost, s);
-  if (!e) e = hipStreamSynchronize(s);
-  const uint64_t total = (uint64_t)last[0] + last[1];
-  if (!e && total) e = hipMalloc((void **)dst, total * n_cols * sizeof(int64_t));
-  if (!e && total)
-    hipLaunchKernelGGL(scatter_payload_dense, dim3(grid_for(positions * n_cols, 256)), dim3(256), 0, s, src, n_cols, row,
-                       positions, rank, *dst);
-  if (!e) e = hipGetLastError();
-  if (!e) e = hipStreamSynchronize(s);
-  (void)hipFree(tmp);
-  (void)hipFree(cnt);
-  if (e && *dst) {
-    (void)hipFree(*dst);
-    *dst = nullptr;
-  }
-  *n_dense = e ? 0 : total;
-  return e;
-}
-
 hipError_t launch_scatter_payload(const int64_t *src, uint32_t n_cols, const uint32_t *row, uint64_t positions,
                                   int64_t *dst, hipStream_t s) {
   if (positions == 0 || n_cols == 0) return hipSuccess;
@@ -1863,9 +1644,10 @@ hipError_t launch_scatter_payload(const int64_t *src, uint32_t n_cols, const uin
 }
 
 hipError_t launch_gen_c3(int64_t *out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t n_build, uint64_t cf,
-                         uint32_t hit_ppm, hipStream_t s) {
+                         uint32_t hit_ppm, const uint32_t *zipf, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(gen_c3, dim3(grid_for(n, 256)), dim3(256), 0, s, out, n, seed, first_row, n_build, cf, hit_ppm);
+  hipLaunchKernelGGL(gen_c3, dim3(grid_for(n, 256)), dim3(256), 0, s, out, n, seed, first_row, n_build, cf, hit_ppm,
+                     zipf);
   return hipGetLastError();
 }
 

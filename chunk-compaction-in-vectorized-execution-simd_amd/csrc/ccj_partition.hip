@@ -20,6 +20,7 @@
 #include <cmath>
 
 #include "ccj_internal.h"
+#include "ccj_tuning.h"
 
 namespace ccj {
 namespace {
@@ -264,11 +265,8 @@ hipError_t launch_segment_chunk_counts(const uint64_t *counts, uint32_t n_segs, 
 
 // ---- slot-range partitioning for the L2-resident probe ------------------------------------------
 SlotPlan slot_plan(uint64_t table_size, int kind) {
-  // CCJ_WINDOW_BITS (tuning override): log2 slots of table per partition.
-  static const uint32_t wbits = [] {
-    const char *e = getenv("CCJ_WINDOW_BITS");
-    return e ? (uint32_t)atoi(e) : kWindowBits;
-  }();
+  // log2 slots of table per partition (the tuning build sweeps CCJ_WINDOW_BITS)
+  const uint32_t wbits = (uint32_t)ccj_tune_int("CCJ_WINDOW_BITS", (int)kWindowBits);
   SlotPlan pl{};
   const uint32_t sbits = log2u(table_size);  // table_size is a power of two
   const uint32_t wb = kind == CCJ_TABLE_CHAIN && wbits > 0 ? wbits - 1 : wbits;
@@ -299,7 +297,7 @@ constexpr int kSplitPer = 11;  // CCJ_SPLIT_PER sweep at C2: 8-13 keys -> 6.35 6
 constexpr uint32_t kSplitParts = 1u << kSplitPartBits;
 static_assert(kSplitParts <= (uint32_t)kSplitThreads, "one partition per thread in the scan");
 
-template <bool COUNTS, int THREADS, int MAXP, int PER, bool SD = false>
+template <bool COUNTS, int THREADS, int MAXP, int PER>
 __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys, uint64_t n, uint32_t shift,
                                                                  uint32_t parts, uint64_t n_tiles, uint32_t *cur,
                                                                  uint64_t cap, uint64_t ovf_base, uint64_t ovf_cap,
@@ -309,8 +307,9 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
   static_assert(MAXP <= THREADS, "one partition per thread in the scan");
   __shared__ int64_t s_k[kTileKeys];
   __shared__ uint32_t s_ovf[MAXP], s_olim[MAXP];  // overflow-area run: start, length
-  // image row: tile-local row (16 bits), with SD also its partition (bits 16+: no second hash)
-  __shared__ std::conditional_t<SD, uint32_t, uint16_t> s_i[kTileKeys];
+  // image row: tile-local row (16 bits); the partition is re-hashed when the row is written (keeping
+  // it beside the row measured the same)
+  __shared__ uint16_t s_i[kTileKeys];
   __shared__ uint32_t s_hist[MAXP], s_loc[MAXP], s_lim[MAXP];
   __shared__ uint64_t s_dst[MAXP];
   __shared__ uint32_t s_wsum[THREADS / 64], s_tot;
@@ -335,7 +334,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
         in = pos - c * chunk < counts[c];
       }
       live |= (in ? 1u : 0u) << it;
-      if (ablate & 0x20u) kk[it] = (int64_t)((t0 + li) * 0x9E3779B97F4A7C15ull >> 20);  // timing only: no key reads
+      if CCJ_ABLATED(ablate, 0x20u) kk[it] = (int64_t)((t0 + li) * 0x9E3779B97F4A7C15ull >> 20);  // timing only: no key reads
       else kk[it] = in ? __builtin_nontemporal_load(keys + t0 + li) : 0;
     }
   };
@@ -361,7 +360,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
       if (lane >= (uint32_t)o) incl += v;
     }
     if (lane == 63) s_wsum[wave] = incl;
-    const uint32_t r = h && !(ablate & 0x40u) ? atomicAdd(&cur[(uint64_t)g * parts + tid], h) : 0u;  // flies during the image build
+    const uint32_t r = h && !CCJ_ABLATED(ablate, 0x40u) ? atomicAdd(&cur[(uint64_t)g * parts + tid], h) : 0u;  // flies during the image build
     __syncthreads();
     uint32_t wpre = 0;
     for (uint32_t w = 0; w < wave; ++w) wpre += s_wsum[w];
@@ -374,8 +373,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
       if ((live >> it) & 1u) {
         const uint32_t pos = s_loc[dd[it]] + rk[it];
         s_k[pos] = kk[it];
-        if constexpr (SD) s_i[pos] = li | dd[it] << 16;
-        else s_i[pos] = (uint16_t)li;
+        s_i[pos] = (uint16_t)li;
       }
     }
     if (tid < parts) {
@@ -399,10 +397,10 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
     for (uint32_t q = tid; q < tl; q += THREADS) {
       const int64_t k = s_k[q];
       const uint32_t si = s_i[q];
-      const uint32_t d = SD ? si >> 16 : (uint32_t)(murmurhash64((uint64_t)k) >> shift) & mask;
+      const uint32_t d = (uint32_t)(murmurhash64((uint64_t)k) >> shift) & mask;
       const uint32_t o = q - s_loc[d];
       const uint32_t lim = s_lim[d];
-      if ((o < lim || o - lim < s_olim[d]) && !(ablate & 0x10u)) {  // (0x10: timing only, no stores)
+      if ((o < lim || o - lim < s_olim[d]) && !CCJ_ABLATED(ablate, 0x10u)) {  // (0x10: timing only, no stores)
         const uint64_t dest = o < lim ? s_dst[d] + o : ovf_base + s_ovf[d] + (o - lim);
         out_k[dest] = k;  // plain stores: the L2 merges neighbouring runs' partial lines
         out_r[dest] = (uint32_t)(t0 + (si & 0xFFFFu));  // (non-temporal stores measured the same)
@@ -439,61 +437,26 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
     (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
     return (unsigned)(n >= 8 ? n / 8 * 8 : 8);
   }();
-  const char *ab = getenv("CCJ_ABLATE");  // timing-only ablations (never set in product calls)
-  const uint32_t ablate = ab ? (uint32_t)atoi(ab) : 0u;
-  // keys per thread per tile: 11 (11264-key tiles, 141 KB of LDS); CCJ_SPLIT_PER = 8 ... 13 is a
-  // tuning override (13: longer runs per partition, 162 KB of the CU's 160 KiB, and slower)
-  uint32_t per = kSplitPer;
-  if (const char *e = getenv("CCJ_SPLIT_PER")) {
-    const uint32_t v = (uint32_t)atoi(e);
-    if (v >= 8 && v <= 13) per = v;
-  }
-  const uint32_t tile = (uint32_t)kSplitThreads * per;
+  const uint32_t ablate = (uint32_t)ccj_tune_int("CCJ_ABLATE", 0);  // timing-only (tuning build)
+  // keys per thread per tile: 11 (11264-key tiles, 141 KB of LDS); the tuning build sweeps 10-12
+  const int per = ccj_tune_int("CCJ_SPLIT_PER", kSplitPer);
+  const uint32_t tile = (uint32_t)kSplitThreads * (uint32_t)per;
   const uint64_t n_tiles = (n + tile - 1) / tile;
-  unsigned nb = cus;
-  if (const char *e = getenv("CCJ_SPLIT_BLOCKS")) {  // tuning override: fewer persistent workgroups
-    const unsigned v = (unsigned)atoi(e) / 8 * 8;
-    if (v >= 8 && v <= nb) nb = v;
-  }
 #define CCJ_SPLIT_LAUNCH(C, P)                                                                                      \
-  hipLaunchKernelGGL((slot_split_fixed<C, kSplitThreads, kSplitParts, P>), dim3(nb), dim3(kSplitThreads), 0, s, keys, n, \
+  hipLaunchKernelGGL((slot_split_fixed<C, kSplitThreads, kSplitParts, P>), dim3(cus), dim3(kSplitThreads), 0, s, keys, n, \
                      pl.window_bits, parts, n_tiles, cursors, cap, ovf_base, ovf_cap, out_keys, out_rows, status, ablate, \
                      counts, chunk)
-#define CCJ_SPLIT_LAUNCH_SD(C, P)                                                                                   \
-  hipLaunchKernelGGL((slot_split_fixed<C, kSplitThreads, kSplitParts, P, true>), dim3(nb), dim3(kSplitThreads), 0, s, keys, \
-                     n, pl.window_bits, parts, n_tiles, cursors, cap, ovf_base, ovf_cap, out_keys, out_rows, status,     \
-                     ablate, counts, chunk)
-#define CCJ_SPLIT_PER_CASE(P) \
-  case P:                     \
-    if (counts)               \
-      CCJ_SPLIT_LAUNCH(true, P); \
-    else                      \
-      CCJ_SPLIT_LAUNCH(false, P); \
-    break;
-  const char *sd = getenv("CCJ_SPLIT_SD");  // tuning override: partition kept beside the image row
-  if (sd && atoi(sd) && (per == 9 || per == 10)) {
-    if (per == 9) {
-      if (counts) CCJ_SPLIT_LAUNCH_SD(true, 9);
-      else CCJ_SPLIT_LAUNCH_SD(false, 9);
-    } else {
-      if (counts) CCJ_SPLIT_LAUNCH_SD(true, 10);
-      else CCJ_SPLIT_LAUNCH_SD(false, 10);
-    }
-    return hipGetLastError();
+  if (per == 10) {
+    if (counts) CCJ_SPLIT_LAUNCH(true, 10);
+    else CCJ_SPLIT_LAUNCH(false, 10);
+  } else if (per == 12) {
+    if (counts) CCJ_SPLIT_LAUNCH(true, 12);
+    else CCJ_SPLIT_LAUNCH(false, 12);
+  } else {
+    if (counts) CCJ_SPLIT_LAUNCH(true, kSplitPer);
+    else CCJ_SPLIT_LAUNCH(false, kSplitPer);
   }
-  switch (per) {
-    CCJ_SPLIT_PER_CASE(8)
-    CCJ_SPLIT_PER_CASE(9)
-    CCJ_SPLIT_PER_CASE(10)
-    CCJ_SPLIT_PER_CASE(12)
-    CCJ_SPLIT_PER_CASE(13)
-    default:
-      if (counts) CCJ_SPLIT_LAUNCH(true, kSplitPer);
-      else CCJ_SPLIT_LAUNCH(false, kSplitPer);
-  }
-#undef CCJ_SPLIT_PER_CASE
 #undef CCJ_SPLIT_LAUNCH
-#undef CCJ_SPLIT_LAUNCH_SD
   return hipGetLastError();
 }
 

@@ -51,23 +51,49 @@ static inline uint64_t ccj_perm(uint64_t x, uint64_t n, uint64_t seed) {
   return x;
 }
 
+/* Zipf s = 1 over ranks 1..n ("Zipf s=1.0 over 2^26 ranks") as a 2^16-bucket
+ * inverse CDF: T[j] = the smallest rank r whose CDF H_r / H_n exceeds j / 2^16, T[2^16] = n + 1
+ * (T has 2^16 + 1 entries; n < 2^32).  A draw takes bucket j from the top 16 bits of a random word
+ * and a rank uniform over the bucket's ranks [T[j], max(T[j], T[j+1] - 1)]: rank 1 alone holds
+ * 1 / H_n of the buckets (5.4 % at n = 2^26), and where a bucket spans several ranks their 1 / r
+ * weights differ by at most the bucket's width / r (< 0.03 % at n = 2^26).  Plain IEEE double
+ * sums and products of exactly-representable operands, so every compiler builds the same table;
+ * the device generator (csrc/ccj_api.hip) builds it the same way. */
+#define CCJ_ZIPF_BITS 16
+#define CCJ_ZIPF_BUCKETS (1u << CCJ_ZIPF_BITS)
+static inline void ccj_zipf_table(uint64_t n, uint32_t *T) {
+  double hn = 0.0;
+  for (uint64_t r = 1; r <= n; ++r) hn += 1.0 / (double)r;
+  uint32_t j = 0;
+  double h = 0.0;
+  for (uint64_t r = 1; r <= n && j < CCJ_ZIPF_BUCKETS; ++r) {
+    h += 1.0 / (double)r;
+    while (j < CCJ_ZIPF_BUCKETS && h * (double)CCJ_ZIPF_BUCKETS > (double)j * hn) T[j++] = (uint32_t)r;
+  }
+  while (j < CCJ_ZIPF_BUCKETS) T[j++] = (uint32_t)(n ? n : 1);
+  T[CCJ_ZIPF_BUCKETS] = (uint32_t)(n + 1);
+}
+
+/* Zipf rank in [1, n] from random word z and table T (ccj_zipf_table). */
+static inline uint64_t ccj_zipf_rank(const uint32_t *T, uint64_t z) {
+  const uint32_t j = (uint32_t)(z >> (64 - CCJ_ZIPF_BITS));
+  const uint64_t lo = T[j], hi = T[j + 1] > T[j] ? (uint64_t)T[j + 1] - 1 : lo;
+  return lo + (z & 0xffffffffULL) % (hi - lo + 1);
+}
+
 /* Row i of the C3 stream over the reference generator's build side (n_build, cf): with
- * probability hit_ppm / 1e6 a build key whose rank r in [1, n_unique] is log-uniform over dyadic
- * levels (a bit length b uniform in [1, bitlen(n_unique)], r uniform in that level: the
- * integer-only stand-in for Zipf s = 1, density ~ 1/r), mapped through ccj_perm so the popular
- * keys spread over the table; otherwise a key in [n_build, 2^62), which is never a build key
- * (every build key is < n_build, linear_probing_ht.cpp:16-25). */
-static inline int64_t ccj_c3_key(uint64_t seed, uint64_t i, uint64_t n_build, uint64_t cf, uint32_t hit_ppm) {
+ * probability hit_ppm / 1e6 a build key whose rank r in [1, n_unique] is Zipf (s = 1) distributed
+ * (zipf = ccj_zipf_table(n_unique)), mapped through ccj_perm so the popular keys spread over the
+ * table; otherwise a key in [n_build, 2^62), which is never a build key (every build key is
+ * < n_build, linear_probing_ht.cpp:16-25). */
+static inline int64_t ccj_c3_key(const uint32_t *zipf, uint64_t seed, uint64_t i, uint64_t n_build, uint64_t cf,
+                                 uint32_t hit_ppm) {
   const uint64_t z1 = ccj_splitmix_at(seed, 3 * i), z2 = ccj_splitmix_at(seed, 3 * i + 1);
   const uint64_t z3 = ccj_splitmix_at(seed, 3 * i + 2);
   const uint64_t n_unique = n_build / cf + (n_build % cf != 0);
   if (z1 % 1000000ULL < hit_ppm && n_unique) {
     const uint64_t step = n_build / n_unique;
-    const uint32_t levels = ccj_bitlen(n_unique);
-    const uint32_t b = (uint32_t)((z2 >> 32) % levels); /* rank bit length b + 1 */
-    const uint64_t lo = 1ULL << b;
-    const uint64_t hi = (b + 1 < 64 && (2ULL << b) - 1 < n_unique) ? (2ULL << b) - 1 : n_unique;
-    const uint64_t r = lo + (z2 & 0xffffffffULL) % (hi - lo + 1);
+    const uint64_t r = ccj_zipf_rank(zipf, z2);
     return (int64_t)(ccj_perm(r - 1, n_unique, seed) * step);
   }
   return (int64_t)(n_build + z3 % ((1ULL << 62) - n_build));

@@ -259,24 +259,36 @@ uint64_t ccj_o_count_uniform(uint64_t seed, uint64_t row_begin, uint64_t row_end
   return matches;
 }
 
+/* Zipf table of the C3 stream over n_build keys of multiplicity cf (ccj_gen.h ccj_zipf_table). */
+static uint32_t *c3_zipf(uint64_t n_build, uint64_t cf) {
+  const uint64_t n_unique = n_build / cf + (n_build % cf != 0);
+  uint32_t *t = (uint32_t *)malloc((CCJ_ZIPF_BUCKETS + 1) * sizeof(uint32_t));
+  ccj_zipf_table(n_unique, t);
+  return t;
+}
+
 void ccj_o_gen_c3(uint64_t seed, uint64_t row_begin, uint64_t n, uint64_t n_build, uint64_t cf, uint32_t hit_ppm,
                   int64_t *out, int threads) {
   if (threads <= 0) threads = omp_get_max_threads();
+  uint32_t *zipf = c3_zipf(n_build, cf);
 #pragma omp parallel for num_threads(threads) schedule(static)
-  for (uint64_t i = 0; i < n; ++i) out[i] = ccj_c3_key(seed, row_begin + i, n_build, cf, hit_ppm);
+  for (uint64_t i = 0; i < n; ++i) out[i] = ccj_c3_key(zipf, seed, row_begin + i, n_build, cf, hit_ppm);
+  free(zipf);
 }
 
 uint64_t ccj_o_count_c3(uint64_t seed, uint64_t row_begin, uint64_t row_end, uint64_t n_build, uint64_t cf,
                         uint32_t hit_ppm, uint64_t *l2_out, int threads) {
   uint64_t matches = 0, l2 = 0;
   if (threads <= 0) threads = omp_get_max_threads();
+  uint32_t *zipf = c3_zipf(n_build, cf);
 #pragma omp parallel for num_threads(threads) schedule(static) reduction(+ : matches, l2)
   for (uint64_t i = row_begin; i < row_end; ++i) {
-    int64_t k = ccj_c3_key(seed, i, n_build, cf, hit_ppm);
+    int64_t k = ccj_c3_key(zipf, seed, i, n_build, cf, hit_ppm);
     uint64_t m = ccj_o_ref_multiplicity(k, n_build, cf);
     matches += m;
     l2 += m * ccj_l2_term(i, k);
   }
+  free(zipf);
   if (l2_out) *l2_out = l2;
   return matches;
 }
@@ -321,4 +333,30 @@ uint64_t ccj_o_compact_plan_threshold(const uint32_t *seg_counts, uint64_t n_seg
 uint64_t ccj_o_compact_plan(const uint32_t *seg_counts, uint64_t n_segs, uint32_t chunk, uint64_t *dest,
                             uint32_t *out_chunk_counts) {
   return ccj_o_compact_plan_threshold(seg_counts, n_segs, chunk, chunk, dest, out_chunk_counts);
+}
+
+void ccj_o_gen_mt64(uint64_t seed, uint64_t n, uint64_t range, int64_t *out) {
+  ccj_mt19937_64 g;
+  ccj_mt19937_64_seed(&g, seed);
+  for (uint64_t i = 0; i < n; ++i) out[i] = (int64_t)(ccj_mt19937_64_next(&g) % range);
+}
+
+void ccj_o_result_sums(const uint32_t *count, const uint32_t *sel, const int64_t *payload, uint64_t n_chunks,
+                       uint64_t cap, uint32_t chunk, uint64_t *out) {
+  uint64_t m = 0, l2 = 0, l3 = CCJ_L3_SEED, chk = 0;
+  for (uint64_t c = 0; c < n_chunks; ++c) {
+    for (uint32_t j = 0; j < count[c]; ++j) {
+      const uint32_t s = sel[c * cap + j];
+      const int64_t p = payload[c * cap + j];
+      const uint64_t row = c * chunk + s;
+      ++m;
+      l2 += ccj_l2_term(row, p);
+      l3 = ccj_l3_fold(l3, row, p);
+      chk += (uint64_t)p * 1315423911ULL + s;
+    }
+  }
+  out[0] = m;
+  out[1] = l2;
+  out[2] = l3;
+  out[3] = chk;
 }

@@ -80,6 +80,15 @@ uint64_t ccj_o_compact_plan(const uint32_t *seg_counts, uint64_t n_segs, uint32_
 uint64_t ccj_o_compact_plan_threshold(const uint32_t *seg_counts, uint64_t n_segs, uint32_t chunk,
                                       uint32_t threshold, uint64_t *dest, uint32_t *out_chunk_counts);
 
+/* The SURVEY §4 driver's probe stream: mt19937_64(seed) % range, n keys (ref_driver.cpp RunProbe
+ * gen 1; the reference's own sources draw the keys the same way). */
+void ccj_o_gen_mt64(uint64_t seed, uint64_t n, uint64_t range, int64_t *out);
+/* The reference driver's sink (ref_driver.cpp Sink::Emit) over a probe output in its stored
+ * order: chunk c's matches are sel/payload[c*cap, c*cap + count[c]).  out[0..3] = matches, L2,
+ * L3 fold, SURVEY chk (ccj_gen.h), with global row = c * chunk + sel. */
+void ccj_o_result_sums(const uint32_t *count, const uint32_t *sel, const int64_t *payload, uint64_t n_chunks,
+                       uint64_t cap, uint32_t chunk, uint64_t *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -61,6 +61,8 @@ def lib():
         L.ccj_o_compact_plan.argtypes = [u32p, u64, C.c_uint32, u64p, u32p]
         L.ccj_o_compact_plan_threshold.restype = u64
         L.ccj_o_compact_plan_threshold.argtypes = [u32p, u64, C.c_uint32, C.c_uint32, u64p, u32p]
+        L.ccj_o_gen_mt64.argtypes = [u64, u64, u64, i64p]
+        L.ccj_o_result_sums.argtypes = [u32p, u32p, i64p, u64, u64, C.c_uint32, u64p]
     return _LIB
 
 
@@ -153,6 +155,25 @@ def c3_keys(seed, begin, end, n_build, cf, hit_ppm=100000, threads=0):
     out = np.empty(end - begin, dtype=np.int64)
     lib().ccj_o_gen_c3(seed, begin, end - begin, n_build, cf, hit_ppm, _p(out, C.c_int64), threads)
     return out
+
+
+def mt64_keys(seed, n, rng):
+    """The SURVEY §4 driver's probe keys: mt19937_64(seed) % rng (ccj_o_gen_mt64)."""
+    out = np.empty(n, dtype=np.int64)
+    lib().ccj_o_gen_mt64(seed, n, rng, _p(out, C.c_int64))
+    return out
+
+
+def result_sums(count, sel, payload, cap, chunk):
+    """(matches, L2, L3, SURVEY chk) of a probe output in stored order — the reference driver's
+    sink (oracle/ref_driver.cpp Sink::Emit), so they compare directly with known_answers.json."""
+    count = np.ascontiguousarray(count).view(np.uint32)
+    sel = np.ascontiguousarray(sel).view(np.uint32)
+    payload = np.ascontiguousarray(payload, dtype=np.int64)
+    out = np.zeros(4, np.uint64)
+    lib().ccj_o_result_sums(_p(count, C.c_uint32), _p(sel, C.c_uint32), _p(payload, C.c_int64), len(count), cap,
+                            chunk, _p(out, C.c_uint64))
+    return tuple(int(x) for x in out)
 
 
 def count_c3(seed, begin, end, n_build, cf, hit_ppm=100000, threads=0):

@@ -279,8 +279,10 @@ template <typename Table>
 void BenchProbe(Table &ht, Variant v, size_t n_probe, uint64_t range, uint64_t seed, bool c3, size_t n_build,
                 size_t cf) {
   std::vector<int64_t> keys(n_probe);
+  std::vector<uint32_t> zipf(CCJ_ZIPF_BUCKETS + 1);
+  if (c3) ccj_zipf_table(n_build / cf + (n_build % cf != 0), zipf.data());
   for (size_t i = 0; i < n_probe; ++i)
-    keys[i] = c3 ? ccj_c3_key(seed, i, n_build, cf, 100000) : ccj_uniform_key(seed, i, range);
+    keys[i] = c3 ? ccj_c3_key(zipf.data(), seed, i, n_build, cf, 100000) : ccj_uniform_key(seed, i, range);
   std::vector<AttributeType> in_types{AttributeType::INTEGER};
   std::vector<AttributeType> out_types{AttributeType::INTEGER, AttributeType::INTEGER, AttributeType::INTEGER};
   DataChunk input(in_types);

@@ -161,3 +161,180 @@ def test_fixed_capacity_exchange_gloo(world):
         assert p.exitcode == 0
     n_build, cf, n_probe, rng, seed = cfg
     assert got == O.count_uniform(seed, 0, world * n_probe, rng, n_build, cf)
+
+
+# ---- the pipelined ShardedProbe protocol itself, on CPU: same class, oracle-backed kernels ----
+
+class HostOps:
+    """ccj_dist's ops interface on CPU tensors: numpy stand-ins for the owner split, the segment
+    chunk counts and the slot-partitioned local probe (a permuted layout with a row map, probed
+    by the oracle).  `local_overflow` makes this rank's local probe raise the slot-split overflow
+    flag (ccj.FLAG_PART_OVERFLOW), as the one-pass split does under skew."""
+
+    def __init__(self, local_overflow=False):
+        import ccj_dist
+        self.base = ccj_dist.HostOpsBase()
+        self.local_overflow = local_overflow
+        self.probes = 0
+
+    def __getattr__(self, name):
+        return getattr(self.base, name)
+
+    def build_local(self, n_build_total, cf, world, rank, stream):
+        from oracle import oracle as O
+        build = O.ref_build_keys(n_build_total, cf)
+        own = build[np_owner(build, world) == rank]
+        self.table, self.cf = O.Table(O.LP, own), cf
+        return len(own)
+
+    def fixed_partitioner(self, n, world, seg_cap):
+        def run(keys, row_base, sk, sr, sc, status, stream):
+            k = keys.numpy()
+            owner = np_owner(k, world)
+            for d in range(world):
+                idx = np.nonzero(owner == d)[0]
+                sc[d] = len(idx)
+                keep = idx[:seg_cap]
+                sk[d * seg_cap:d * seg_cap + len(keep)] = torch.from_numpy(k[keep])
+                sr[d * seg_cap:d * seg_cap + len(keep)] = torch.from_numpy((row_base + keep).astype(np.int32))
+                if len(idx) > seg_cap:
+                    status |= 1  # CCJ_FLAG_CAP_OVERFLOW
+        return run
+
+    def segment_chunk_counts(self, seg_counts, seg_cap, chunk, out, status, stream):
+        per = seg_cap // chunk
+        for g, live in enumerate(seg_counts.tolist()):
+            if live > seg_cap:
+                status |= 1
+                live = seg_cap
+            for j in range(per):
+                out[g * per + j] = max(0, min(chunk, live - j * chunk))
+
+    def alloc_group(self, gslots, chunk, status):
+        return {"row_map": None}, {"status": status}
+
+    def probe_group(self, keys, counts, part, out, chunk, stream):
+        """Live rows permuted by home slot (the slot split's layout), probed chunk by chunk."""
+        from oracle import oracle as O
+        self.probes += 1
+        k, cnt = keys.numpy(), counts.numpy()
+        live = np.concatenate([c * chunk + np.arange(int(n)) for c, n in enumerate(cnt)] + [np.zeros(0, np.int64)])
+        order = live[np.argsort(O_hash(k[live]) & np.uint64(self.table.size - 1), kind="stable")]
+        part["row_map"] = order
+        n = len(order)
+        new_counts = np.array([min(chunk, n - c * chunk) for c in range(-(-n // chunk))], np.uint32)
+        res = self.table.probe(k[order], chunk, counts=new_counts if n else None, cap_factor=self.cf, max_rounds=4096)
+        out.update(count=res["count"], sel=res["sel"], payload=res["payload"], cap=res["cap"])
+        if self.local_overflow:
+            out["status"] |= 8  # CCJ_FLAG_PART_OVERFLOW
+
+    def group_rows(self, part, recv_rows, n_probe, seg_cap, slots, stream):
+        q = np.arange(recv_rows.numel()) % slots
+        recv = (q // seg_cap) * n_probe + recv_rows.numpy().astype(np.int64)
+        return recv[part["row_map"]]
+
+    def checksum(self, out, chunk, row_map, stream):
+        from oracle import oracle as O
+        rm = row_map.numpy() if isinstance(row_map, torch.Tensor) else row_map
+        m, l2 = 0, 0
+        for c in range(len(out["count"])):
+            k = int(out["count"][c])
+            sel = out["sel"][c * out["cap"]:c * out["cap"] + k].astype(np.int64)
+            m += k
+            l2 = (l2 + O.l2_sum(rm[c * chunk + sel].astype(np.uint64), out["payload"][c * out["cap"]:c * out["cap"] + k])) \
+                % (1 << 64)
+        return m, l2
+
+    def owner_partitioner(self, n, world):
+        def run(keys, row_base, stream):
+            k = keys.numpy()
+            owner = np_owner(k, world)
+            order = np.argsort(owner, kind="stable")
+            return (torch.from_numpy(k[order]), torch.from_numpy(row_base + order.astype(np.int64)),
+                    torch.from_numpy(np.bincount(owner, minlength=world).astype(np.int64)))
+        return run
+
+    def probe_exact(self, keys, chunk, stream):
+        res = self.table.probe(keys.numpy(), chunk, cap_factor=self.cf, max_rounds=4096)
+        return dict(count=res["count"], sel=res["sel"], payload=res["payload"], cap=res["cap"])
+
+
+def O_hash(k):
+    return np_hash(k)
+
+
+def _sharded_worker(rank, world, port, cfg, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "chunk-compaction-in-vectorized-execution-simd_amd"),
+                    os.path.join(root, "tests")]
+    from oracle import oracle as O
+    import ccj_dist
+    from test_dist_cpu import HostOps
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n_build, cf, n_probe, rng, seed, chunk, batches, group, skew_rank, local_ovf_rank = cfg
+    ops = HostOps(local_overflow=(rank == local_ovf_rank))
+    sp = ccj_dist.ShardedProbe(n_build, cf, n_probe, chunk, world, rank, batches=batches, ops=ops, group=group)
+    keys = O.uniform_keys(seed, rank * n_probe, (rank + 1) * n_probe, rng)
+    if rank == skew_rank:  # one hot key: its owner's send segment overflows on this rank only
+        keys[:] = keys[0]
+    res = []
+    for _ in range(2):
+        m, l2 = sp.step(torch.from_numpy(keys), rank * n_probe, verify=True)
+        res.append((m, l2, sp.last_exact))
+    tot = torch.tensor([m, l2 - (1 << 64) if l2 >= (1 << 63) else l2], dtype=torch.int64)
+    dist.all_reduce(tot)
+    # the exact answer for this rank's stream (full build side, global rows)
+    want = O.Table(O.LP, O.ref_build_keys(n_build, cf)).probe_totals(keys, chunk, row_base=rank * n_probe)
+    wt = torch.tensor([want[0], want[1] - (1 << 64) if want[1] >= (1 << 63) else want[1]], dtype=torch.int64)
+    dist.all_reduce(wt)
+    q.put((rank, int(tot[0]), int(tot[1]) % (1 << 64), int(wt[0]), int(wt[1]) % (1 << 64),
+           [r[2] for r in res], sp.batches, sp.n_groups, ops.probes))
+    dist.destroy_process_group()
+
+
+def _run_sharded(world, cfg, timeout=240):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, cfg, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        got = sorted(q.get(timeout=timeout) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():  # a diverged collective sequence hangs: never leave it running
+                p.kill()
+    for p in procs:
+        assert p.exitcode == 0
+    return got
+
+
+@pytest.mark.parametrize("world,batches,group", [(2, 3, 2), (2, 4, 8), (4, 5, 2)])
+def test_sharded_probe_protocol_gloo(world, batches, group):
+    """ShardedProbe.step end to end with gloo: batching, double-buffered send slots, receive-group
+    slots (short last group included), group_row_map and the verify checksum; L1 + L2 equal the
+    exact answer over all ranks' streams and no rank falls back."""
+    cfg = (1 << 13, 2, 3 << 12, 3 << 12, 21, 256, batches, group, -1, -1)
+    got = _run_sharded(world, cfg)
+    for rank, m, l2, wm, wl2, exact, nb, ng, probes in got:
+        assert (m, l2) == (wm, wl2)
+        assert exact == [False, False]
+        assert nb == batches and ng == -(-batches // min(batches, group)) and probes == 2 * ng
+
+
+@pytest.mark.parametrize("world,skew_rank,local_ovf_rank", [(2, 0, -1), (2, -1, 1), (4, 2, -1)])
+def test_sharded_overflow_on_one_rank_all_fall_back(world, skew_rank, local_ovf_rank):
+    """An overflow seen by ONE rank only (a hot key overflowing its send segment, or the local
+    probe's slot split overflowing) makes EVERY rank redo the step with the exact-size protocol:
+    the status word is all-reduced before the branch, so no collective sequence diverges (a hang
+    here is caught by the queue timeout).  Results stay exact."""
+    cfg = (1 << 13, 2, 3 << 12, 3 << 12, 22, 256, 3, 2, skew_rank, local_ovf_rank)
+    got = _run_sharded(world, cfg)
+    for rank, m, l2, wm, wl2, exact, nb, ng, probes in got:
+        assert (m, l2) == (wm, wl2)
+        assert exact == [True, True]

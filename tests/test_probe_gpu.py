@@ -178,20 +178,37 @@ def test_partitioned_probe_l1_l2(n_build, cf, n_probe, rng, exact):
         assert np.array_equal(np.sort(rm), np.arange(n_probe, dtype=np.uint32))
 
 
-@pytest.mark.parametrize("variant", ["w2_4l_3", "w2_4s_3", "w2_4u_3", "w2_4u_4", "w2_4a_4", "w1_2u_3", "w1_4u_2", "pair4", "flat"])
 @pytest.mark.parametrize("n_build,cf,n_probe,rng", [(1 << 20, 1, 1 << 22, 1 << 20), (1 << 16, 3, 300000, 1 << 17),
-                                                    (5000, 1, 70000, 20000)])
-def test_partitioned_probe_walk_variants(variant, n_build, cf, n_probe, rng, monkeypatch):
-    """Every form of the partitioned walk (CCJ_PROBE_VARIANT, read per launch: probe_win windows,
-    probe_pair, probe_flat) gives the exact L1 + L2 answer, duplicates (cf 3) and misses included."""
-    monkeypatch.setenv("CCJ_PROBE_VARIANT", variant)
+                                                    (5000, 1, 70000, 20000), (4096, 64, 100000, 8192),
+                                                    (3, 1, 5000, 6), (1 << 19, 2, 1 << 21, 3 << 19)])
+@pytest.mark.parametrize("positions", [False, True])
+def test_partitioned_probe_walks(n_build, cf, n_probe, rng, positions):
+    """The partitioned walks give the exact L1 + L2 answer: probe_walk (match counts, wave-ordered
+    emit) and, with match positions requested, probe_win (C5); duplicates (cf 3, cf 64: runs far
+    longer than 32 slots), misses, a tiny table (identity layout) and a table of exactly one
+    window included."""
     table = ccj.Table.reference(ccj.LP, n_build, cf, ccj.LAYOUT_DEVICE)
     keys = ccj.gen_uniform_keys(n_probe, 17, rng)
-    out = table.probe_partitioned(keys, 2048)
+    kw = dict(pos=True) if positions and table.size >= 16 else {}
+    out = table.probe_partitioned(keys, 2048, **kw)
     torch.cuda.synchronize()
     assert int(out["status"].item()) == 0
     m, l2 = ccj.result_checksum(out, 2048, row_map=out["row_map"].to(torch.int64))
     assert (m, l2) == O.count_uniform(17, 0, n_probe, rng, n_build, cf)
+    if kw:  # every recorded position holds the matched key
+        h = host(out)
+        tab = table_slots(table)
+        valid = np.arange(h["cap"])[None, :] < h["count"].astype(np.int64)[:, None]
+        pos = h["pos"].reshape(-1, h["cap"])[valid].view(np.uint32)
+        assert np.array_equal(tab[pos], h["payload"].reshape(-1, h["cap"])[valid])
+
+
+def table_slots(table):
+    """The device table's slot array on the host (LP)."""
+    import ctypes as C
+    out = np.empty(max(table.size, 4), np.int64)
+    from ccj import _d2h_i64
+    return _d2h_i64(table.d_table, len(out))
 
 
 @pytest.mark.parametrize("distinct", [1, 7, 3000])
@@ -299,3 +316,29 @@ def test_partitioned_probe_chunk_counts(n_build):
     live = (pos % chunk) < counts_h[pos // chunk]
     want = (int(live.sum()), O.l2_sum(pos[live].astype(np.uint64), keys_h[live]))
     assert ccj.result_checksum(out, chunk, row_map=out["row_map"].to(torch.int64)) == want
+
+
+def test_c2_table_size_reference_vector():
+    """The reference's own answer at C2's table size (SURVEY §4 survey_lp_2048_64M_64M: a 2^26-key
+    LP table = 2^28 slots = 2 GiB, 2^26 mt19937_64(42) probe keys % 2^26, B = 2048).
+    Chunk path on the reference-order table: matches, L2, the ordered L3 fold and the SURVEY
+    checksum equal the reference's (L3).  Partitioned path (bench.py's headline) on a device-built
+    table: matches and L2 equal it (L1 + L2)."""
+    entry = KA["sum_cases"]["survey_lp_2048_64M_64M"]
+    spec, want = entry["spec"], entry["variants"]["next"]
+    n, B = spec["n_build"], spec["B"]
+    keys = to_dev(O.mt64_keys(spec["seed"], spec["n_probe"], spec["range"]))
+    table = ccj.Table.reference(ccj.LP, n, spec["cf"], ccj.LAYOUT_REFERENCE)
+    assert table.size == 1 << 28
+    out = host(table.probe(keys, B, rounds=False))
+    assert out["status"][0] == 0
+    got = O.result_sums(out["count"], out["sel"], out["payload"], out["cap"], B)
+    assert got == (want["matches"], want["l2"], want["l3"], want["survey_chk"])
+    table.free()
+    del out
+    table = ccj.Table.reference(ccj.LP, n, spec["cf"], ccj.LAYOUT_DEVICE)
+    pout = table.probe_partitioned(keys, B)
+    torch.cuda.synchronize()
+    assert int(pout["status"].item()) == 0
+    assert ccj.result_checksum(pout, B, row_map=pout["row_map"].to(torch.int64)) == (want["matches"], want["l2"])
+    table.free()
