@@ -1225,7 +1225,6 @@ __global__ __launch_bounds__(kFlatThreads) void probe_chain_win(ProbeParams p) {
 // and writes its rows' matches in row order, coalesced (payload = the probe key, sel = the row's
 // position).  A lane pair walks a row, 16 B each (one DPP swap joins the halves), R rows per pair
 // in flight.
-constexpr uint32_t kWaveRows = kMaxChunk / (kFlatThreads / kWave);  // 512
 
 template <bool HOME>
 struct WalkShared {
@@ -1243,7 +1242,7 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <bool HOME>
+template <uint32_t kWaveRows, bool HOME>
 __device__ __forceinline__ void walk_stage(const ProbeParams &p, WalkShared<HOME> &sm, uint64_t base, uint32_t w0,
                                            uint32_t wend, uint32_t lane) {
   int64_t v[kWaveRows / kWave];  // all loads in flight before the first LDS write
@@ -1262,7 +1261,7 @@ __device__ __forceinline__ void walk_stage(const ProbeParams &p, WalkShared<HOME
 }
 
 // Emit the wave's rows [w0, wend): counts in sm.hc; returns 1 on output overflow.
-template <typename SM>
+template <uint32_t kWaveRows, typename SM>
 __device__ __forceinline__ uint32_t walk_emit(const ProbeParams &p, SM &sm, uint64_t c, uint32_t w0,
                                               uint32_t wend, uint32_t lane) {
   wave_lds_sync();
@@ -1351,8 +1350,9 @@ __device__ __forceinline__ void walk_finish(const ProbeParams &p, SM &sm, uint64
   if (p.status && overflow) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
 }
 
-template <int R, bool HOME>
-__global__ __launch_bounds__(kFlatThreads) void probe_walk(ProbeParams p) {
+template <int R, bool HOME, int NW = 4>
+__global__ __launch_bounds__(kWave * NW) void probe_walk(ProbeParams p) {
+  constexpr uint32_t kWaveRows = kMaxChunk / NW;  // rows per wave
   __shared__ WalkShared<HOME> sm;
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   const uint32_t sub = lane & 1u;
@@ -1368,7 +1368,7 @@ __global__ __launch_bounds__(kFlatThreads) void probe_walk(ProbeParams p) {
     sm.total = 0;
     sm.rounds = 0;
   }
-  walk_stage<HOME>(p, sm, base, w0, wend, lane);
+  walk_stage<kWaveRows, HOME>(p, sm, base, w0, wend, lane);
   CCJ_STAMP(t1);
   const uint32_t last_start = p.mask - 3u;  // table size - 4 (size >= 16)
   const uint32_t pair = lane >> 1;
@@ -1460,7 +1460,7 @@ __global__ __launch_bounds__(kFlatThreads) void probe_walk(ProbeParams p) {
     }
   }
   CCJ_STAMP(t2);
-  const uint32_t overflow = walk_emit(p, sm, c, w0, wend, lane);
+  const uint32_t overflow = walk_emit<kWaveRows>(p, sm, c, w0, wend, lane);
   walk_finish(p, sm, c, lane, lane_rounds, overflow, t0, t1, t2, steps);
 }
 
@@ -1474,12 +1474,17 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
     return hipGetLastError();
   }
   if (size < 16) return launch_probe(kind, p, s);  // a table of < 16 slots is one identity window
-  // At C2 (profiles/r2_*): probe_walk 9.4 ms against 9.9-10.1 for probe_win's per-step output
-  // placement; R = 2 / 3 / 4 / 6 rows per pair 9.65 / 9.4 / 9.7 / 10.9 ms, home slots staged in
-  // LDS 9.4 vs hashed at row start 9.6 ms; one lane per row with two 16-B loads (twice the L2
-  // requests) 11.0-12.3 ms; write-through (sc1) or plain output stores 10.2 ms vs non-temporal.
-  if (p.out_pos) hipLaunchKernelGGL((probe_win<3>), g, b, 0, s, p);  // C5: match positions too
-  else hipLaunchKernelGGL((probe_walk<3, true>), g, b, 0, s, p);
+  // At C2 (DESIGN §3.2, r2 sweeps): probe_walk 9.4 ms against 9.9-10.1 for probe_win's per-step
+  // output placement; R = 2 / 3 / 4 / 6 rows per pair 9.65 / 9.4 / 9.7 / 10.9 ms; home slots
+  // staged in LDS 9.4 vs hashed at row start 9.6 ms; 8 waves x 256 rows per chunk 10.0 ms; one
+  // lane per row with two 16-B loads (twice the L2 requests) 11.0-12.3 ms; a rolling load
+  // pipeline (each slot re-issued as soon as it is consumed, vmcnt(R - 1) waits) 10.4-10.5 ms;
+  // write-through (sc1) or plain output stores 10.2 ms vs non-temporal.
+  if (p.out_pos) {
+    hipLaunchKernelGGL((probe_win<3>), g, b, 0, s, p);  // C5: match positions too
+  } else {
+    hipLaunchKernelGGL((probe_walk<3, true>), g, b, 0, s, p);
+  }
   return hipGetLastError();
 }
 
