@@ -43,6 +43,11 @@ import ccj  # noqa: E402
 METRIC = "probe tuples/sec + achieved HBM GB/s, 1B-row int64 join at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
 SEED = 42
+PATH_KERNELS = {
+    "partitioned": "ccj_probe_partitioned (slot_split_fixed + probe_walk<3>)",
+    "ordered": "ccj_probe_ordered (slot_split_fixed with runs + probe_walk<3,MM> + unsplit_words + probe_chunks<LP,2,FROM_W>)",
+    "chunk": "ccj_probe (probe_chunks<LP,2>)",
+}
 
 
 def log(*a):
@@ -70,7 +75,7 @@ def parse():
     ap.add_argument("--n-probe", type=int, default=1 << 30, help="probe keys per GPU")
     ap.add_argument("--chunk", type=int, default=2048)
     ap.add_argument("--layout", default="device", choices=["device", "reference"])
-    ap.add_argument("--path", default="partitioned", choices=["partitioned", "chunk"],
+    ap.add_argument("--path", default="partitioned", choices=["partitioned", "chunk", "ordered"],
                     help="partitioned: slot-range partition + L2-resident probe (L1/L2 parity); "
                          "chunk: reference-order chunk probe (L3 parity)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -430,9 +435,12 @@ def main():
             table.set_payload(pay.reshape(-1), P, stream=stream)
             del bk, pay
         keys = ccj.gen_uniform_keys(n_probe, SEED, n_build, first_row=rank * n_probe, stream=stream)
-        out = part = out_p = None
-        if args.path == "chunk" or not c5:  # C2: both paths (the headline and the one timed beside it)
+        out = part = out_p = out_o = ws_o = None
+        if args.path == "chunk" or not c5:  # C2: every path (the headline and the ones timed beside it)
             out = table.alloc_outputs(n_probe, chunk, rounds=True, payload_cols=P, pos=c5)
+        if args.path == "ordered" or not c5:
+            out_o = table.alloc_outputs(n_probe, chunk, rounds=True)
+            ws_o = table.alloc_ordered(n_probe, chunk)
         if args.path == "partitioned" or not c5:
             part = table.alloc_partitioned(n_probe, chunk)
             # C5: the match positions the payload gather reads are a caller-owned buffer, so no
@@ -445,6 +453,8 @@ def main():
     def step(path=args.path):
         if path == "partitioned":  # no host check inside the timed region: status is read after it
             table.probe_partitioned(keys, chunk, out=out_p, part=part, stream=stream, retry=False)
+        elif path == "ordered":  # L3 through the partitioned layout (status read after the timing)
+            table.probe_ordered(keys, chunk, out=out_o, ws=ws_o, stream=stream, retry=False)
         else:
             table.probe(keys, chunk, out=out, stream=stream)
 
@@ -484,12 +494,13 @@ def main():
         matches, l2 = ccj.result_checksum(out_p, chunk, row_map=rm, stream=stream)
         del rm
     else:
-        status = int(out["status"].item())
-        matches, l2 = ccj.result_checksum(out, chunk, row_base=rank * n_probe, stream=stream)
-    # the other path, timed the same way (reported beside the headline)
-    other = "chunk" if args.path == "partitioned" else "partitioned"
-    other_ms = other_parity = None
-    if not c5:
+        res0 = out_o if args.path == "ordered" else out
+        status = int(res0["status"].item())
+        matches, l2 = ccj.result_checksum(res0, chunk, row_base=rank * n_probe, stream=stream)
+    # the other paths, timed the same way (reported beside the headline)
+    others = [] if c5 else [q for q in ("ordered", "chunk", "partitioned") if q != args.path]
+    other_runs = {}
+    for other in others:
         step(other)
         stream.synchronize()
         ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
@@ -498,15 +509,36 @@ def main():
             step(other)
             b.record(stream)
         stream.synchronize()
-        other_ms = sum(a.elapsed_time(b) for a, b in ev2) / len(ev2)
-        if other == "partitioned":  # its L1/L2 against the oracle answer too
+        o_ms = sum(a.elapsed_time(b) for a, b in ev2) / len(ev2)
+        if other == "partitioned":
             out_p["n_chunks"] = (part["positions"] + chunk - 1) // chunk
             rm = part["row_map"].to(torch.int64) + rank * n_probe
             om, ol2 = ccj.result_checksum(out_p, chunk, row_map=rm, stream=stream)
             del rm
-            other_parity = {"status_flags": int(out_p["status"].item()), "matches": om, "l2": hex(ol2)}
+            o_par = {"status_flags": int(out_p["status"].item()), "matches": om, "l2": hex(ol2)}
+        else:
+            res = out_o if other == "ordered" else out
+            om, ol2 = ccj.result_checksum(res, chunk, row_base=rank * n_probe, stream=stream)
+            o_par = {"status_flags": int(res["status"].item()), "matches": om, "l2": hex(ol2)}
+        other_runs[other] = (o_ms, o_par)
+    l3_same = None
+    if out is not None and out_o is not None and "chunk" in (other_runs.keys() | {args.path}):
+        # L3 at full size: the ordered route's whole output equals probe_chunks' (counts, rounds,
+        # every Next's count, and the ordered (sel, payload) stream of every chunk)
+        torch.cuda.synchronize()
+        same = all(torch.equal(out_o[k], out[k]) for k in ("count", "rounds", "round_counts"))
+        if same:
+            valid = (torch.arange(out["cap"], device=dev)[None, :] < out["count"].to(torch.int64)[:, None]).reshape(-1)
+            same = bool(torch.equal(out_o["sel"][valid], out["sel"][valid])) and \
+                bool(torch.equal(out_o["payload"][valid], out["payload"][valid]))
+            del valid
+        l3_same = same
+        if "ordered" in other_runs:
+            other_runs["ordered"][1]["equals_chunk_path_l3"] = same
     examined, cost_matches = table.probe_cost(keys, stream=stream)
     parity = {"status_flags": status, "matches": matches, "l2": hex(l2)}
+    if args.path == "ordered" and l3_same is not None:
+        parity["equals_chunk_path_l3"] = l3_same
     if c5:  # every gathered payload column holds the matched build tuple's p_c (key == payload)
         torch.cuda.current_stream().wait_stream(stream)
         res = out_p if args.path == "partitioned" else out
@@ -524,8 +556,8 @@ def main():
         want_m, want_l2 = O.count_uniform(SEED, rank * n_probe, (rank + 1) * n_probe, n_build, n_build, 1,
                                           threads=args.cpu_threads)
         parity.update(expected_matches=want_m, l1_ok=(want_m == matches), l2_ok=(want_l2 == l2))
-        if other_parity is not None:
-            other_parity.update(l1_ok=(want_m == other_parity["matches"]), l2_ok=(hex(want_l2) == other_parity["l2"]))
+        for _, o_par in other_runs.values():
+            o_par.update(l1_ok=(want_m == o_par["matches"]), l2_ok=(hex(want_l2) == o_par["l2"]))
     s_bar = examined / n_probe
     m_bar = matches / n_probe
     alg_bytes_per_tuple = 8 + 8 * s_bar + m_bar * (12 + 16 * P)  # +16 B per payload column
@@ -564,20 +596,19 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          # measured DRAM bytes (whole 128-B lines per random slot read) per second
                          "traffic_GBps": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
-                         "kernel": (("ccj_probe_partitioned (slot_split_fixed + probe_win<2,4,3,next-slot windows>"
-                                     + (" with positions + gather_payload_quad)" if c5 else ")"))
-                                    if args.path == "partitioned" else "probe_chunks<LP,2>"
-                                    + (" + gather_payload_quad" if c5 else "")),
+                         "kernel": (("ccj_probe_partitioned (slot_split_fixed + probe_win<3> with positions + "
+                                     "gather_payload_quad)") if c5 and args.path == "partitioned" else
+                                    "probe_chunks<LP,2> + gather_payload_quad" if c5 else PATH_KERNELS[args.path]),
                          "kernel_ms": kern_ms, "rocprof_kernels_ms": kernels_ms,
                          "alg_bytes_per_tuple": alg_bytes_per_tuple, "s_bar": s_bar, "m_bar": m_bar},
             "cpu_baseline": cpu,
             "parity": parity,
             "path": args.path,
-            "other_path": None if other_ms is None else {
-                "path": other, "ms_per_step": other_ms, "value": n_probe / (other_ms * 1e-3),
-                "frac": alg_bytes / (other_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                "parity": "L3 (reference order)" if other == "chunk" else "L1/L2",
-                "check": other_parity},
+            "other_paths": [{
+                "path": o, "ms_per_step": o_ms, "value": n_probe / (o_ms * 1e-3),
+                "frac": alg_bytes / (o_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "parity": "L3 (reference order)" if o != "partitioned" else "L1/L2",
+                "kernel": PATH_KERNELS[o], "check": o_par} for o, (o_ms, o_par) in other_runs.items()],
         }
         print(json.dumps(line), flush=True)
     if dist:

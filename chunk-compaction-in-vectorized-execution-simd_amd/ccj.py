@@ -64,7 +64,8 @@ EXPORTS = ["ccj_last_error", "ccj_abi_version", "ccj_device_init", "ccj_table_bu
            "ccj_probe_partitioned_workspace_size", "ccj_probe_partitioned", "ccj_probe_partitioned_positions",
            "ccj_pipeline_create",
            "ccj_pipeline_run", "ccj_pipeline_free", "ccj_pipeline_checksum", "ccj_partition_by_owner_fixed",
-           "ccj_segment_chunk_counts", "ccj_pipeline_set_thresholds", "ccj_gen_c3_keys"]
+           "ccj_segment_chunk_counts", "ccj_pipeline_set_thresholds", "ccj_gen_c3_keys",
+           "ccj_probe_ordered_workspace_size", "ccj_probe_ordered"]
 
 MAX_JOINS = 8
 COMPACT_NONE, COMPACT_FULL = 0, 1
@@ -105,6 +106,9 @@ def lib():
         L.ccj_probe_partitioned_positions.argtypes = [vp, u64, C.c_uint32]
         L.ccj_probe_partitioned.argtypes = [vp, C.POINTER(ProbeArgs), C.c_uint32, vp, vp, C.c_size_t, vp]
         L.ccj_probe.argtypes = [vp, C.POINTER(ProbeArgs), vp]
+        L.ccj_probe_ordered_workspace_size.restype = C.c_size_t
+        L.ccj_probe_ordered_workspace_size.argtypes = [vp, u64, C.c_uint32]
+        L.ccj_probe_ordered.argtypes = [vp, C.POINTER(ProbeArgs), vp, C.c_size_t, vp]
         L.ccj_gen_uniform_keys.argtypes = [vp, u64, u64, u64, u64, vp]
         L.ccj_gen_reference_keys.argtypes = [vp, u64, u64, u64, u64, vp]
         L.ccj_gen_c3_keys.argtypes = [vp, u64, u64, u64, u64, u64, C.c_uint32, vp]
@@ -360,6 +364,41 @@ class Table:
         for i, col in enumerate(cols):
             a.out_payload_cols[i] = col.data_ptr()
         return a
+
+    def alloc_ordered(self, n_rows: int, chunk: int, device=None):
+        """Workspace of probe_ordered (None when the table takes ccj_probe's one-pass route)."""
+        import torch
+        b = lib().ccj_probe_ordered_workspace_size(self._h, n_rows, chunk)
+        if b == 0:
+            return None
+        dev = device or torch.device("cuda", torch.cuda.current_device())
+        return dict(ws=torch.empty(b, dtype=torch.uint8, device=dev), ws_bytes=b, n_rows=n_rows, chunk=chunk)
+
+    def probe_ordered(self, keys, chunk: int, counts=None, out=None, ws=None, stream=None, retry: bool = True,
+                      **alloc_kw):
+        """ccj_probe_ordered: probe()'s reference-order (L3) outputs, through the slot-partitioned
+        layout for large LP tables.  With retry=True an overflow of the split (extreme key skew)
+        is checked (one stream synchronisation) and the chunk is re-run with probe()."""
+        if out is None:
+            out = self.alloc_outputs(keys.numel(), chunk, **alloc_kw)
+        if ws is None:
+            ws = self.alloc_ordered(keys.numel(), chunk)
+        a = self._args(keys, chunk, None, counts, out)
+        w, wb = (None, 0) if ws is None else (_ptr(ws["ws"]), ws["ws_bytes"])
+        check(lib().ccj_probe_ordered(self._h, C.byref(a), w, wb, _stream(stream)), "ccj_probe_ordered")
+        if retry and ws is not None:
+            import torch
+            if stream is not None:
+                stream.synchronize()
+            else:
+                torch.cuda.synchronize()
+            st = int(out["status"].item())
+            if st & FLAG_PART_OVERFLOW:
+                out["status"].fill_(st & ~FLAG_PART_OVERFLOW)
+                torch.cuda.synchronize()
+                self.probe(keys, chunk, counts=counts, out=out, stream=stream)
+                out["exact_retry"] = True
+        return out
 
     def probe(self, keys, chunk: int, sel=None, counts=None, out=None, stream=None, **alloc_kw):
         """Batched Probe + Next loop (include/ccj.h ccj_probe).  Returns the output dict."""

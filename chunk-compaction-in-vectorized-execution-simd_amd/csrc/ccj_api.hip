@@ -599,6 +599,107 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   return CCJ_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// Ordered probe (ccj_probe_ordered): tables of at least this many LP slots take the partitioned
+// route (below it the table sits in L2 / the Infinity Cache and probe_chunks' random reads hit).
+constexpr uint64_t kOrderedMinSlots = 1ull << 22;
+
+struct OrderedLayout {
+  bool partitioned = false;
+  PartLayout L{};
+  uint32_t tile = 0;
+  uint64_t n_tiles = 0;
+  size_t pkeys = 0, row_map = 0, w_pos = 0, w_row = 0, cursors = 0, runs = 0, ovf_runs = 0, total = 0;
+};
+
+OrderedLayout ordered_layout(const ccj_table *t, uint64_t n_rows, uint32_t chunk) {
+  OrderedLayout O;
+  if (!t || t->info.kind != CCJ_TABLE_LP || t->info.size < kOrderedMinSlots || n_rows == 0 || chunk == 0 ||
+      n_rows >= (1ull << 32))
+    return O;
+  O.L = part_layout(t, n_rows, chunk);
+  if (O.L.pl.lo_bits == 0) return O;
+  O.partitioned = true;
+  O.tile = ccj::slot_split_tile_keys();
+  O.n_tiles = (n_rows + O.tile - 1) / O.tile;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = off;
+    off += align256(bytes);
+    return at;
+  };
+  O.pkeys = take(O.L.positions * 8);
+  O.row_map = take(O.L.positions * 4);
+  O.w_pos = take(O.L.positions * 4);
+  O.w_row = take(n_rows * 4);
+  O.cursors = take(((uint64_t)O.L.parts * 8 + 1) * 4);
+  O.runs = take(O.n_tiles * O.L.parts * 8);
+  O.ovf_runs = take(O.n_tiles * O.L.parts * 4);
+  O.total = off;
+  return O;
+}
+}  // namespace
+
+extern "C" {
+
+size_t ccj_probe_ordered_workspace_size(const ccj_table *t, uint64_t n_rows, uint32_t chunk) {
+  const OrderedLayout O = ordered_layout(t, n_rows, chunk);
+  return O.partitioned ? O.total : 0;
+}
+
+int ccj_probe_ordered(const ccj_table *t, const ccj_probe_args *a, void *ws, size_t ws_bytes, ccj_stream stream) {
+  ccj::ProbeParams p;
+  if (int rc = fill_probe_params(t, a, p)) return rc;
+  if (a->n_rows == 0) return CCJ_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const OrderedLayout O = ordered_layout(t, a->n_rows, a->chunk);
+  if (!O.partitioned || a->sel || a->out_pos || a->n_payload_cols) {  // small table / gathered input: one pass
+    if (p.n_pay == 0) {
+      HIP_TRY(ccj::launch_probe(t->info.kind, p, s), "probe launch");
+      return CCJ_OK;
+    }
+    return ccj_probe(t, a, stream);
+  }
+  if (!ws || ws_bytes < O.total)
+    return fail(CCJ_ERR_INVALID, "ccj_probe_ordered: workspace missing or smaller than ccj_probe_ordered_workspace_size");
+  if (!a->status) return fail(CCJ_ERR_INVALID, "ccj_probe_ordered: the partitioned route needs args->status");
+  char *w = (char *)ws;
+  int64_t *pkeys = (int64_t *)(w + O.pkeys);
+  uint32_t *row_map = (uint32_t *)(w + O.row_map), *w_pos = (uint32_t *)(w + O.w_pos);
+  uint32_t *w_row = (uint32_t *)(w + O.w_row), *cursors = (uint32_t *)(w + O.cursors);
+  uint2 *runs = (uint2 *)(w + O.runs);
+  uint32_t *ovf_runs = (uint32_t *)(w + O.ovf_runs);
+  const PartLayout &L = O.L;
+  // 1. one-pass slot split of the live rows, recording where every tile's runs went
+  HIP_TRY(ccj::launch_slot_split_fixed(a->keys, a->n_rows, L.pl, L.seg_cap, L.ovf_base, L.ovf_cap, cursors, pkeys,
+                                       row_map, a->status, s, a->counts, a->chunk, runs, ovf_runs),
+          "slot split");
+  // 2. walk with the table window L2-resident: every row's Next-round word at its position
+  ccj::ProbeParams q = p;
+  q.keys = pkeys;
+  q.counts = nullptr;
+  q.seg_count = cursors;
+  q.seg_parts = L.parts;
+  q.seg_cap = L.seg_cap;
+  q.ovf_base = L.ovf_base;
+  q.swz_chunks = L.ovf_base / a->chunk;
+  q.n_rows = L.positions;
+  q.n_chunks = L.positions / a->chunk + (L.positions % a->chunk ? 1 : 0);
+  q.xcd_swizzle = 1;
+  q.out_w = w_pos;
+  HIP_TRY(ccj::launch_ordered_walk(q, s), "ordered walk");
+  // 3. the words back into row order, one split tile per workgroup
+  HIP_TRY(ccj::launch_unsplit_words(runs, ovf_runs, row_map, w_pos, w_row, a->n_rows, L.parts, O.tile, a->status, s),
+          "unsplit");
+  // 4. per chunk: the reference's per-Next stream from its rows' words (probe_chunks' emit)
+  p.in_w = w_row;
+  p.xcd_swizzle = 0;
+  HIP_TRY(ccj::launch_ordered_emit(p, s), "ordered emit");
+  return CCJ_OK;
+}
+
 int ccj_probe(const ccj_table *t, const ccj_probe_args *a, ccj_stream stream) {
   ccj::ProbeParams p;
   if (int rc = fill_probe_params(t, a, p)) return rc;

@@ -80,12 +80,23 @@ struct ProbeParams {
   uint32_t xcd_swizzle;  // 1: consecutive chunks go to the same XCD (L2 reuse of partitioned input)
   uint32_t ablate;       // timing-only ablations (tuning build only: CCJ_ABLATE)
   unsigned long long *stats;  // tuning build only (CCJ_STATS): per-phase cycle sums of the walk
+  // Ordered probe (ccj_probe_ordered): round words per position (walk) / per row (emit input)
+  uint32_t *out_w;
+  const uint32_t *in_w;
 };
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 
 // Launchers (ccj_kernels.hip).  Return hipError_t of the launch.
 hipError_t launch_probe(int kind, const ProbeParams &p, hipStream_t s);
 hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s);
+// Ordered probe (ccj_probe_ordered, LP): walk of the slot-partitioned column leaving each row's
+// round word at its position (p.out_w); the words back into row order, one split tile per
+// workgroup; the reference-order emit of each chunk from its rows' words (p.in_w).
+hipError_t launch_ordered_walk(const ProbeParams &p, hipStream_t s);
+hipError_t launch_unsplit_words(const uint2 *runs, const uint32_t *ovf_runs, const uint32_t *row_map,
+                                const uint32_t *w_pos, uint32_t *w_row, uint64_t n, uint32_t parts, uint32_t tile,
+                                uint32_t *status, hipStream_t s);
+hipError_t launch_ordered_emit(const ProbeParams &p, hipStream_t s);
 // C5 payload columns of a finished probe: out_cols[q][slot] = payload row of pos[slot], column q.
 hipError_t launch_gather_payload(const ProbeParams &p, const uint32_t *pos, hipStream_t s);
 hipError_t launch_gen_reference_keys(int64_t *out, uint64_t first, uint64_t n, uint64_t n_total, uint64_t cf,
@@ -141,10 +152,15 @@ hipError_t launch_slot_partition(const int64_t *keys, uint64_t n, const SlotPlan
 // cursors[g*parts + d] = rows that went to it (may exceed cap: CCJ_FLAG_PART_OVERFLOW raised).
 uint64_t slot_seg_cap(uint64_t n, const SlotPlan &pl, uint32_t chunk);
 // cursors[parts * 8] = rows that went to the overflow area [ovf_base, ovf_base + ovf_cap).
+// counts: live rows per input chunk.  runs (optional; the ordered probe): per (tile, partition)
+// {segment position of the run, segment length | overflow-area length << 16}; ovf_runs: the
+// overflow-area position where that length is non-zero.  Tiles are slot_split_tile_keys() keys.
 hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPlan &pl, uint64_t cap,
                                    uint64_t ovf_base, uint64_t ovf_cap, uint32_t *cursors, int64_t *out_keys,
                                    uint32_t *out_rows, uint32_t *status, hipStream_t s,
-                                   const uint32_t *counts = nullptr, uint32_t chunk = 0);  // counts: live rows per input chunk
+                                   const uint32_t *counts = nullptr, uint32_t chunk = 0, uint2 *runs = nullptr,
+                                   uint32_t *ovf_runs = nullptr);
+uint32_t slot_split_tile_keys();
 hipError_t launch_partition_fixed(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t row_base, uint64_t seg_cap,
                                   int64_t *out_keys, uint32_t *out_rows, uint64_t *out_counts, uint32_t *status,
                                   void *ws, hipStream_t s);

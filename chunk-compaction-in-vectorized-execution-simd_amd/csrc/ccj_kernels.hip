@@ -39,20 +39,23 @@ __device__ __forceinline__ void emit_extra(const ProbeParams &p, uint64_t obase,
   }
 }
 
+// Wave reductions over DPP / permlane (ROCm device library ockl), returned wave-uniform (an SGPR
+// value: loops over its bits are scalar).  A shuffle tree (__shfl_xor) is 6 dependent
+// ds_bpermute round trips through LDS instead.
+extern "C" __device__ uint32_t __ockl_wfred_or_u32(uint32_t);
+extern "C" __device__ uint32_t __ockl_wfred_max_u32(uint32_t);
+
 __device__ __forceinline__ uint32_t wave_or(uint32_t x) {
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) x |= (uint32_t)__shfl_xor((int)x, d);
-  return x;
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)__ockl_wfred_or_u32(x));
 }
 
 __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) {
-    const uint32_t o = (uint32_t)__shfl_xor((int)x, d);
-    x = o > x ? o : x;
-  }
-  return x;
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)__ockl_wfred_max_u32(x));
 }
+
+extern "C" __device__ uint32_t __ockl_wfscan_add_u32(uint32_t, bool);
+// Inclusive prefix sum over the wave's lanes (DPP row shifts + permlane, no LDS).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) { return __ockl_wfscan_add_u32(x, true); }
 
 __device__ __forceinline__ void record_round(const ProbeParams &p, uint64_t c, uint32_t r, uint32_t rc,
                                              uint32_t lane, uint32_t &flags) {
@@ -123,6 +126,10 @@ __device__ void rounds_generic(const ProbeParams &p, uint64_t c, uint64_t base, 
 
 constexpr int kWin = 4;             // slots (LP) / chain keys per window load: 32 B, one aligned sector
 constexpr int kMaxFastRounds = 32;  // rounds recorded by the windowed path (bits of a u32)
+// Round words of the ordered probe (probe_walk<..., MM>): mm in bits 0-25, rounds in bits 26-30;
+// a row of more than 26 rounds is kMmLong | rounds.
+constexpr uint32_t kMmRounds = 26;
+constexpr uint32_t kMmLong = 0x80000000u;
 constexpr int kWalkRows = 2;  // rows per lane walked concurrently (loads in flight)
 
 constexpr int kEmitRows = 4;    // row groups per lane whose sel loads are issued together in the emit
@@ -360,12 +367,7 @@ __global__ __launch_bounds__(kBlock) void probe_chunks(ProbeParams p) {
         loc[t] = s_off[lane * 16 + t];
         sum += loc[t];
       }
-      uint32_t incl = sum;
-#pragma unroll
-      for (int d = 1; d < kWave; d <<= 1) {
-        const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
-        if (lane >= (uint32_t)d) incl += o;
-      }
+      uint32_t incl = wave_incl_scan(sum);
       uint32_t run = incl - sum;
 #pragma unroll
       for (int t = 0; t < 16; ++t) {
@@ -582,12 +584,7 @@ __global__ __launch_bounds__(kBlock) void probe_multi(ProbeParams p) {
       uint32_t tk = 0;
       if (lane < kMaxFastRounds)
         for (uint32_t j = k * gpc; j < (k + 1) * gpc; ++j) tk += s_off[lane * 32 + j];
-      uint32_t incl = tk;
-#pragma unroll
-      for (int d = 1; d < kMaxFastRounds; d <<= 1) {
-        const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
-        if (lane >= (uint32_t)d) incl += o;
-      }
+      const uint32_t incl = wave_incl_scan(tk);  // lanes >= kMaxFastRounds add 0
       if (lane < kMaxFastRounds) {
         uint32_t run = incl - tk;
         for (uint32_t j = k * gpc; j < (k + 1) * gpc; ++j) {
@@ -1289,12 +1286,7 @@ __device__ __forceinline__ uint32_t walk_emit(const ProbeParams &p, SM &sm, uint
       pre = lane_prefix(bm);
       tot = (uint32_t)__popcll(bm);
     } else {
-      uint32_t incl = n;
-#pragma unroll
-      for (int d = 1; d < kWave; d <<= 1) {
-        const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
-        if (lane >= (uint32_t)d) incl += o;
-      }
+      uint32_t incl = wave_incl_scan(n);
       pre = incl - n;
       tot = (uint32_t)__shfl((int)incl, kWave - 1);
     }
@@ -1350,7 +1342,11 @@ __device__ __forceinline__ void walk_finish(const ProbeParams &p, SM &sm, uint64
   if (p.status && overflow) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
 }
 
-template <int R, bool HOME, int NW = 4>
+// MM (the ordered probe, ccj_probe_ordered): instead of counts, each row leaves its Next-round
+// word W = mm | L << 26 (bit r of mm: the row matches in round r; L: occupied slots walked = its
+// rounds, the reference's Next calls for it; L > 26: bit 31 | L, the chunk re-walks round by
+// round), written to p.out_w at the row's position; no emit.
+template <int R, bool HOME, int NW = 4, bool MM = false>
 __global__ __launch_bounds__(kWave * NW) void probe_walk(ProbeParams p) {
   constexpr uint32_t kWaveRows = kMaxChunk / NW;  // rows per wave
   __shared__ WalkShared<HOME> sm;
@@ -1425,10 +1421,13 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk(ProbeParams p) {
         const uint32_t off = cur[k] - st[k];
         const uint32_t ee = (em & 15u) >> off;
         const uint32_t f = (uint32_t)__builtin_ctz(ee | (16u >> off));  // run end (or window end) past cur
-        cnt[k] += (uint32_t)__builtin_popcount(((em >> 4) >> off) & ((1u << f) - 1u));
+        const uint32_t hits = ((em >> 4) >> off) & ((1u << f) - 1u);
+        if (MM) cnt[k] |= r0[k] < kMmRounds ? hits << r0[k] : 0u;  // rounds >= 26 end as long rows
+        else cnt[k] += (uint32_t)__builtin_popcount(hits);
         if (ee) {
           const uint32_t r = r0[k] + f;  // occupied slots walked = the reference's rounds
           lane_rounds = r > lane_rounds ? r : lane_rounds;
+          if (MM) cnt[k] = r <= kMmRounds ? (cnt[k] & ((1u << kMmRounds) - 1u)) | r << kMmRounds : kMmLong | r;
           done |= 1u << k;
         } else {
           r0[k] += 4u - off;
@@ -1460,8 +1459,217 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk(ProbeParams p) {
     }
   }
   CCJ_STAMP(t2);
+  if (MM) {  // the rows' round words, coalesced at their positions
+    wave_lds_sync();
+#pragma unroll
+    for (int j = 0; j < (int)(kWaveRows / kWave); ++j) {
+      const uint32_t i = w0 + (uint32_t)j * kWave + lane;
+      if (i < wend) __builtin_nontemporal_store((uint32_t)sm.hc[i], p.out_w + base + i);
+    }
+    return;
+  }
   const uint32_t overflow = walk_emit<kWaveRows>(p, sm, c, w0, wend, lane);
   walk_finish(p, sm, c, lane, lane_rounds, overflow, t0, t1, t2, steps);
+}
+
+// Ordered probe, step 4 (emit_ordered): one chunk per 256-thread workgroup, the reference's
+// per-Next stream from its rows' round words (p.in_w: mm | rounds << 26, or kMmLong | rounds).
+// Thread (wave, lane) owns rows q*256 + tid (q < 8), i.e. row group j = 4q + wave, lane `lane`:
+// its keys and words stay in registers, and the count / scan / emit phases are probe_chunks'
+// (per (round, row group) ballots, a round-major exclusive scan, ballot-prefix stores), so the
+// output is exactly ccj_probe's.  A chunk with a row of more than 26 rounds re-walks round by
+// round (rounds_generic).  Only s_off (4 KB) is LDS on the common path: 8 workgroups per CU.
+__global__ __launch_bounds__(kBlock) void emit_ordered(ProbeParams p) {
+  constexpr int kQ = kMaxChunk / kBlock;  // 8 rows per thread
+  __shared__ uint32_t s_off[kMaxFastRounds * 32];
+  __shared__ uint32_t s_red[3 * kChunkWaves];
+  __shared__ int64_t s_key[kMaxChunk];  // only for a chunk with a long row
+  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  const uint64_t c = blockIdx.x;
+  const uint64_t base = c * p.chunk;
+  const uint64_t rem = p.n_rows - base;
+  const uint32_t phys = rem < p.chunk ? (uint32_t)rem : p.chunk;
+  const uint32_t nj = (p.chunk + kWave - 1) / kWave;
+  uint32_t count = p.counts ? p.counts[c] : phys;
+  uint32_t flags = 0;
+  if (count > phys) {
+    flags |= CCJ_FLAG_BAD_INPUT;
+    count = phys;
+  }
+  int64_t key[kQ];
+  uint32_t w[kQ];
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) {  // every load in flight first
+    const uint32_t i = (uint32_t)q * kBlock + tid;
+    key[q] = 0;
+    w[q] = 0;
+    if (i < count) {
+      key[q] = __builtin_nontemporal_load(p.keys + base + i);
+      w[q] = __builtin_nontemporal_load(p.in_w + base + i);
+    }
+  }
+  for (uint32_t q = tid; q < kMaxFastRounds * 32; q += kBlock) s_off[q] = 0u;
+  uint32_t lane_rounds = 0;
+  bool long_run = false;
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) {
+    const uint32_t r = w[q] & kMmLong ? w[q] & ~kMmLong : w[q] >> kMmRounds;
+    long_run |= (w[q] & kMmLong) != 0u;
+    lane_rounds = r > lane_rounds ? r : lane_rounds;
+    w[q] &= (1u << kMmRounds) - 1u;  // from here on: the row's match rounds (mm)
+  }
+  {
+    const uint32_t wr = wave_max(lane_rounds);
+    const bool wl = __ballot(long_run) != 0ull;
+    if (lane == 0) {
+      s_red[wave] = wr;
+      s_red[kChunkWaves + wave] = wl ? 1u : 0u;
+    }
+  }
+  __syncthreads();
+  uint32_t rounds = 0, any_long = 0;
+#pragma unroll
+  for (int v = 0; v < kChunkWaves; ++v) {
+    rounds = s_red[v] > rounds ? s_red[v] : rounds;
+    any_long |= s_red[kChunkWaves + v];
+  }
+  uint64_t total = 0;
+  const uint64_t obase = c * p.cap;
+  if (any_long) {
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) s_key[(uint32_t)q * kBlock + tid] = key[q];
+    __syncthreads();
+    if (wave == 0) {
+      uint32_t act_all = 0;
+      for (uint32_t j = 0; j < nj; ++j)
+        if (j * kWave + lane < count) act_all |= 1u << j;
+      rounds_generic<CCJ_TABLE_LP>(p, c, base, nj, act_all, s_key, flags, total, rounds);
+    }
+  } else {
+    // Count: matches per (round r, row group j = 4q + wave).
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      const uint32_t j = (uint32_t)q * kChunkWaves + wave;
+      if (j < nj) {
+        for (uint32_t any = wave_or(w[q]); any != 0u; any &= any - 1u) {
+          const uint32_t r = (uint32_t)__builtin_ctz(any);
+          const uint32_t n = (uint32_t)__popcll(__ballot((w[q] >> r) & 1u));
+          if (lane == 0) s_off[r * 32 + j] = n;
+        }
+      }
+    }
+    __syncthreads();
+    if (wave == 0) {  // exclusive prefix over (r, j) in round-major order, 16 entries per lane
+      uint32_t loc[16], sum = 0;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        loc[t] = s_off[lane * 16 + t];
+        sum += loc[t];
+      }
+      uint32_t incl = wave_incl_scan(sum);
+      uint32_t run = incl - sum;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        s_off[lane * 16 + t] = run;
+        run += loc[t];
+      }
+      if (lane == kWave - 1) s_red[2 * kChunkWaves] = incl;
+    }
+    __syncthreads();
+    total = s_red[2 * kChunkWaves];
+    if (p.out_round_counts) {  // Next return values: differences of the round starts
+      for (uint32_t r = tid; r < rounds; r += kBlock) {
+        const uint32_t a = s_off[r * 32], b = r + 1 < rounds ? s_off[(r + 1) * 32] : (uint32_t)total;
+        if (r < p.max_rounds) p.out_round_counts[c * p.max_rounds + r] = b - a;
+      }
+      if (rounds > p.max_rounds) flags |= CCJ_FLAG_ROUND_OVERFLOW;
+    }
+    // Emit: group j's matches of round r go to s_off[r][j] + their ballot prefix.
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      const uint32_t j = (uint32_t)q * kChunkWaves + wave;
+      const uint32_t i = (uint32_t)q * kBlock + tid;
+      if (j < nj) {
+        for (uint32_t any = wave_or(w[q]); any != 0u; any &= any - 1u) {
+          const uint32_t r = (uint32_t)__builtin_ctz(any);
+          const bool bit = (w[q] >> r) & 1u;
+          const uint64_t mb = __ballot(bit);
+          if (bit && !CCJ_ABLATED(p.ablate, 1u)) {
+            const uint64_t o = (uint64_t)s_off[r * 32 + j] + lane_prefix(mb);
+            if (o < p.cap) {
+              __builtin_nontemporal_store(i, p.out_sel + obase + o);
+              if (p.out_payload) __builtin_nontemporal_store(key[q], p.out_payload + obase + o);
+            }
+          }
+        }
+      }
+    }
+  }
+  if (total > p.cap) flags |= CCJ_FLAG_CAP_OVERFLOW;
+  if (tid == 0) {
+    p.out_count[c] = (uint32_t)(total < p.cap ? total : p.cap);
+    if (p.out_rounds) p.out_rounds[c] = rounds;
+  }
+  if (p.status) {
+    const uint64_t any = __ballot(flags != 0u);
+    if (any && flags) atomicOr(p.status, flags);
+  }
+}
+
+// Ordered probe, step 3: the round words of one split tile back into row order.  The split
+// recorded where each (tile, partition) run went (runs / ovf_runs); the tile's runs are numbered
+// consecutively (an exclusive scan of their lengths), every thread takes entries j = tid, tid +
+// 1024, ... (consecutive positions inside a run: coalesced reads of the row map and the words),
+// finds j's partition by a binary search over the scan, and drops the word into an LDS image of
+// the tile at row - t0; the image is written out whole.  Rows that were not live stay 0.
+constexpr int kUnsplitThreads = 1024;
+constexpr uint32_t kUnsplitMaxTile = 13u * kUnsplitThreads;  // the split's largest tile (13 keys per thread)
+
+__global__ __launch_bounds__(kUnsplitThreads) void unsplit_words(const uint2 *runs, const uint32_t *ovf_runs,
+                                                                 const uint32_t *row_map, const uint32_t *w_pos,
+                                                                 uint32_t *w_row, uint64_t n, uint32_t parts,
+                                                                 uint32_t tile, uint32_t *status) {
+  __shared__ uint32_t s_img[kUnsplitMaxTile];
+  __shared__ uint32_t s_loc[kUnsplitThreads + 1];
+  __shared__ uint2 s_run[kUnsplitThreads];
+  __shared__ uint32_t s_wsum[kUnsplitThreads / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint64_t t = blockIdx.x, t0 = t * tile;
+  const uint32_t tn = (uint32_t)(n - t0 < tile ? n - t0 : tile);
+  for (uint32_t i = tid; i < tn; i += kUnsplitThreads) s_img[i] = 0u;
+  const uint2 r = tid < parts ? runs[t * parts + tid] : make_uint2(0u, 0u);
+  const uint32_t len = (r.y & 0xFFFFu) + (r.y >> 16);
+  uint32_t incl = wave_incl_scan(len);
+  if (lane == 63) s_wsum[wave] = incl;
+  __syncthreads();
+  uint32_t wpre = 0;
+  for (uint32_t w = 0; w < wave; ++w) wpre += s_wsum[w];
+  if (tid < parts) {
+    s_loc[tid] = wpre + incl - len;
+    s_run[tid] = r;
+  }
+  if (tid == parts - 1) s_loc[parts] = wpre + incl;
+  __syncthreads();
+  const uint32_t total = s_loc[parts];
+  bool bad = false;
+  for (uint32_t j = tid; j < total; j += kUnsplitThreads) {
+    uint32_t lo = 0, hi = parts;  // the last d with s_loc[d] <= j
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (s_loc[mid] <= j) lo = mid;
+      else hi = mid;
+    }
+    const uint32_t o = j - s_loc[lo];
+    const uint2 rr = s_run[lo];
+    const uint32_t lim = rr.y & 0xFFFFu;
+    const uint64_t pos = o < lim ? (uint64_t)rr.x + o : (uint64_t)ovf_runs[t * parts + lo] + (o - lim);
+    const uint64_t local = (uint64_t)row_map[pos] - t0;
+    if (local < tn) s_img[local] = w_pos[pos];
+    else bad = true;
+  }
+  if (bad && status) atomicOr(status, CCJ_FLAG_BAD_INPUT);
+  __syncthreads();
+  for (uint32_t i = tid; i < tn; i += kUnsplitThreads) __builtin_nontemporal_store(s_img[i], w_row + t0 + i);
 }
 
 hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
@@ -1602,6 +1810,29 @@ hipError_t launch_gather_payload(const ProbeParams &p, const uint32_t *pos, hipS
     case 8: return launch_gather_np<8>(g, p.n_chunks, s);
     default: return hipSuccess;
   }
+}
+
+hipError_t launch_ordered_walk(const ProbeParams &p, hipStream_t s) {
+  if (p.n_chunks == 0) return hipSuccess;
+  hipLaunchKernelGGL((probe_walk<3, true, 4, true>), dim3((unsigned)p.n_chunks), dim3(kFlatThreads), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_unsplit_words(const uint2 *runs, const uint32_t *ovf_runs, const uint32_t *row_map,
+                                const uint32_t *w_pos, uint32_t *w_row, uint64_t n, uint32_t parts, uint32_t tile,
+                                uint32_t *status, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (tile > kUnsplitMaxTile || parts > (uint32_t)kUnsplitThreads) return hipErrorInvalidValue;
+  const uint64_t n_tiles = (n + tile - 1) / tile;
+  hipLaunchKernelGGL(unsplit_words, dim3((unsigned)n_tiles), dim3(kUnsplitThreads), 0, s, runs, ovf_runs, row_map,
+                     w_pos, w_row, n, parts, tile, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_ordered_emit(const ProbeParams &p, hipStream_t s) {
+  if (p.n_chunks == 0) return hipSuccess;
+  hipLaunchKernelGGL(emit_ordered, dim3((unsigned)p.n_chunks), dim3(kBlock), 0, s, p);
+  return hipGetLastError();
 }
 
 hipError_t launch_probe(int kind, const ProbeParams &p, hipStream_t s) {

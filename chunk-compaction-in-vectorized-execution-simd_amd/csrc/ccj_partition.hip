@@ -25,6 +25,10 @@
 namespace ccj {
 namespace {
 
+extern "C" __device__ uint32_t __ockl_wfscan_add_u32(uint32_t, bool);
+// Inclusive prefix sum over the wave's lanes (DPP row shifts + permlane, no LDS).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) { return __ockl_wfscan_add_u32(x, true); }
+
 constexpr int kTileThreads = 256;
 constexpr int kTileIters = 8;
 constexpr uint64_t kTile = (uint64_t)kTileThreads * kTileIters;  // 2048 keys per tile (24 KB of LDS image)
@@ -302,7 +306,8 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
                                                                  uint32_t parts, uint64_t n_tiles, uint32_t *cur,
                                                                  uint64_t cap, uint64_t ovf_base, uint64_t ovf_cap,
                                                                  int64_t *out_k, uint32_t *out_r, uint32_t *status,
-                                                                 uint32_t ablate, const uint32_t *counts, uint32_t chunk) {
+                                                                 uint32_t ablate, const uint32_t *counts, uint32_t chunk,
+                                                                 uint2 *runs, uint32_t *ovf_runs) {
   constexpr uint32_t kTileKeys = (uint32_t)THREADS * PER;
   static_assert(MAXP <= THREADS, "one partition per thread in the scan");
   __shared__ int64_t s_k[kTileKeys];
@@ -353,12 +358,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
     __syncthreads();
     // thread tid owns partition tid: block-wide exclusive scan + the segment reservation
     const uint32_t h = tid < parts ? s_hist[tid] : 0u;
-    uint32_t incl = h;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t v = (uint32_t)__shfl_up((int)incl, o);
-      if (lane >= (uint32_t)o) incl += v;
-    }
+    uint32_t incl = wave_incl_scan(h);
     if (lane == 63) s_wsum[wave] = incl;
     const uint32_t r = h && !CCJ_ABLATED(ablate, 0x40u) ? atomicAdd(&cur[(uint64_t)g * parts + tid], h) : 0u;  // flies during the image build
     __syncthreads();
@@ -390,6 +390,10 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
       }
       s_ovf[tid] = r2;
       s_olim[tid] = olim;
+      if (runs) {  // where this tile's rows of partition tid went (the ordered probe maps them back)
+        runs[tile * parts + tid] = make_uint2((uint32_t)(seg * cap + r), lim | olim << 16);
+        if (olim) ovf_runs[tile * parts + tid] = (uint32_t)(ovf_base + r2);
+      }
     }
     __syncthreads();
     if (tile + bpg < tend) load(tile + bpg);  // next tile's keys arrive while this one is written
@@ -421,10 +425,12 @@ uint64_t slot_seg_cap(uint64_t n, const SlotPlan &pl, uint32_t chunk) {
   return (c + chunk - 1) / chunk * chunk;
 }
 
+uint32_t slot_split_tile_keys() { return (uint32_t)kSplitThreads * (uint32_t)ccj_tune_int("CCJ_SPLIT_PER", kSplitPer); }
+
 hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPlan &pl, uint64_t cap,
                                    uint64_t ovf_base, uint64_t ovf_cap, uint32_t *cursors, int64_t *out_keys,
                                    uint32_t *out_rows, uint32_t *status, hipStream_t s, const uint32_t *counts,
-                                   uint32_t chunk) {
+                                   uint32_t chunk, uint2 *runs, uint32_t *ovf_runs) {
   const uint32_t parts = 1u << (pl.lo_bits + pl.hi_bits);
   hipError_t e = hipMemsetAsync(cursors, 0, ((size_t)parts * 8 + 1) * 4, s);
   if (e || n == 0) return e;
@@ -440,12 +446,12 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
   const uint32_t ablate = (uint32_t)ccj_tune_int("CCJ_ABLATE", 0);  // timing-only (tuning build)
   // keys per thread per tile: 11 (11264-key tiles, 141 KB of LDS); the tuning build sweeps 10-12
   const int per = ccj_tune_int("CCJ_SPLIT_PER", kSplitPer);
-  const uint32_t tile = (uint32_t)kSplitThreads * (uint32_t)per;
+  const uint32_t tile = slot_split_tile_keys();
   const uint64_t n_tiles = (n + tile - 1) / tile;
 #define CCJ_SPLIT_LAUNCH(C, P)                                                                                      \
   hipLaunchKernelGGL((slot_split_fixed<C, kSplitThreads, kSplitParts, P>), dim3(cus), dim3(kSplitThreads), 0, s, keys, n, \
                      pl.window_bits, parts, n_tiles, cursors, cap, ovf_base, ovf_cap, out_keys, out_rows, status, ablate, \
-                     counts, chunk)
+                     counts, chunk, runs, ovf_runs)
   if (per == 10) {
     if (counts) CCJ_SPLIT_LAUNCH(true, 10);
     else CCJ_SPLIT_LAUNCH(false, 10);

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CCJ_ABI_VERSION 3
+#define CCJ_ABI_VERSION 4
 
 enum ccj_status {
   CCJ_OK = 0,
@@ -143,6 +143,24 @@ typedef struct ccj_probe_args {
 } ccj_probe_args;
 
 int ccj_probe(const ccj_table *table, const ccj_probe_args *args, ccj_stream stream);
+
+/* Same outputs as ccj_probe — every chunk's per-Next stream in the reference's order (L3) — for
+ * large LP tables (>= 2^22 slots) with sel == NULL, computed through the slot-partitioned layout:
+ *   1. the one-pass slot split of the live rows (as ccj_probe_partitioned), which also records
+ *      where every split tile's run of every partition went;
+ *   2. a walk with the table window L2-resident that leaves each row's Next-round word (the
+ *      rounds in which it matches + its round count) at its partitioned position;
+ *   3. the words back into row order, one split tile per workgroup;
+ *   4. per chunk, the round-major / idx-ascending emit of linear_probing_ht.cpp:62-115 from them.
+ * Random slot reads become L2 hits instead of 128-byte HBM lines (C2: 1.24 lines per probe row on
+ * ccj_probe).  Other tables, sel != NULL, out_pos or payload columns run ccj_probe itself and need
+ * no workspace.  The partitioned route needs args->status: CCJ_FLAG_PART_OVERFLOW there (extreme
+ * key skew filled the split's overflow area) means the outputs are incomplete — re-run ccj_probe.
+ * ws: device workspace of ccj_probe_ordered_workspace_size bytes (0: no workspace needed).
+ * Replaces the same reference interface as ccj_probe. */
+size_t ccj_probe_ordered_workspace_size(const ccj_table *table, uint64_t n_rows, uint32_t chunk);
+int ccj_probe_ordered(const ccj_table *table, const ccj_probe_args *args, void *ws, size_t ws_bytes,
+                      ccj_stream stream);
 
 /* Slot-range-partitioned probe (the throughput path; L1/L2 parity, not L3 order).
  * LP tables only.  The probe column (args->keys, n_rows < 2^32; sel and counts must be NULL) is

@@ -342,3 +342,63 @@ def test_c2_table_size_reference_vector():
     assert int(pout["status"].item()) == 0
     assert ccj.result_checksum(pout, B, row_map=pout["row_map"].to(torch.int64)) == (want["matches"], want["l2"])
     table.free()
+
+
+@pytest.mark.parametrize("layout", [ccj.LAYOUT_REFERENCE, ccj.LAYOUT_DEVICE])
+@pytest.mark.parametrize("n_build,cf,n_probe,rng,chunk,ragged", [
+    (1 << 20, 1, 1 << 22, 1 << 20, 2048, False),
+    (1 << 20, 3, 3000000, 3 << 19, 2048, True),
+    (1 << 20, 1, 1 << 21, 5 << 20, 256, False),       # 80 % misses, the reference's default chunk
+    (1 << 20, 1, 999999, 1 << 20, 1000, True),        # ragged chunks of an odd width
+    (1 << 20, 40, 1 << 20, 1 << 20, 2048, False),     # runs longer than 26 rounds: re-walked chunks
+])
+def test_ordered_probe_equals_chunk_probe(layout, n_build, cf, n_probe, rng, chunk, ragged):
+    """ccj_probe_ordered (split -> round words -> back to row order -> emit) gives exactly
+    ccj_probe's outputs: per-chunk counts, rounds, every Next's count and the ordered
+    (sel, payload) stream (L3)."""
+    table = ccj.Table.reference(ccj.LP, n_build, cf, layout)
+    assert table.size >= 1 << 22
+    keys = ccj.gen_uniform_keys(n_probe, 23, rng)
+    counts = None
+    if ragged:
+        n_chunks = -(-n_probe // chunk)
+        g = np.random.default_rng(cf)
+        c = g.integers(0, chunk + 1, size=n_chunks).astype(np.int32)
+        c[::5] = chunk
+        c[-1] = min(c[-1], n_probe - (n_chunks - 1) * chunk)
+        counts = to_dev(c)
+    want = host(table.probe(keys, chunk, counts=counts))
+    got = host(table.probe_ordered(keys, chunk, counts=counts))
+    assert got["status"][0] == 0 and want["status"][0] == 0
+    assert np.array_equal(got["count"], want["count"])
+    assert np.array_equal(got["rounds"], want["rounds"])
+    assert np.array_equal(got["round_counts"], want["round_counts"])
+    cap = want["cap"]
+    valid = np.arange(cap)[None, :] < want["count"].astype(np.int64)[:, None]
+    assert np.array_equal(got["sel"].reshape(-1, cap)[valid], want["sel"].reshape(-1, cap)[valid])
+    assert np.array_equal(got["payload"].reshape(-1, cap)[valid], want["payload"].reshape(-1, cap)[valid])
+
+
+def test_ordered_probe_c2_table_reference_vector():
+    """ccj_probe_ordered on the reference-order 2^26-key table against the reference's own vector
+    (SURVEY §4 survey_lp_2048_64M_64M): matches, L2, the ordered L3 fold, the SURVEY checksum."""
+    entry = KA["sum_cases"]["survey_lp_2048_64M_64M"]
+    spec, want = entry["spec"], entry["variants"]["next"]
+    keys = to_dev(O.mt64_keys(spec["seed"], spec["n_probe"], spec["range"]))
+    table = ccj.Table.reference(ccj.LP, spec["n_build"], spec["cf"], ccj.LAYOUT_REFERENCE)
+    out = host(table.probe_ordered(keys, spec["B"], rounds=False))
+    assert out["status"][0] == 0 and not out.get("exact_retry")
+    assert O.result_sums(out["count"], out["sel"], out["payload"], out["cap"], spec["B"]) == \
+        (want["matches"], want["l2"], want["l3"], want["survey_chk"])
+    table.free()
+
+
+def test_ordered_probe_skew_retries_chunk_path():
+    """Extreme skew overflows the split's overflow area: the wrapper re-runs ccj_probe."""
+    n_build, n_probe = 1 << 20, 3 << 20
+    table = ccj.Table.reference(ccj.LP, n_build, 1, ccj.LAYOUT_REFERENCE)
+    keys = torch.full((n_probe,), 12345, dtype=torch.int64, device=DEV)
+    want = host(table.probe(keys, 2048))
+    got = host(table.probe_ordered(keys, 2048))
+    assert got["status"][0] == 0 and got.get("exact_retry")
+    assert np.array_equal(got["count"], want["count"]) and np.array_equal(got["sel"], want["sel"])
