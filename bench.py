@@ -82,6 +82,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-sample", type=int, default=1 << 28, help="probe keys in the multi-thread CPU sample")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-other", action="store_true", help="C2: do not time the other paths beside the headline")
     ap.add_argument("--lib", default="product", choices=["product", "tuning"],
                     help="tuning: libccj_tuning.so (make tuning; A/B sweeps with its env overrides)")
     a = ap.parse_args()
@@ -277,6 +278,15 @@ def bench_c3(args, dev, stream):
                        "cpu_model": cpu_model()}
     n_bar, m_bar = examined / n_probe, matches / n_probe
     alg = 8 + 8 + 8 * n_bar + 12 * m_bar  # key + off[b], off[b+1] + chain keys + (sel, payload)
+    c3_traffic = None  # DRAM bytes of the probe kernels per step (tools/profile.sh, profiles/pmc_c3_<path>.json)
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_c3_{args.path}.json")
+    if os.path.exists(pmc_path):
+        try:
+            pmc = json.load(open(pmc_path))
+            if pmc.get("n_probe") == n_probe and pmc.get("n_build") == n_build:
+                c3_traffic = pmc.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
     achieved = alg * n_probe / (probe_ms * 1e-3) / 1e9
     line = {
         "metric": METRIC, "value": n_probe / (wall / args.steps), "unit": "probe tuples/s", "n_gpus": 1,
@@ -286,7 +296,8 @@ def bench_c3(args, dev, stream):
         "config": {"workload": "C3: 1xMI355X chaining_ht + compactor, Zipf-skewed keys, ~10% match rate, "
                                f"{n_build} build / {n_probe} probe, chunk={chunk}", "parallelism": "dp1"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": c3_traffic,
+                     "traffic_GBps": c3_traffic / (probe_ms * 1e-3) / 1e9 if c3_traffic else None,
                      "kernel": ("ccj_probe_partitioned (bucket-range split + probe_chain_win<3>)" if part_mode
                                 else "probe_chunks<CHAIN,2>"),
                      "kernel_ms": probe_ms, "alg_bytes_per_tuple": alg, "chain_keys_per_tuple": n_bar,
@@ -436,12 +447,13 @@ def main():
             del bk, pay
         keys = ccj.gen_uniform_keys(n_probe, SEED, n_build, first_row=rank * n_probe, stream=stream)
         out = part = out_p = out_o = ws_o = None
-        if args.path == "chunk" or not c5:  # C2: every path (the headline and the ones timed beside it)
+        every = not c5 and not args.no_other  # C2: every path (the headline and the ones timed beside it)
+        if args.path == "chunk" or every:
             out = table.alloc_outputs(n_probe, chunk, rounds=True, payload_cols=P, pos=c5)
-        if args.path == "ordered" or not c5:
+        if args.path == "ordered" or every:
             out_o = table.alloc_outputs(n_probe, chunk, rounds=True)
             ws_o = table.alloc_ordered(n_probe, chunk)
-        if args.path == "partitioned" or not c5:
+        if args.path == "partitioned" or every:
             part = table.alloc_partitioned(n_probe, chunk)
             # C5: the match positions the payload gather reads are a caller-owned buffer, so no
             # allocation runs inside the timed step
@@ -498,7 +510,7 @@ def main():
         status = int(res0["status"].item())
         matches, l2 = ccj.result_checksum(res0, chunk, row_base=rank * n_probe, stream=stream)
     # the other paths, timed the same way (reported beside the headline)
-    others = [] if c5 else [q for q in ("ordered", "chunk", "partitioned") if q != args.path]
+    others = [] if c5 or args.no_other else [q for q in ("ordered", "chunk", "partitioned") if q != args.path]
     other_runs = {}
     for other in others:
         step(other)

@@ -17,7 +17,7 @@ for grp in FETCH_SIZE WRITE_SIZE "TCC_REQ_sum TCC_HIT_sum TCC_MISS_sum" "TCC_EA0
            "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES" "GRBM_GUI_ACTIVE"; do
   name=$(echo "$grp" | tr ' ' '+')
   echo "[profile] pmc $grp"
-  timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-include-regex "${PMC_KERNEL:-slot_split_fixed|probe_win}" -T -f csv -d "$OUT/pmc_$name" -o pmc \
+  timeout -s KILL 240 rocprofv3 --pmc $grp --kernel-include-regex "${PMC_KERNEL:-slot_split_fixed|probe_walk}" -T -f csv -d "$OUT/pmc_$name" -o pmc \
       -- python3 bench.py $ARGS --steps 2 --warmup 1 --no-cpu --no-verify > "$OUT/pmc_$name.log" 2>&1 || { echo "pmc $grp failed rc=$?"; tail -5 "$OUT/pmc_$name.log"; }
 done
 echo "[profile] done"
