@@ -65,7 +65,7 @@ EXPORTS = ["ccj_last_error", "ccj_abi_version", "ccj_device_init", "ccj_table_bu
            "ccj_pipeline_create",
            "ccj_pipeline_run", "ccj_pipeline_free", "ccj_pipeline_checksum", "ccj_partition_by_owner_fixed",
            "ccj_segment_chunk_counts", "ccj_pipeline_set_thresholds", "ccj_gen_c3_keys",
-           "ccj_probe_ordered_workspace_size", "ccj_probe_ordered"]
+           "ccj_probe_ordered_workspace_size", "ccj_probe_ordered", "ccj_probe_visits"]
 
 MAX_JOINS = 8
 COMPACT_NONE, COMPACT_FULL = 0, 1
@@ -113,6 +113,7 @@ def lib():
         L.ccj_gen_reference_keys.argtypes = [vp, u64, u64, u64, u64, vp]
         L.ccj_gen_c3_keys.argtypes = [vp, u64, u64, u64, u64, u64, C.c_uint32, vp]
         L.ccj_probe_cost.argtypes = [vp, vp, u64, vp, vp]
+        L.ccj_probe_visits.argtypes = [vp, vp, vp, C.c_uint32, C.c_uint32, vp, vp, vp]
         L.ccj_compact_workspace_size.restype = C.c_size_t
         L.ccj_compact_workspace_size.argtypes = [u64, u64, C.c_uint32, C.c_uint32, C.c_uint32]
         L.ccj_compact.argtypes = [C.POINTER(CompactArgs), vp]
@@ -399,6 +400,18 @@ class Table:
                 self.probe(keys, chunk, counts=counts, out=out, stream=stream)
                 out["exact_retry"] = True
         return out
+
+    def probe_visits(self, keys, sel=None, count: int | None = None, max_rounds: int | None = None, stream=None):
+        """ccj_probe_visits: (vals [count, max_rounds] int64, len [count] uint32) — the table value
+        row i = keys[sel[i]] visits in each round it stays active (InOneNext's writes)."""
+        import torch
+        n = int(sel.numel() if sel is not None else keys.numel()) if count is None else int(count)
+        mr = int(max_rounds or self.max_rounds + 1)
+        vals = torch.zeros((n, mr), dtype=torch.int64, device=keys.device)
+        ln = torch.zeros(n, dtype=torch.int32, device=keys.device)
+        check(lib().ccj_probe_visits(self._h, _ptr(keys), _ptr(sel) if sel is not None else None, n, mr, _ptr(vals),
+                                     _ptr(ln), _stream(stream)), "ccj_probe_visits")
+        return vals, ln
 
     def probe(self, keys, chunk: int, sel=None, counts=None, out=None, stream=None, **alloc_kw):
         """Batched Probe + Next loop (include/ccj.h ccj_probe).  Returns the output dict."""

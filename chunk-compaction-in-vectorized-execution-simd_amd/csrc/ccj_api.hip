@@ -839,6 +839,16 @@ int ccj_probe_cost(const ccj_table *t, const int64_t *d_keys, uint64_t n, uint64
   return CCJ_OK;
 }
 
+int ccj_probe_visits(const ccj_table *t, const int64_t *d_keys, const uint32_t *d_sel, uint32_t count,
+                     uint32_t max_rounds, int64_t *d_vals, uint32_t *d_len, ccj_stream stream) {
+  if (!t || (count && (!d_keys || !d_vals || !d_len || max_rounds == 0)))
+    return fail(CCJ_ERR_INVALID, "ccj_probe_visits: bad argument");
+  HIP_TRY(ccj::launch_probe_visits(t->info.kind, t->d_table, t->d_off, (uint32_t)(t->info.size - 1), d_keys, d_sel,
+                                   count, max_rounds, d_vals, d_len, (hipStream_t)stream),
+          "probe visits");
+  return CCJ_OK;
+}
+
 int ccj_result_checksum(const uint32_t *out_count, const uint32_t *out_sel, const int64_t *out_payload,
                         uint64_t n_chunks, uint64_t cap, uint32_t chunk, uint64_t row_base, uint64_t *d_acc,
                         ccj_stream stream) {

@@ -119,6 +119,9 @@ hipError_t launch_gen_c3(int64_t *out, uint64_t n, uint64_t seed, uint64_t first
 constexpr uint32_t kZipfBits = 16, kZipfBuckets = 1u << kZipfBits;
 hipError_t launch_gen_uniform(int64_t *out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t range,
                               hipStream_t s);
+hipError_t launch_probe_visits(int kind, const int64_t *table, const uint32_t *off, uint32_t mask,
+                               const int64_t *keys, const uint32_t *sel, uint32_t count, uint32_t max_rounds,
+                               int64_t *vals, uint32_t *len, hipStream_t s);
 hipError_t launch_probe_cost(int kind, const int64_t *table, const uint32_t *off, uint32_t mask,
                              const int64_t *keys, uint64_t n, unsigned long long *acc, hipStream_t s);
 hipError_t launch_result_checksum(const uint32_t *count, const uint32_t *sel, const int64_t *payload,

@@ -824,6 +824,31 @@ __global__ void probe_cost(const int64_t *table, const uint32_t *off, uint32_t m
   }
 }
 
+// ccj_probe_visits: the values InOneNext writes into result column m+1 for every active row
+// (linear_probing_ht.cpp:125-141, chaining_ht.cpp:148-163).  One thread per row; only the facade's
+// one-chunk InOneNext calls it, so it is a plain walk.
+template <int KIND>
+__global__ void probe_visits(const int64_t *table, const uint32_t *off, uint32_t mask, const int64_t *keys,
+                             const uint32_t *sel, uint32_t count, uint32_t max_rounds, int64_t *vals, uint32_t *len) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const int64_t k = keys[sel ? sel[i] : i];
+  const uint32_t h = (uint32_t)murmurhash64((uint64_t)k) & mask;
+  int64_t *v = vals + (uint64_t)i * max_rounds;
+  uint32_t r = 0;
+  if (KIND == CCJ_TABLE_LP) {
+    // active in round r while slot home + r is occupied (Probe :53-56, advance :136-140)
+    for (uint32_t s = h; r < max_rounds; s = (s + 1u) & mask) {
+      const int64_t x = table[s];
+      if (x == -1) break;
+      v[r++] = x;
+    }
+  } else {
+    for (uint32_t q = off[h], e = off[h + 1]; q < e && r < max_rounds; ++q) v[r++] = table[q];
+  }
+  len[i] = r;
+}
+
 __device__ __forceinline__ uint64_t fmix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
   z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
@@ -1903,6 +1928,18 @@ hipError_t launch_probe_cost(int kind, const int64_t *table, const uint32_t *off
   const dim3 g(grid_for(n, 256)), b(256);
   if (kind == CCJ_TABLE_LP) hipLaunchKernelGGL(probe_cost<CCJ_TABLE_LP>, g, b, 0, s, table, off, mask, keys, n, acc);
   else hipLaunchKernelGGL(probe_cost<CCJ_TABLE_CHAIN>, g, b, 0, s, table, off, mask, keys, n, acc);
+  return hipGetLastError();
+}
+
+hipError_t launch_probe_visits(int kind, const int64_t *table, const uint32_t *off, uint32_t mask,
+                               const int64_t *keys, const uint32_t *sel, uint32_t count, uint32_t max_rounds,
+                               int64_t *vals, uint32_t *len, hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  const dim3 g((count + 255) / 256), b(256);
+  if (kind == CCJ_TABLE_LP)
+    hipLaunchKernelGGL(probe_visits<CCJ_TABLE_LP>, g, b, 0, s, table, off, mask, keys, sel, count, max_rounds, vals, len);
+  else
+    hipLaunchKernelGGL(probe_visits<CCJ_TABLE_CHAIN>, g, b, 0, s, table, off, mask, keys, sel, count, max_rounds, vals, len);
   return hipGetLastError();
 }
 

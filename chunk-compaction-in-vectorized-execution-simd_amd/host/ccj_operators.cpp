@@ -120,6 +120,32 @@ class DeviceTable {
   }
   const ccj_table *handle() const { return t_; }
 
+  // ccj_probe_visits for one chunk: v.vals / v.len (the InOneNext side writes).  One pinned staging
+  // buffer mirrors one device buffer: [keys | sel | len | vals].
+  void Visits(ChunkVisits &v) {
+    Ensure();
+    const uint32_t count = (uint32_t)v.sel.size(), mr = max_rounds_;
+    v.stride = mr;
+    v.vals.assign((size_t)count * mr, 0);
+    v.len.assign(count, 0);
+    if (count) {
+      if (count > kBlockSize || v.keys.size() != kBlockSize) throw EngineError("InOneNext: chunk exceeds kBlockSize");
+      char *h = h_vis_, *d = d_vis_;
+      std::memcpy(h, v.keys.data(), v.keys.size() * 8);
+      std::memcpy(h + vis_sel_, v.sel.data(), count * 4);
+      hip_check(hipMemcpyAsync(d, h, vis_len_, hipMemcpyHostToDevice, stream_), "H2D");
+      check(ccj_probe_visits(t_, reinterpret_cast<const int64_t *>(d), reinterpret_cast<const uint32_t *>(d + vis_sel_),
+                             count, mr, reinterpret_cast<int64_t *>(d + vis_vals_), reinterpret_cast<uint32_t *>(d + vis_len_),
+                             stream_),
+            "ccj_probe_visits");
+      hip_check(hipMemcpyAsync(h + vis_len_, d + vis_len_, vis_end_ - vis_len_, hipMemcpyDeviceToHost, stream_), "D2H");
+      hip_check(hipStreamSynchronize(stream_), "sync");
+      std::memcpy(v.len.data(), h + vis_len_, count * 4);
+      std::memcpy(v.vals.data(), h + vis_vals_, v.vals.size() * 8);
+    }
+    v.loaded = true;
+  }
+
  private:
   static size_t Align(size_t x) { return (x + 15) & ~(size_t)15; }
   void Ensure() {
@@ -138,12 +164,20 @@ class DeviceTable {
     end_ = off_pay_ + cap_ * 8;
     hip_check(hipMalloc(&d_buf_, end_), "hipMalloc");
     hip_check(hipHostMalloc(&h_buf_, end_, hipHostMallocDefault), "hipHostMalloc");
+    vis_sel_ = Align(n * 8);
+    vis_len_ = Align(vis_sel_ + n * 4);
+    vis_vals_ = Align(vis_len_ + n * 4);
+    vis_end_ = vis_vals_ + n * (size_t)max_rounds_ * 8;
+    hip_check(hipMalloc(&d_vis_, vis_end_), "hipMalloc");
+    hip_check(hipHostMalloc(&h_vis_, vis_end_, hipHostMallocDefault), "hipHostMalloc");
     sized_for_ = n;
   }
   void Release() {
     if (d_buf_) (void)hipFree(d_buf_);
     if (h_buf_) (void)hipHostFree(h_buf_);
-    d_buf_ = h_buf_ = nullptr;
+    if (d_vis_) (void)hipFree(d_vis_);
+    if (h_vis_) (void)hipHostFree(h_vis_);
+    d_buf_ = h_buf_ = d_vis_ = h_vis_ = nullptr;
     sized_for_ = 0;
   }
 
@@ -155,6 +189,8 @@ class DeviceTable {
   uint32_t max_rounds_ = 0;
   size_t off_keys_ = 0, off_sel_ = 0, off_cnt_ = 0, off_hdr_ = 0, off_rc_ = 0, off_osel_ = 0, off_pay_ = 0, end_ = 0;
   char *d_buf_ = nullptr, *h_buf_ = nullptr;
+  size_t vis_sel_ = 0, vis_len_ = 0, vis_vals_ = 0, vis_end_ = 0;  // ccj_probe_visits staging
+  char *d_vis_ = nullptr, *h_vis_ = nullptr;
 };
 
 // Fills `result` with one Next result: Slice (base.cpp:37-47) + payload column m+1 at the selected
@@ -169,13 +205,29 @@ static void Materialise(const ChunkProbeResult &res, size_t pos, size_t rc, Data
   }
 }
 
+void ChunkVisits::Scribble(size_t round, DataChunk &input, DataChunk &result) {
+  if (!loaded) table->Visits(*this);
+  auto &col = result.data_[input.data_.size() + 1];
+  // active rows in slot_sel_vector_ order (ascending row), so a later row wins a shared position
+  for (size_t i = 0; i < sel.size(); ++i)
+    if (round < len[i]) col.GetValue(sel[i]) = vals[i * stride + round];
+}
+
+static ChunkVisits MakeVisits(DeviceTable *t, Vector &join_key, size_t count, const vector<uint32_t> &sel) {
+  ChunkVisits v;
+  v.table = t;
+  v.keys.assign(join_key.Data(), join_key.Data() + kBlockSize);
+  v.sel.assign(sel.begin(), sel.begin() + count);
+  return v;
+}
+
 // ---------------------------------------------------------------------------------------------
 LPHashTable::LPHashTable(size_t n, size_t cf) : t_(new DeviceTable(CCJ_TABLE_LP, n, cf)) {}
 LPHashTable::~LPHashTable() = default;
 const ccj_table *LPHashTable::handle() const { return t_->handle(); }
 
 LPScanStructure LPHashTable::Probe(Vector &join_key, size_t count, vector<uint32_t> &sel_vec) {
-  return LPScanStructure(t_->Run(join_key, count, sel_vec));
+  return LPScanStructure(t_->Run(join_key, count, sel_vec), MakeVisits(t_.get(), join_key, count, sel_vec));
 }
 
 size_t LPScanStructure::Next(Vector &, DataChunk &input, DataChunk &result) {
@@ -187,12 +239,22 @@ size_t LPScanStructure::Next(Vector &, DataChunk &input, DataChunk &result) {
   return rc;
 }
 
+size_t LPScanStructure::InOneNext(Vector &, DataChunk &input, DataChunk &result) {
+  result.Reset();
+  if (!HasNext()) return 0;
+  visits_.Scribble(round_, input, result);  // :133, before the slice of :144
+  const size_t rc = res_.round_counts[round_++];
+  Materialise(res_, pos_, rc, input, result);
+  pos_ += rc;
+  return rc;
+}
+
 HashTable::HashTable(size_t n, size_t cf) : t_(new DeviceTable(CCJ_TABLE_CHAIN, n, cf)) {}
 HashTable::~HashTable() = default;
 const ccj_table *HashTable::handle() const { return t_->handle(); }
 
 ScanStructure HashTable::Probe(Vector &join_key, size_t count, vector<uint32_t> &sel_vec) {
-  return ScanStructure(t_->Run(join_key, count, sel_vec));
+  return ScanStructure(t_->Run(join_key, count, sel_vec), MakeVisits(t_.get(), join_key, count, sel_vec));
 }
 
 size_t ScanStructure::EmitRound(DataChunk &input, DataChunk &result) {
@@ -216,6 +278,7 @@ size_t ScanStructure::Next(Vector &, DataChunk &input, DataChunk &result) {
 size_t ScanStructure::InOneNext(Vector &, DataChunk &input, DataChunk &result) {
   result.Reset();
   if (!HasNext()) return 0;
+  visits_.Scribble(round_, input, result);  // :156, before the slice of :168
   const size_t rc = EmitRound(input, result);
   result.count_ = rc;
   return rc;

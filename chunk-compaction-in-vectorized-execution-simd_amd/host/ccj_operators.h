@@ -11,8 +11,10 @@
 // returned scan structure then hands out the reference's Next() results one by one (LP: one per
 // probe round, possibly empty; chaining Next: rounds without matches merged, chaining_ht.cpp:82-107).
 // Differences from the reference, all deliberate:
-//  - InOneNext/SIMD* variants return the same results as Next (the reference's variants agree on
-//    every selected row; InOneNext additionally scribbles payloads of unmatched rows, :133).
+//  - SIMD* variants are the scalar ones (the reference's variants agree result for result).
+//    InOneNext / SIMDInOneNext also replay the reference's writes of the visited slot / chain key
+//    into result column m+1 for every active row, matched or not (linear_probing_ht.cpp:133,
+//    chaining_ht.cpp:156): the values come from one ccj_probe_visits launch on the first such call.
 //  - NaiveCompactor allocates a fresh temp chunk (the commented compactor.cpp:36), removing the
 //    aliasing defect of SURVEY §A.3.
 //  - Errors from the engine throw simd_compaction_amd::EngineError (the reference only asserts).
@@ -79,18 +81,35 @@ struct ChunkProbeResult {
 
 class DeviceTable;  // RAII wrapper of ccj_table + per-chunk probe buffers
 
+// What the InOneNext variants need beyond the matches: the chunk's probe rows (copied at Probe
+// time) and, fetched on first use, the table value each active row visits per round.
+struct ChunkVisits {
+  DeviceTable *table = nullptr;
+  vector<int64_t> keys;  // the probe column (kBlockSize rows)
+  vector<uint32_t> sel;  // Probe's sel_vec[0, count)
+  bool loaded = false;
+  uint32_t stride = 0;   // rounds per row in vals
+  vector<int64_t> vals;  // [row][round]
+  vector<uint32_t> len;  // rounds each row stays active
+  // result column m+1 at the physical row of every row active in `round` := its visited value
+  void Scribble(size_t round, DataChunk &input, DataChunk &result);
+};
+
 class LPScanStructure {
  public:
   size_t Next(Vector &join_key, DataChunk &input, DataChunk &result);
-  size_t InOneNext(Vector &join_key, DataChunk &input, DataChunk &result) { return Next(join_key, input, result); }
+  size_t InOneNext(Vector &join_key, DataChunk &input, DataChunk &result);  // :117-146
   size_t SIMDNext(Vector &join_key, DataChunk &input, DataChunk &result) { return Next(join_key, input, result); }
-  size_t SIMDInOneNext(Vector &join_key, DataChunk &input, DataChunk &result) { return Next(join_key, input, result); }
+  size_t SIMDInOneNext(Vector &join_key, DataChunk &input, DataChunk &result) {
+    return InOneNext(join_key, input, result);
+  }
   bool HasNext() const { return round_ < res_.round_counts.size(); }
 
  private:
   friend class LPHashTable;
-  explicit LPScanStructure(ChunkProbeResult res) : res_(std::move(res)) {}
+  LPScanStructure(ChunkProbeResult res, ChunkVisits v) : res_(std::move(res)), visits_(std::move(v)) {}
   ChunkProbeResult res_;
+  ChunkVisits visits_;
   size_t round_ = 0, pos_ = 0;
 };
 
@@ -122,9 +141,10 @@ class ScanStructure {
 
  private:
   friend class HashTable;
-  explicit ScanStructure(ChunkProbeResult res) : res_(std::move(res)) {}
+  ScanStructure(ChunkProbeResult res, ChunkVisits v) : res_(std::move(res)), visits_(std::move(v)) {}
   size_t EmitRound(DataChunk &input, DataChunk &result);
   ChunkProbeResult res_;
+  ChunkVisits visits_;
   size_t round_ = 0, pos_ = 0;
 };
 

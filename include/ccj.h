@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CCJ_ABI_VERSION 4
+#define CCJ_ABI_VERSION 5
 
 enum ccj_status {
   CCJ_OK = 0,
@@ -161,6 +161,17 @@ int ccj_probe(const ccj_table *table, const ccj_probe_args *args, ccj_stream str
 size_t ccj_probe_ordered_workspace_size(const ccj_table *table, uint64_t n_rows, uint32_t chunk);
 int ccj_probe_ordered(const ccj_table *table, const ccj_probe_args *args, void *ws, size_t ws_bytes,
                       ccj_stream stream);
+
+/* The table values one chunk's rows visit, round by round: the side effect of the reference's
+ * InOneNext / SIMDInOneNext, which write the visited slot (LP) or chain key (chaining) into result
+ * column m+1 at the row's physical position for EVERY active row, matched or not
+ * (linear_probing_ht.cpp:133, :301, :322; chaining_ht.cpp:156, :341, :362).  Row i = keys[sel[i]]
+ * (sel NULL: keys[i]), i < count; d_len[i] = the number of rounds it stays active (LP: the
+ * non-empty run from its home slot; chaining: its chain's length), capped at max_rounds;
+ * d_vals[i * max_rounds + r] = the value visited in round r < d_len[i].  The facade's
+ * InOneNext replays these writes (host/ccj_operators.cpp); the batched paths never need them. */
+int ccj_probe_visits(const ccj_table *table, const int64_t *d_keys, const uint32_t *d_sel, uint32_t count,
+                     uint32_t max_rounds, int64_t *d_vals, uint32_t *d_len, ccj_stream stream);
 
 /* Slot-range-partitioned probe (the throughput path; L1/L2 parity, not L3 order).
  * LP tables only.  The probe column (args->keys, n_rows < 2^32; sel and counts must be NULL) is
@@ -311,9 +322,9 @@ int ccj_segment_chunk_counts(const uint64_t *d_seg_counts, uint32_t n_segs, uint
 int ccj_gen_uniform_keys(int64_t *d_out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t range,
                          ccj_stream stream);
 /* C3 probe column (BASELINE configs[2]): row i is, with probability hit_ppm / 1e6, a
- * build key of the reference generator (n_build, cf) drawn with Zipf-like skew (log-uniform rank
- * over dyadic levels, ranks spread by a fixed permutation), else a key in [n_build, 2^62) that
- * matches nothing — the stream of oracle/ccj_gen.h ccj_c3_key. */
+ * build key of the reference generator (n_build, cf) drawn with Zipf s = 1 skew over its distinct
+ * keys (a 2^16-bucket inverse-CDF table, ranks spread by a fixed permutation), else a key in
+ * [n_build, 2^62) that matches nothing — the stream of oracle/ccj_gen.h ccj_c3_key. */
 int ccj_gen_c3_keys(int64_t *d_out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t n_build, uint64_t cf,
                     uint32_t hit_ppm, ccj_stream stream);
 /* Build-side keys first..first+n-1 of the reference generator for n_total tuples

@@ -73,6 +73,13 @@ struct Sink {
       if (trace) printf(" %u:%lld", s, (long long)p);
     }
     if (trace) printf("\n");
+    if (trace) {
+      // result column m+1 over all kBlockSize physical rows: InOneNext also writes unmatched
+      // active rows (linear_probing_ht.cpp:133, chaining_ht.cpp:156), visible here only
+      uint64_t h = CCJ_L3_SEED;
+      for (size_t s = 0; s < kBlockSize; ++s) h = ccj_l3_fold(h, s, result.data_[m + 1].GetValue(s));
+      printf("P %llu\n", (unsigned long long)h);
+    }
   }
 };
 

@@ -7,9 +7,11 @@ script only runs in the build container, where the reference tree exists; the fi
 are data (inputs + expected outputs) and are committed so the tests never need the reference.
 
   python tests/golden/make_golden.py          # rebuilds _ref/ref_driver if needed
+  python tests/golden/make_golden.py phys     # only the trace_*_phys.npz files
 
 Outputs
   trace_<case>_<view>.npz   per-Next traces (every Next call: chunk, rc, result.sel, payload)
+  trace_<case>_phys.npz     per variant, result column m+1 over every physical row after each Next
   known_answers.json        counts / checksums for larger runs and the main.cpp pipeline
 """
 from __future__ import annotations
@@ -115,6 +117,22 @@ def parse_trace(out):
     )
 
 
+def parse_phys(out):
+    """Per Next call: the fold of result column m+1 over all kBlockSize physical rows ("P" lines)."""
+    return np.array([int(l.split()[1]) for l in out.splitlines() if l.startswith("P ")], np.uint64)
+
+
+def make_phys():
+    """trace_<case>_phys.npz: per variant, the physical payload-column fold after every Next call.
+    Next / SIMDNext write matched rows only; InOneNext / SIMDInOneNext also write the visited value of
+    every unmatched active row (linear_probing_ht.cpp:133, chaining_ht.cpp:156)."""
+    for name, (kind, B, n, cf, npb, rng, seed, gen, selm) in TRACE_CASES.items():
+        ph = {v: parse_phys(run(["probe", kind, v, B, n, cf, npb, rng, seed, gen, selm, 1])) for v in VARIANTS}
+        assert np.array_equal(ph["next"], ph["simdnext"]) and np.array_equal(ph["inone"], ph["simdinone"]), name
+        np.savez_compressed(os.path.join(HERE, f"trace_{name}_phys.npz"), **ph)
+        print("phys", name, {v: len(x) for v, x in ph.items()}, flush=True)
+
+
 def same(a, b):
     return all(np.array_equal(a[k], b[k]) for k in a)
 
@@ -122,6 +140,9 @@ def same(a, b):
 def main():
     if not os.path.exists(DRIVER):
         subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
+    make_phys()
+    if sys.argv[1:] == ["phys"]:
+        return 0
     answers = {"trace_cases": {}, "sum_cases": {}, "pipe_cases": {}}
     for name, (kind, B, n, cf, npb, rng, seed, gen, selm) in TRACE_CASES.items():
         traces = {}

@@ -4,7 +4,8 @@
 // result, for comparison with the per-Next traces recorded from the reference itself
 // (tests/golden/trace_*).
 //   facade_trace <lp|chain> <next|inone|simdnext|simdinone> B n_build cf n_probe range seed selmode
-// Output: "N <chunk> <rc>" per Next call, then "M <sel> <payload>" per result row.
+// Output: "N <chunk> <rc>" per Next call, then "M <sel> <payload>" per result row, then "P <fold>"
+// of result column m+1 over all kBlockSize physical rows.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -54,6 +55,10 @@ static void Run(Table &ht, const std::string &variant, size_t n_probe, uint64_t 
         const uint32_t s = output.selection_vector_[i];
         printf("M %u %lld\n", s, (long long)output.data_[2].GetValue(s));
       }
+      // column m+1 over every physical row (InOneNext's writes to unmatched active rows included)
+      uint64_t h = CCJ_L3_SEED;
+      for (size_t s = 0; s < kBlockSize; ++s) h = ccj_l3_fold(h, s, output.data_[2].GetValue(s));
+      printf("P %llu\n", (unsigned long long)h);
     }
   }
 }
