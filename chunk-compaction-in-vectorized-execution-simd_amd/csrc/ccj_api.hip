@@ -622,7 +622,7 @@ OrderedLayout ordered_layout(const ccj_table *t, uint64_t n_rows, uint32_t chunk
   O.L = part_layout(t, n_rows, chunk);
   if (O.L.pl.lo_bits == 0) return O;
   O.partitioned = true;
-  O.tile = ccj::slot_split_tile_keys();
+  O.tile = ccj::slot_split_tile_keys(1u << (O.L.pl.lo_bits + O.L.pl.hi_bits));
   O.n_tiles = (n_rows + O.tile - 1) / O.tile;
   size_t off = 0;
   auto take = [&](size_t bytes) {

@@ -157,13 +157,13 @@ uint64_t slot_seg_cap(uint64_t n, const SlotPlan &pl, uint32_t chunk);
 // cursors[parts * 8] = rows that went to the overflow area [ovf_base, ovf_base + ovf_cap).
 // counts: live rows per input chunk.  runs (optional; the ordered probe): per (tile, partition)
 // {segment position of the run, segment length | overflow-area length << 16}; ovf_runs: the
-// overflow-area position where that length is non-zero.  Tiles are slot_split_tile_keys() keys.
+// overflow-area position where that length is non-zero.  Tiles are slot_split_tile_keys(parts) keys.
 hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPlan &pl, uint64_t cap,
                                    uint64_t ovf_base, uint64_t ovf_cap, uint32_t *cursors, int64_t *out_keys,
                                    uint32_t *out_rows, uint32_t *status, hipStream_t s,
                                    const uint32_t *counts = nullptr, uint32_t chunk = 0, uint2 *runs = nullptr,
                                    uint32_t *ovf_runs = nullptr);
-uint32_t slot_split_tile_keys();
+uint32_t slot_split_tile_keys(uint32_t parts);
 hipError_t launch_partition_fixed(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t row_base, uint64_t seg_cap,
                                   int64_t *out_keys, uint32_t *out_rows, uint64_t *out_counts, uint32_t *status,
                                   void *ws, hipStream_t s);

@@ -312,9 +312,10 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
   static_assert(MAXP <= THREADS, "one partition per thread in the scan");
   __shared__ int64_t s_k[kTileKeys];
   __shared__ uint32_t s_ovf[MAXP], s_olim[MAXP];  // overflow-area run: start, length
-  // image row: tile-local row (16 bits); the partition is re-hashed when the row is written (keeping
-  // it beside the row measured the same)
-  __shared__ uint16_t s_i[kTileKeys];
+  // image entry: tile-local row (low 16 bits) | partition << 16, so the write phase does not hash the
+  // key again (C2: 5.57 ms against 6.03 with the second hash; tools/hashbench: 46 SIMD cycles per
+  // wave-hash)
+  __shared__ uint32_t s_i[kTileKeys];
   __shared__ uint32_t s_hist[MAXP], s_loc[MAXP], s_lim[MAXP];
   __shared__ uint64_t s_dst[MAXP];
   __shared__ uint32_t s_wsum[THREADS / 64], s_tot;
@@ -360,7 +361,10 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
     const uint32_t h = tid < parts ? s_hist[tid] : 0u;
     uint32_t incl = wave_incl_scan(h);
     if (lane == 63) s_wsum[wave] = incl;
-    const uint32_t r = h && !CCJ_ABLATED(ablate, 0x40u) ? atomicAdd(&cur[(uint64_t)g * parts + tid], h) : 0u;  // flies during the image build
+    uint32_t r = h && !CCJ_ABLATED(ablate, 0x40u) ? atomicAdd(&cur[(uint64_t)g * parts + tid], h) : 0u;  // flies during the image build
+    // (timing only, 0xC0: no reservation atomics, runs at their expected offsets: 9.5 ms, not less —
+    // the atomics keep one segment's runs written close together in time, so its L2 merges them)
+    if CCJ_ABLATED(ablate, 0x80u) r = (uint32_t)(((tile - g * n_tiles / 8) * (kTileKeys / parts)) % cap);
     __syncthreads();
     uint32_t wpre = 0;
     for (uint32_t w = 0; w < wave; ++w) wpre += s_wsum[w];
@@ -373,7 +377,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
       if ((live >> it) & 1u) {
         const uint32_t pos = s_loc[dd[it]] + rk[it];
         s_k[pos] = kk[it];
-        s_i[pos] = (uint16_t)li;
+        s_i[pos] = li | dd[it] << 16;
       }
     }
     if (tid < parts) {
@@ -397,11 +401,13 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
     }
     __syncthreads();
     if (tile + bpg < tend) load(tile + bpg);  // next tile's keys arrive while this one is written
+    // (An unrolled write loop with a fixed store count, so that the next tile's keys are awaited
+    // with vmcnt(2 * PER) and these stores drain under the next tile's ranking, measured 7.8 ms
+    // against 5.6: the reservation atomics then queue behind the stores.)
     const uint32_t tl = s_tot;  // rows in the image
     for (uint32_t q = tid; q < tl; q += THREADS) {
       const int64_t k = s_k[q];
-      const uint32_t si = s_i[q];
-      const uint32_t d = (uint32_t)(murmurhash64((uint64_t)k) >> shift) & mask;
+      const uint32_t si = s_i[q], d = si >> 16;
       const uint32_t o = q - s_loc[d];
       const uint32_t lim = s_lim[d];
       if ((o < lim || o - lim < s_olim[d]) && !CCJ_ABLATED(ablate, 0x10u)) {  // (0x10: timing only, no stores)
@@ -425,7 +431,14 @@ uint64_t slot_seg_cap(uint64_t n, const SlotPlan &pl, uint32_t chunk) {
   return (c + chunk - 1) / chunk * chunk;
 }
 
-uint32_t slot_split_tile_keys() { return (uint32_t)kSplitThreads * (uint32_t)ccj_tune_int("CCJ_SPLIT_PER", kSplitPer); }
+// keys per thread per tile: 11 (11264-key tiles, 149 KB of LDS with <= 512 partitions); 1024
+// partitions leave room for 10 (the tuning build sweeps 10-12 below that)
+static int split_per(uint32_t parts) {
+  const int per = ccj_tune_int("CCJ_SPLIT_PER", kSplitPer);
+  return parts > kSplitParts / 2 && per > 10 ? 10 : per;
+}
+
+uint32_t slot_split_tile_keys(uint32_t parts) { return (uint32_t)kSplitThreads * (uint32_t)split_per(parts); }
 
 hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPlan &pl, uint64_t cap,
                                    uint64_t ovf_base, uint64_t ovf_cap, uint32_t *cursors, int64_t *out_keys,
@@ -434,7 +447,7 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
   const uint32_t parts = 1u << (pl.lo_bits + pl.hi_bits);
   hipError_t e = hipMemsetAsync(cursors, 0, ((size_t)parts * 8 + 1) * 4, s);
   if (e || n == 0) return e;
-  // One persistent 1024-thread workgroup per CU (141 KB of LDS), a multiple of 8 (one tile group
+  // One persistent 1024-thread workgroup per CU (<= 149 KB of LDS), a multiple of 8 (one tile group
   // per XCD).  Two 512-thread workgroups per CU on 6144-key tiles (same run length at 512
   // partitions, phases overlapping between the two) measured 7.8 ms against 6.5 at C2.
   static const unsigned cus = [] {
@@ -444,23 +457,25 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
     return (unsigned)(n >= 8 ? n / 8 * 8 : 8);
   }();
   const uint32_t ablate = (uint32_t)ccj_tune_int("CCJ_ABLATE", 0);  // timing-only (tuning build)
-  // keys per thread per tile: 11 (11264-key tiles, 141 KB of LDS); the tuning build sweeps 10-12
-  const int per = ccj_tune_int("CCJ_SPLIT_PER", kSplitPer);
-  const uint32_t tile = slot_split_tile_keys();
+  const int per = split_per(parts);
+  const uint32_t tile = slot_split_tile_keys(parts);
   const uint64_t n_tiles = (n + tile - 1) / tile;
-#define CCJ_SPLIT_LAUNCH(C, P)                                                                                      \
-  hipLaunchKernelGGL((slot_split_fixed<C, kSplitThreads, kSplitParts, P>), dim3(cus), dim3(kSplitThreads), 0, s, keys, n, \
+#define CCJ_SPLIT_LAUNCH(C, MAXP, P)                                                                                \
+  hipLaunchKernelGGL((slot_split_fixed<C, kSplitThreads, MAXP, P>), dim3(cus), dim3(kSplitThreads), 0, s, keys, n,       \
                      pl.window_bits, parts, n_tiles, cursors, cap, ovf_base, ovf_cap, out_keys, out_rows, status, ablate, \
                      counts, chunk, runs, ovf_runs)
-  if (per == 10) {
-    if (counts) CCJ_SPLIT_LAUNCH(true, 10);
-    else CCJ_SPLIT_LAUNCH(false, 10);
+  if (parts > kSplitParts / 2) {  // 1024 partitions: 10 keys per thread
+    if (counts) CCJ_SPLIT_LAUNCH(true, kSplitParts, 10);
+    else CCJ_SPLIT_LAUNCH(false, kSplitParts, 10);
+  } else if (per == 10) {
+    if (counts) CCJ_SPLIT_LAUNCH(true, kSplitParts / 2, 10);
+    else CCJ_SPLIT_LAUNCH(false, kSplitParts / 2, 10);
   } else if (per == 12) {
-    if (counts) CCJ_SPLIT_LAUNCH(true, 12);
-    else CCJ_SPLIT_LAUNCH(false, 12);
+    if (counts) CCJ_SPLIT_LAUNCH(true, kSplitParts / 2, 12);
+    else CCJ_SPLIT_LAUNCH(false, kSplitParts / 2, 12);
   } else {
-    if (counts) CCJ_SPLIT_LAUNCH(true, kSplitPer);
-    else CCJ_SPLIT_LAUNCH(false, kSplitPer);
+    if (counts) CCJ_SPLIT_LAUNCH(true, kSplitParts / 2, kSplitPer);
+    else CCJ_SPLIT_LAUNCH(false, kSplitParts / 2, kSplitPer);
   }
 #undef CCJ_SPLIT_LAUNCH
   return hipGetLastError();
