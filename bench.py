@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5", "pipeline"])
     ap.add_argument("--batches", type=int, default=4, help="N > 1: exchange batches per step (pipelined)")
+    ap.add_argument("--group", type=int, default=16,
+                    help="N > 1: received batches per local probe (each local probe sweeps the whole table)")
     ap.add_argument("--sharded", action="store_true", help="run the N > 1 protocol even at N = 1 (rehearsal)")
     ap.add_argument("--pipe-lhs", type=int, default=20000000)
     ap.add_argument("--pipe-rhs", type=int, default=2000000)
@@ -639,7 +641,7 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
     t0 = time.perf_counter()
     with torch.cuda.stream(stream):
         sp = ccj_dist.ShardedProbe(n_build_total, 1, n_probe, chunk, world, rank, stream=stream,
-                                   batches=args.batches)
+                                   batches=args.batches, group=args.group)
         keys = ccj.gen_uniform_keys(n_probe, SEED, n_build_total, first_row=rank * n_probe, stream=stream)
     torch.cuda.synchronize()
     log(f"[rank {rank}] setup {time.perf_counter() - t0:.1f} s, local build {sp.n_build_local}, "
@@ -670,7 +672,7 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
     # verification (untimed): global L1 / L2 against the exact membership answer
     m, l2 = sp.step(keys, rank * n_probe, verify=True)
     rk = sp.received_keys(sp.batches - 1)
-    examined, _ = sp.table.probe_cost(rk, stream=stream)
+    examined, _ = sp.ops.probe_cost(rk, stream)
     s_bar = examined / max(rk.numel(), 1)
     tot = torch.tensor([m, l2 - (1 << 64) if l2 >= (1 << 63) else l2], dtype=torch.int64, device=dev)
     dist.all_reduce(tot)
@@ -694,7 +696,8 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
             "config": {"workload": f"C4: {world}xMI355X radix-partitioned LP join, {n_build_total} build / "
                                    f"{world * n_probe} probe int64, chunk=2048, RCCL all-to-all tuple shuffle",
                        "table": "linear_probing", "n_build_total": n_build_total, "n_probe_per_gpu": n_probe,
-                       "chunk": chunk, "batches": sp.batches, "parallelism": f"dp{world} (owner-partitioned)"},
+                       "chunk": chunk, "batches": sp.batches, "group": sp.group,
+                       "parallelism": f"dp{world} (owner-partitioned)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernel": "ccj_probe_partitioned (local split + walk of received tuples, slowest rank)",

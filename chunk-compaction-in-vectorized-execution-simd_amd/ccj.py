@@ -65,6 +65,7 @@ EXPORTS = ["ccj_last_error", "ccj_abi_version", "ccj_device_init", "ccj_table_bu
            "ccj_pipeline_create",
            "ccj_pipeline_run", "ccj_pipeline_free", "ccj_pipeline_checksum", "ccj_partition_by_owner_fixed",
            "ccj_segment_chunk_counts", "ccj_pipeline_set_thresholds", "ccj_gen_c3_keys",
+           "ccj_partition_grouped_workspace_size", "ccj_partition_by_owner_grouped", "ccj_partition_grouped_sub_cap",
            "ccj_probe_ordered_workspace_size", "ccj_probe_ordered", "ccj_probe_visits"]
 
 MAX_JOINS = 8
@@ -125,6 +126,12 @@ def lib():
         L.ccj_partition_by_owner_fixed.argtypes = [vp, u64, C.c_uint32, C.c_uint32, u64, vp, vp, vp, vp, vp,
                                                    C.c_size_t, vp]
         L.ccj_segment_chunk_counts.argtypes = [vp, C.c_uint32, u64, C.c_uint32, vp, vp, vp]
+        L.ccj_partition_grouped_workspace_size.argtypes = [C.c_uint32]
+        L.ccj_partition_grouped_workspace_size.restype = C.c_size_t
+        L.ccj_partition_grouped_sub_cap.argtypes = [u64, C.c_uint32, C.c_uint32]
+        L.ccj_partition_grouped_sub_cap.restype = u64
+        L.ccj_partition_by_owner_grouped.argtypes = [vp, u64, C.c_uint32, C.c_uint32, u64, vp, vp, vp, vp, vp,
+                                                     C.c_size_t, vp]
         L.ccj_pipeline_create.argtypes = [C.POINTER(vp), C.c_uint32, C.c_uint32, i32, C.POINTER(vp)]
         L.ccj_pipeline_run.argtypes = [vp, C.POINTER(vp), u64, vp, C.POINTER(PipelineResult)]
         L.ccj_pipeline_free.argtypes = [vp]
@@ -511,6 +518,35 @@ class FixedOwnerPartitioner:
                                                  _ptr(out_keys), _ptr(out_rows), _ptr(out_counts), _ptr(status),
                                                  _ptr(self.ws), self.ws_bytes, _stream(stream)),
               "ccj_partition_by_owner_fixed")
+
+
+OWNER_GROUPS = 8  # CCJ_OWNER_GROUPS
+
+
+class GroupedOwnerPartitioner:
+    """One-pass fixed-capacity owner partitioning (ccj_partition_by_owner_grouped): destination d's
+    region is OWNER_GROUPS sub-segments of sub_cap slots, sub-segment (d, g) at (d*8 + g)*sub_cap
+    holding counts[d*8 + g] rows (u32 row ids row_base + i)."""
+
+    def __init__(self, n: int, parts: int, sub_cap: int, device=None):
+        import torch
+        dev = device or torch.device("cuda", torch.cuda.current_device())
+        self.n, self.parts, self.sub_cap = n, parts, sub_cap
+        self.ws_bytes = lib().ccj_partition_grouped_workspace_size(parts)
+        self.ws = torch.empty(max(self.ws_bytes, 8), dtype=torch.uint8, device=dev)
+
+    def __call__(self, keys, row_base, out_keys, out_rows, out_counts, status, stream=None):
+        assert keys.numel() == self.n and out_keys.numel() >= self.parts * OWNER_GROUPS * self.sub_cap
+        assert out_counts.numel() >= self.parts * OWNER_GROUPS
+        check(lib().ccj_partition_by_owner_grouped(_ptr(keys), self.n, self.parts, row_base, self.sub_cap,
+                                                   _ptr(out_keys), _ptr(out_rows), _ptr(out_counts), _ptr(status),
+                                                   _ptr(self.ws), self.ws_bytes, _stream(stream)),
+              "ccj_partition_by_owner_grouped")
+
+
+def grouped_sub_cap(n: int, parts: int, chunk: int) -> int:
+    """Sub-segment capacity for GroupedOwnerPartitioner over n uniformly hashed keys."""
+    return int(lib().ccj_partition_grouped_sub_cap(n, parts, chunk))
 
 
 def segment_chunk_counts(seg_counts, seg_cap: int, chunk: int, out, status, stream=None):

@@ -51,10 +51,12 @@ def seg_capacity(n: int, world: int, chunk: int) -> int:
     return (cap + chunk - 1) // chunk * chunk
 
 
-def batch_count(n_probe: int, world: int, chunk: int, at_least: int = 1) -> int:
-    """Batches per step so that one batch's key buffer (world segments of int64) fits MAX_A2A_BYTES."""
+def batch_count(n_probe: int, world: int, chunk: int, at_least: int = 1, subs: int = 1, cap=None) -> int:
+    """Batches per step so that one batch's key buffer (world * subs segments of int64) fits
+    MAX_A2A_BYTES.  cap(n): the sub-segment capacity for a batch of n keys."""
+    cap = cap or (lambda n: seg_capacity(n, world * subs, chunk))
     b = max(1, at_least)
-    while world * seg_capacity(-(-n_probe // b), world, chunk) * 8 > MAX_A2A_BYTES and b < n_probe:
+    while world * subs * cap(-(-n_probe // b)) * 8 > MAX_A2A_BYTES and b < n_probe:
         b *= 2
     return b
 
@@ -136,8 +138,14 @@ class DeviceOps:
         return own_keys.numel()
 
     # pipelined protocol
-    def fixed_partitioner(self, n, world, seg_cap):
-        p = self.ccj.FixedOwnerPartitioner(n, world, seg_cap, device=self.device)
+    # sub-segments per destination: the one-pass grouped partition fills one per XCD
+    subs = 8
+
+    def sub_capacity(self, n, world, chunk):
+        return self.ccj.grouped_sub_cap(n, world, chunk)
+
+    def fixed_partitioner(self, n, world, sub_cap):
+        p = self.ccj.GroupedOwnerPartitioner(n, world, sub_cap, device=self.device)
         return lambda keys, row_base, sk, sr, sc, status, stream: p(keys, row_base, sk, sr, sc, status, stream=stream)
 
     def segment_chunk_counts(self, seg_counts, seg_cap, chunk, out, status, stream):
@@ -192,14 +200,18 @@ class ShardedProbe:
         self.n_build_local = o.build_local(n_build_total, cf, world, rank, self.stream)
         # batched, fixed-capacity exchange buffers: two send slots; receive buffers of `group`
         # batches each, two of them, so one group is probed while the next one arrives
-        self.batches = batch_count(n_probe, world, chunk, batches)
+        # a destination's region: `subs` sub-segments (the device partitioner fills one per XCD)
+        self.subs = getattr(o, "subs", 1)
+        sub_cap = getattr(o, "sub_capacity", None)
+        cap = (lambda n: sub_cap(n, world, chunk)) if sub_cap else (lambda n: seg_capacity(n, world * self.subs, chunk))
+        self.batches = batch_count(n_probe, world, chunk, batches, self.subs, cap)
         self.bn = -(-n_probe // self.batches)
         self.group = min(self.batches, group)
         self.n_groups = -(-self.batches // self.group)
         # the rank's status word: owner-split overflow, receive-count overflow and the local
         # probe's own flags (slot-split overflow, output capacity) all land here
         self.status = o.zeros(1, torch.int32)
-        self._resize(seg_capacity(self.bn, world, chunk))
+        self._resize(cap(self.bn))
         ev = lambda: [o.event() for _ in range(2)]  # noqa: E731
         self.ev_part, self.ev_comm, self.ev_probe = ev(), ev(), ev()
         self.probe_events = []
@@ -207,19 +219,22 @@ class ShardedProbe:
         self.last_exact = False
         self.exact_steps = 0  # steps redone with the exact-size protocol (on every rank alike)
 
-    def _resize(self, seg_cap: int):
-        """(Re)allocate the exchange buffers for receive segments of seg_cap slots."""
-        assert seg_cap % self.chunk == 0
+    def _resize(self, sub_cap: int):
+        """(Re)allocate the exchange buffers for receive sub-segments of sub_cap slots (a source's
+        region: subs of them, seg_cap slots)."""
+        assert sub_cap % self.chunk == 0
         o = self.ops
-        self.seg_cap = seg_cap
+        self.sub_cap = sub_cap
+        self.seg_cap = seg_cap = self.subs * sub_cap
+        self.nseg = self.world * self.subs  # received sub-segments per batch
         slots = self.world * seg_cap  # one batch's receive segments
         self.slots = slots
         gslots = self.group * slots
         self.fparts = {}
         mk = lambda dt, n: [o.zeros(n, dt) for _ in range(2)]  # noqa: E731
-        self.sk, self.sr, self.sc = mk(torch.int64, slots), mk(torch.int32, slots), mk(torch.int64, self.world)
+        self.sk, self.sr, self.sc = mk(torch.int64, slots), mk(torch.int32, slots), mk(torch.int64, self.nseg)
         self.rk, self.rr = mk(torch.int64, gslots), mk(torch.int32, gslots)
-        self.rc = mk(torch.int64, self.group * self.world)
+        self.rc = mk(torch.int64, self.group * self.nseg)
         self.cc = mk(torch.int32, gslots // self.chunk)
         # local probe on the slot-partitioned path, one call per group of received batches
         self.parts, self.outs = [], []
@@ -237,7 +252,7 @@ class ShardedProbe:
         gs, sub = (i // self.group) % 2, i % self.group
         lo = sub * self.slots
         return (gs, self.rk[gs][lo:lo + self.slots], self.rr[gs][lo:lo + self.slots],
-                self.rc[gs][sub * self.world:(sub + 1) * self.world])
+                self.rc[gs][sub * self.nseg:(sub + 1) * self.nseg])
 
     # ---- pipelined fixed-capacity step ----
     # Send slot s = i % 2 serves batches i, i+2, ...; receive group slot g % 2 serves groups g, g+2;
@@ -247,7 +262,7 @@ class ShardedProbe:
         s = i % 2
         lo, n = self._batch(i)
         if n not in self.fparts:
-            self.fparts[n] = self.ops.fixed_partitioner(n, self.world, self.seg_cap)
+            self.fparts[n] = self.ops.fixed_partitioner(n, self.world, self.sub_cap)
         self.pstream.wait_event(self.ev_comm[s])  # the previous all-to-all from send slot s is done
         self.fparts[n](keys[lo:lo + n], lo, self.sk[s], self.sr[s], self.sc[s], self.status, self.pstream)
         self.ev_part[s].record(self.pstream)
@@ -274,7 +289,7 @@ class ShardedProbe:
         per = self.slots // self.chunk
         for i in range(first, last + 1):
             sub = i % self.group
-            o.segment_chunk_counts(self.rc[gs][sub * self.world:(sub + 1) * self.world], self.seg_cap, self.chunk,
+            o.segment_chunk_counts(self.rc[gs][sub * self.nseg:(sub + 1) * self.nseg], self.sub_cap, self.chunk,
                                    self.cc[gs][sub * per:(sub + 1) * per], self.status, self.stream)
         if last - first + 1 < self.group:  # a short last group: its missing batches have no live rows
             with o.on(self.stream):
@@ -297,7 +312,7 @@ class ShardedProbe:
         gs, rk, rr, rc = self._recv(i)
         self.ops.current().wait_event(self.ev_comm[i % 2])
         pos = torch.arange(self.slots, device=rk.device)
-        live = (pos % self.seg_cap) < rc[pos // self.seg_cap]
+        live = (pos % self.sub_cap) < rc[pos // self.sub_cap]
         return rk[live]
 
     def step(self, keys, row_base: int = 0, timing: bool = False, verify: bool = False):

@@ -785,6 +785,30 @@ int ccj_partition_by_owner_fixed(const int64_t *d_keys, uint64_t n, uint32_t par
   return CCJ_OK;
 }
 
+size_t ccj_partition_grouped_workspace_size(uint32_t parts) { return ccj::partition_grouped_workspace(parts); }
+
+uint64_t ccj_partition_grouped_sub_cap(uint64_t n, uint32_t parts, uint32_t chunk) {
+  return parts ? ccj::partition_grouped_sub_cap(n, parts, chunk) : 0;
+}
+
+int ccj_partition_by_owner_grouped(const int64_t *d_keys, uint64_t n, uint32_t parts, uint32_t row_base,
+                                   uint64_t sub_cap, int64_t *d_out_keys, uint32_t *d_out_rows,
+                                   uint64_t *d_out_counts, uint32_t *d_status, void *d_workspace,
+                                   size_t workspace_bytes, ccj_stream stream) {
+  if (parts == 0 || parts > ccj::kMaxParts || (parts & (parts - 1)))
+    return fail(CCJ_ERR_INVALID, "ccj_partition_by_owner_grouped: parts must be a power of two <= 64");
+  if (sub_cap == 0 || sub_cap >= (1ull << 32)) return fail(CCJ_ERR_INVALID, "ccj_partition_by_owner_grouped: bad sub_cap");
+  if (!d_out_counts || !d_status || !d_workspace || (n && (!d_keys || !d_out_keys || !d_out_rows)))
+    return fail(CCJ_ERR_INVALID, "ccj_partition_by_owner_grouped: missing buffer");
+  if (workspace_bytes < ccj::partition_grouped_workspace(parts))
+    return fail(CCJ_ERR_INVALID, "ccj_partition_by_owner_grouped: workspace too small");
+  if ((uint64_t)row_base + n > (1ull << 32)) return fail(CCJ_ERR_LIMIT, "ccj_partition_by_owner_grouped: rows exceed u32");
+  HIP_TRY(ccj::launch_partition_grouped(d_keys, n, parts, row_base, sub_cap, d_out_keys, d_out_rows, d_out_counts,
+                                        d_status, d_workspace, (hipStream_t)stream),
+          "grouped partition launch");
+  return CCJ_OK;
+}
+
 int ccj_segment_chunk_counts(const uint64_t *d_seg_counts, uint32_t n_segs, uint64_t seg_cap, uint32_t chunk,
                              uint32_t *d_out_counts, uint32_t *d_status, ccj_stream stream) {
   if (chunk == 0 || chunk > ccj::kMaxChunk || seg_cap % chunk)

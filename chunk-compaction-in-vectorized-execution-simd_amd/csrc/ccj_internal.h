@@ -162,7 +162,13 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
                                    uint64_t ovf_base, uint64_t ovf_cap, uint32_t *cursors, int64_t *out_keys,
                                    uint32_t *out_rows, uint32_t *status, hipStream_t s,
                                    const uint32_t *counts = nullptr, uint32_t chunk = 0, uint2 *runs = nullptr,
-                                   uint32_t *ovf_runs = nullptr);
+                                   uint32_t *ovf_runs = nullptr, uint32_t row_base = 0, uint32_t shift = ~0u,
+                                   uint32_t wgs = 0);
+size_t partition_grouped_workspace(uint32_t parts);
+uint64_t partition_grouped_sub_cap(uint64_t n, uint32_t parts, uint32_t chunk);
+hipError_t launch_partition_grouped(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t row_base,
+                                    uint64_t sub_cap, int64_t *out_keys, uint32_t *out_rows, uint64_t *out_counts,
+                                    uint32_t *status, void *ws, hipStream_t s);
 uint32_t slot_split_tile_keys(uint32_t parts);
 hipError_t launch_partition_fixed(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t row_base, uint64_t seg_cap,
                                   int64_t *out_keys, uint32_t *out_rows, uint64_t *out_counts, uint32_t *status,

@@ -240,6 +240,51 @@ hipError_t launch_partition_fixed(const int64_t *keys, uint64_t n, uint32_t part
 }
 
 namespace {
+// cursors[g * parts + d] (u32, group-major) -> counts[d * 8 + g] (u64, destination-major)
+__global__ void grouped_counts(const uint32_t *cur, uint32_t parts, uint64_t *out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < parts * 8) out[i] = cur[(i % 8) * parts + i / 8];
+}
+}  // namespace
+
+size_t partition_grouped_workspace(uint32_t parts) { return ((size_t)parts * 8 + 1) * 4; }
+
+uint64_t partition_grouped_sub_cap(uint64_t n, uint32_t parts, uint32_t chunk) {
+  // tile group g takes tiles [g * n_tiles / 8, (g + 1) * n_tiles / 8): at most ceil(n_tiles / 8)
+  const uint64_t tile = slot_split_tile_keys(parts), n_tiles = (n + tile - 1) / tile;
+  const uint64_t g_rows = std::min<uint64_t>(n, (n_tiles + 7) / 8 * tile);
+  const double m = (double)g_rows / parts;
+  const uint64_t c = (uint64_t)(m + 8.0 * std::sqrt(m) + chunk);
+  return chunk ? (c + chunk - 1) / chunk * chunk : c;
+}
+
+hipError_t launch_partition_grouped(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t row_base,
+                                    uint64_t sub_cap, int64_t *out_keys, uint32_t *out_rows, uint64_t *out_counts,
+                                    uint32_t *status, void *ws, hipStream_t s) {
+  // the slot split's one-pass kernel with partition = the owner (top log2(parts) hash bits) and no
+  // overflow area: a sub-segment that overflows drops rows and raises CCJ_FLAG_PART_OVERFLOW
+  SlotPlan pl{};
+  pl.lo_bits = log2u(parts);
+  pl.hi_bits = 0;
+  const uint32_t shift = parts > 1 ? 64u - pl.lo_bits : 0u;
+  uint32_t *cur = (uint32_t *)ws;
+  // Half the CUs: the multi-GPU step runs this beside the previous batch's all-to-all and the
+  // local probe, and a persistent one-workgroup-per-CU grid would hold every CU (its LDS).
+  static const uint32_t half = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return (uint32_t)(n >= 16 ? n / 16 * 8 : 8);
+  }();
+  const uint32_t wgs = (uint32_t)ccj_tune_int("CCJ_OWNER_WGS", (int)half);
+  hipError_t e = launch_slot_split_fixed(keys, n, pl, sub_cap, 0, 0, cur, out_keys, out_rows, status, s, nullptr, 0,
+                                         nullptr, nullptr, row_base, shift, wgs);
+  if (e) return e;
+  hipLaunchKernelGGL(grouped_counts, dim3((parts * 8 + 255) / 256), dim3(256), 0, s, cur, parts, out_counts);
+  return hipGetLastError();
+}
+
+namespace {
 // Chunk counts of fixed-capacity segments: segment g holds counts[g] live rows at the front of its
 // seg_cap slots; chunk j of segment g is rows [j*chunk, (j+1)*chunk) of it.
 __global__ void seg_chunk_counts(const uint64_t *counts, uint32_t n_segs, uint64_t seg_cap, uint32_t chunk,
@@ -307,7 +352,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
                                                                  uint64_t cap, uint64_t ovf_base, uint64_t ovf_cap,
                                                                  int64_t *out_k, uint32_t *out_r, uint32_t *status,
                                                                  uint32_t ablate, const uint32_t *counts, uint32_t chunk,
-                                                                 uint2 *runs, uint32_t *ovf_runs) {
+                                                                 uint2 *runs, uint32_t *ovf_runs, uint32_t row_base) {
   constexpr uint32_t kTileKeys = (uint32_t)THREADS * PER;
   static_assert(MAXP <= THREADS, "one partition per thread in the scan");
   __shared__ int64_t s_k[kTileKeys];
@@ -327,29 +372,48 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
   uint64_t tile = g * n_tiles / 8 + (blockIdx.x >> 3);
   int64_t kk[PER];
   uint32_t live = 0;  // bit it: row it of this thread is in the column (counts: within its chunk's count)
+  // COUNTS (fixed-capacity input segments: chunk c's first counts[c] rows are live): the counts of
+  // a tile's chunks travel through LDS (thread j loads chunk c0 + j's beside the keys), so every key
+  // load is unconditional and in flight at once — a per-row counts load ahead of a conditional key
+  // load made each row a dependent round trip
+  __shared__ uint32_t s_ccnt[COUNTS ? THREADS : 1];
+  uint32_t cpre = 0;
+  auto tile_rows = [&](uint64_t t) { return (uint32_t)(n - t * kTileKeys < kTileKeys ? n - t * kTileKeys : kTileKeys); };
   auto load = [&](uint64_t t) {
     const uint64_t t0 = t * kTileKeys;
-    const uint32_t tn = (uint32_t)(n - t0 < kTileKeys ? n - t0 : kTileKeys);
+    const uint32_t tn = tile_rows(t);
     live = 0;
 #pragma unroll
     for (int it = 0; it < PER; ++it) {
       const uint32_t li = (uint32_t)it * THREADS + tid;
-      bool in = li < tn;
-      if (COUNTS && in) {  // fixed-capacity input segments: chunk c's first counts[c] rows are live
-        const uint32_t pos = (uint32_t)(t0 + li), c = pos / chunk;
-        in = pos - c * chunk < counts[c];
-      }
-      live |= (in ? 1u : 0u) << it;
+      const bool in = li < tn;
+      if (!COUNTS) live |= (in ? 1u : 0u) << it;
       if CCJ_ABLATED(ablate, 0x20u) kk[it] = (int64_t)((t0 + li) * 0x9E3779B97F4A7C15ull >> 20);  // timing only: no key reads
-      else kk[it] = in ? __builtin_nontemporal_load(keys + t0 + li) : 0;
+      else kk[it] = __builtin_nontemporal_load(keys + t0 + (in ? li : 0u));
+    }
+    if (COUNTS) {
+      const uint64_t c0 = t0 / chunk, nc = (t0 + tn - 1) / chunk - c0 + 1;
+      cpre = tid < nc ? counts[c0 + tid] : 0u;
     }
   };
   if (tile < tend) load(tile);
   bool dropped = false;
   for (; tile < tend; tile += bpg) {
     const uint64_t t0 = tile * kTileKeys;
+    if (COUNTS) s_ccnt[tid] = cpre;
     if (tid < MAXP) s_hist[tid] = 0;
     __syncthreads();
+    if (COUNTS) {
+      const uint32_t tn = tile_rows(tile);
+      const uint64_t c0 = t0 / chunk;
+      live = 0;
+#pragma unroll
+      for (int it = 0; it < PER; ++it) {
+        const uint32_t li = (uint32_t)it * THREADS + tid;
+        const uint64_t pos = t0 + li, c = pos / chunk;
+        live |= (li < tn && pos - c * chunk < s_ccnt[c - c0] ? 1u : 0u) << it;
+      }
+    }
     uint32_t dd[PER], rk[PER];
 #pragma unroll
     for (int it = 0; it < PER; ++it) {
@@ -413,7 +477,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
       if ((o < lim || o - lim < s_olim[d]) && !CCJ_ABLATED(ablate, 0x10u)) {  // (0x10: timing only, no stores)
         const uint64_t dest = o < lim ? s_dst[d] + o : ovf_base + s_ovf[d] + (o - lim);
         out_k[dest] = k;  // plain stores: the L2 merges neighbouring runs' partial lines
-        out_r[dest] = (uint32_t)(t0 + (si & 0xFFFFu));  // (non-temporal stores measured the same)
+        out_r[dest] = row_base + (uint32_t)(t0 + (si & 0xFFFFu));  // (non-temporal stores measured the same)
       }
     }
     __syncthreads();
@@ -432,7 +496,7 @@ uint64_t slot_seg_cap(uint64_t n, const SlotPlan &pl, uint32_t chunk) {
 }
 
 // keys per thread per tile: 11 (11264-key tiles, 149 KB of LDS with <= 512 partitions); 1024
-// partitions leave room for 10 (the tuning build sweeps 10-12 below that)
+// partitions leave room for 10 (the tuning build sweeps 10 / 11 below that)
 static int split_per(uint32_t parts) {
   const int per = ccj_tune_int("CCJ_SPLIT_PER", kSplitPer);
   return parts > kSplitParts / 2 && per > 10 ? 10 : per;
@@ -443,8 +507,12 @@ uint32_t slot_split_tile_keys(uint32_t parts) { return (uint32_t)kSplitThreads *
 hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPlan &pl, uint64_t cap,
                                    uint64_t ovf_base, uint64_t ovf_cap, uint32_t *cursors, int64_t *out_keys,
                                    uint32_t *out_rows, uint32_t *status, hipStream_t s, const uint32_t *counts,
-                                   uint32_t chunk, uint2 *runs, uint32_t *ovf_runs) {
+                                   uint32_t chunk, uint2 *runs, uint32_t *ovf_runs, uint32_t row_base,
+                                   uint32_t shift, uint32_t wgs) {
   const uint32_t parts = 1u << (pl.lo_bits + pl.hi_bits);
+  // counts: a tile's chunks (tile / chunk + 2 at most) fit one count per thread
+  if (counts && (chunk == 0 || slot_split_tile_keys(parts) / chunk + 2 > (uint32_t)kSplitThreads))
+    return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(cursors, 0, ((size_t)parts * 8 + 1) * 4, s);
   if (e || n == 0) return e;
   // One persistent 1024-thread workgroup per CU (<= 149 KB of LDS), a multiple of 8 (one tile group
@@ -459,20 +527,19 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
   const uint32_t ablate = (uint32_t)ccj_tune_int("CCJ_ABLATE", 0);  // timing-only (tuning build)
   const int per = split_per(parts);
   const uint32_t tile = slot_split_tile_keys(parts);
+  if (shift == ~0u) shift = pl.window_bits;  // the slot split: partition = home slot >> window bits
   const uint64_t n_tiles = (n + tile - 1) / tile;
+  const unsigned grid = wgs ? (wgs + 7) / 8 * 8 : cus;  // wgs: leave CUs to kernels of other streams
 #define CCJ_SPLIT_LAUNCH(C, MAXP, P)                                                                                \
-  hipLaunchKernelGGL((slot_split_fixed<C, kSplitThreads, MAXP, P>), dim3(cus), dim3(kSplitThreads), 0, s, keys, n,       \
-                     pl.window_bits, parts, n_tiles, cursors, cap, ovf_base, ovf_cap, out_keys, out_rows, status, ablate, \
-                     counts, chunk, runs, ovf_runs)
+  hipLaunchKernelGGL((slot_split_fixed<C, kSplitThreads, MAXP, P>), dim3(grid), dim3(kSplitThreads), 0, s, keys, n,      \
+                     shift, parts, n_tiles, cursors, cap, ovf_base, ovf_cap, out_keys, out_rows, status, ablate,         \
+                     counts, chunk, runs, ovf_runs, row_base)
   if (parts > kSplitParts / 2) {  // 1024 partitions: 10 keys per thread
     if (counts) CCJ_SPLIT_LAUNCH(true, kSplitParts, 10);
     else CCJ_SPLIT_LAUNCH(false, kSplitParts, 10);
   } else if (per == 10) {
     if (counts) CCJ_SPLIT_LAUNCH(true, kSplitParts / 2, 10);
     else CCJ_SPLIT_LAUNCH(false, kSplitParts / 2, 10);
-  } else if (per == 12) {
-    if (counts) CCJ_SPLIT_LAUNCH(true, kSplitParts / 2, 12);
-    else CCJ_SPLIT_LAUNCH(false, kSplitParts / 2, 12);
   } else {
     if (counts) CCJ_SPLIT_LAUNCH(true, kSplitParts / 2, kSplitPer);
     else CCJ_SPLIT_LAUNCH(false, kSplitParts / 2, kSplitPer);

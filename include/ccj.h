@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CCJ_ABI_VERSION 5
+#define CCJ_ABI_VERSION 6
 
 enum ccj_status {
   CCJ_OK = 0,
@@ -308,6 +308,21 @@ int ccj_partition_by_owner(const int64_t *d_keys, uint64_t n, uint32_t parts, ui
 int ccj_partition_by_owner_fixed(const int64_t *d_keys, uint64_t n, uint32_t parts, uint32_t row_base,
                                  uint64_t seg_cap, int64_t *d_out_keys, uint32_t *d_out_rows, uint64_t *d_out_counts,
                                  uint32_t *d_status, void *d_workspace, size_t workspace_bytes, ccj_stream stream);
+/* One-pass form of the fixed-capacity split (the slot split's kernel with the owner as its
+ * partition): destination d's region is CCJ_OWNER_GROUPS sub-segments of sub_cap slots,
+ * [(d*G + g)*sub_cap, ... + count_{d,g}), sub-segment g filled only by the workgroups of XCD g (so
+ * each is written from one L2); d_out_counts[d*G + g] gets the true counts.  Rows beyond a
+ * sub-segment's sub_cap are dropped and CCJ_FLAG_PART_OVERFLOW is OR-ed into *d_status.
+ * Workspace: ccj_partition_grouped_workspace_size(parts) bytes. */
+#define CCJ_OWNER_GROUPS 8
+size_t ccj_partition_grouped_workspace_size(uint32_t parts);
+/* A sub_cap that n uniformly hashed keys overflow with negligible probability: the largest tile
+ * group's rows / parts + 8 standard deviations + one chunk, a multiple of chunk. */
+uint64_t ccj_partition_grouped_sub_cap(uint64_t n, uint32_t parts, uint32_t chunk);
+int ccj_partition_by_owner_grouped(const int64_t *d_keys, uint64_t n, uint32_t parts, uint32_t row_base,
+                                   uint64_t sub_cap, int64_t *d_out_keys, uint32_t *d_out_rows,
+                                   uint64_t *d_out_counts, uint32_t *d_status, void *d_workspace,
+                                   size_t workspace_bytes, ccj_stream stream);
 /* Probe chunk counts for n_segs received fixed-capacity segments (seg_cap a multiple of chunk):
  * chunk j of segment g gets min(chunk, max(0, count_g - j*chunk)) live rows, so ccj_probe over the
  * whole receive buffer (counts = this, sel = NULL) skips the padding.  count_g > seg_cap raises

@@ -171,10 +171,11 @@ class HostOps:
     by the oracle).  `local_overflow` makes this rank's local probe raise the slot-split overflow
     flag (ccj.FLAG_PART_OVERFLOW), as the one-pass split does under skew."""
 
-    def __init__(self, local_overflow=False):
+    def __init__(self, local_overflow=False, subs=1):
         import ccj_dist
         self.base = ccj_dist.HostOpsBase()
         self.local_overflow = local_overflow
+        self.subs = subs  # sub-segments per destination (the device's grouped partition: 8)
         self.probes = 0
 
     def __getattr__(self, name):
@@ -187,18 +188,23 @@ class HostOps:
         self.table, self.cf = O.Table(O.LP, own), cf
         return len(own)
 
-    def fixed_partitioner(self, n, world, seg_cap):
+    def fixed_partitioner(self, n, world, sub_cap):
+        S = self.subs
+
         def run(keys, row_base, sk, sr, sc, status, stream):
             k = keys.numpy()
             owner = np_owner(k, world)
+            grp = (np.arange(len(k)) * S) // max(len(k), 1)  # sub-segment g: the g-th 1/S of the batch
             for d in range(world):
-                idx = np.nonzero(owner == d)[0]
-                sc[d] = len(idx)
-                keep = idx[:seg_cap]
-                sk[d * seg_cap:d * seg_cap + len(keep)] = torch.from_numpy(k[keep])
-                sr[d * seg_cap:d * seg_cap + len(keep)] = torch.from_numpy((row_base + keep).astype(np.int32))
-                if len(idx) > seg_cap:
-                    status |= 1  # CCJ_FLAG_CAP_OVERFLOW
+                for g in range(S):
+                    idx = np.nonzero((owner == d) & (grp == g))[0]
+                    seg = d * S + g
+                    sc[seg] = len(idx)
+                    keep = idx[:sub_cap]
+                    sk[seg * sub_cap:seg * sub_cap + len(keep)] = torch.from_numpy(k[keep])
+                    sr[seg * sub_cap:seg * sub_cap + len(keep)] = torch.from_numpy((row_base + keep).astype(np.int32))
+                    if len(idx) > sub_cap:
+                        status |= 8  # CCJ_FLAG_PART_OVERFLOW, as the device's grouped partition
         return run
 
     def segment_chunk_counts(self, seg_counts, seg_cap, chunk, out, status, stream):
@@ -274,8 +280,8 @@ def _sharded_worker(rank, world, port, cfg, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    n_build, cf, n_probe, rng, seed, chunk, batches, group, skew_rank, local_ovf_rank = cfg
-    ops = HostOps(local_overflow=(rank == local_ovf_rank))
+    n_build, cf, n_probe, rng, seed, chunk, batches, group, skew_rank, local_ovf_rank, subs = cfg
+    ops = HostOps(local_overflow=(rank == local_ovf_rank), subs=subs)
     sp = ccj_dist.ShardedProbe(n_build, cf, n_probe, chunk, world, rank, batches=batches, ops=ops, group=group)
     keys = O.uniform_keys(seed, rank * n_probe, (rank + 1) * n_probe, rng)
     if rank == skew_rank:  # one hot key: its owner's send segment overflows on this rank only
@@ -314,12 +320,14 @@ def _run_sharded(world, cfg, timeout=240):
     return got
 
 
-@pytest.mark.parametrize("world,batches,group", [(2, 3, 2), (2, 4, 8), (4, 5, 2)])
-def test_sharded_probe_protocol_gloo(world, batches, group):
+@pytest.mark.parametrize("world,batches,group,subs", [(2, 3, 2, 1), (2, 4, 8, 1), (4, 5, 2, 1), (2, 3, 2, 8),
+                                                       (4, 5, 2, 8)])
+def test_sharded_probe_protocol_gloo(world, batches, group, subs):
     """ShardedProbe.step end to end with gloo: batching, double-buffered send slots, receive-group
     slots (short last group included), group_row_map and the verify checksum; L1 + L2 equal the
-    exact answer over all ranks' streams and no rank falls back."""
-    cfg = (1 << 13, 2, 3 << 12, 3 << 12, 21, 256, batches, group, -1, -1)
+    exact answer over all ranks' streams and no rank falls back.  subs = 8: every destination's
+    region in 8 sub-segments, as the device's one-pass grouped owner partition writes it."""
+    cfg = (1 << 13, 2, 3 << 12, 3 << 12, 21, 256, batches, group, -1, -1, subs)
     got = _run_sharded(world, cfg)
     for rank, m, l2, wm, wl2, exact, nb, ng, probes in got:
         assert (m, l2) == (wm, wl2)
@@ -327,13 +335,16 @@ def test_sharded_probe_protocol_gloo(world, batches, group):
         assert nb == batches and ng == -(-batches // min(batches, group)) and probes == 2 * ng
 
 
-@pytest.mark.parametrize("world,skew_rank,local_ovf_rank", [(2, 0, -1), (2, -1, 1), (4, 2, -1)])
-def test_sharded_overflow_on_one_rank_all_fall_back(world, skew_rank, local_ovf_rank):
+@pytest.mark.parametrize("world,skew_rank,local_ovf_rank,subs", [(2, 0, -1, 1), (2, -1, 1, 1), (4, 2, -1, 1),
+                                                                  (2, 0, -1, 8)])
+def test_sharded_overflow_on_one_rank_all_fall_back(world, skew_rank, local_ovf_rank, subs):
     """An overflow seen by ONE rank only (a hot key overflowing its send segment, or the local
     probe's slot split overflowing) makes EVERY rank redo the step with the exact-size protocol:
     the status word is all-reduced before the branch, so no collective sequence diverges (a hang
     here is caught by the queue timeout).  Results stay exact."""
-    cfg = (1 << 13, 2, 3 << 12, 3 << 12, 22, 256, 3, 2, skew_rank, local_ovf_rank)
+    # subs = 8: one batch, so the hot key's rows (1/8 of the batch per sub-segment) exceed sub_cap
+    batches, group = (3, 2) if subs == 1 else (1, 1)
+    cfg = (1 << 13, 2, 3 << 12, 3 << 12, 22, 256, batches, group, skew_rank, local_ovf_rank, subs)
     got = _run_sharded(world, cfg)
     for rank, m, l2, wm, wl2, exact, nb, ng, probes in got:
         assert (m, l2) == (wm, wl2)

@@ -103,6 +103,57 @@ def test_partition_fixed_overflow_flags_and_stays_in_bounds():
         assert (np_owner(kk[d * cap:(d + 1) * cap], parts) == d).all()
 
 
+@pytest.mark.parametrize("parts,n,base", [(1, 1000, 0), (2, 100000, 7), (8, 1234567, 1 << 20), (64, 500000, 3)])
+def test_partition_grouped_segments(parts, n, base):
+    """ccj_partition_by_owner_grouped (the one-pass split with the owner as partition): the 8
+    sub-segments of destination d hold exactly the owner-d (key, base + row) pairs between them (in
+    any order), their counts are the true counts, and nothing past a count is written."""
+    G = ccj.OWNER_GROUPS
+    keys = O.uniform_keys(parts + 13, 0, n, 1 << 40)
+    cap = ccj.grouped_sub_cap(n, parts, 256)
+    fp = ccj.GroupedOwnerPartitioner(n, parts, cap)
+    ok = torch.full((parts * G * cap,), -7, dtype=torch.int64, device="cuda")
+    orow = torch.zeros(parts * G * cap, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(parts * G, dtype=torch.int64, device="cuda")
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    fp(torch.from_numpy(keys).cuda(), base, ok, orow, cnt, st)
+    torch.cuda.synchronize()
+    owner = np_owner(keys, parts)
+    c = cnt.cpu().numpy().reshape(parts, G)
+    assert int(st.item()) == 0
+    assert np.array_equal(c.sum(axis=1), np.bincount(owner, minlength=parts))
+    k, r = ok.cpu().numpy(), orow.cpu().numpy()
+    for d in range(parts):
+        rows, ks = [], []
+        for g in range(G):
+            lo = (d * G + g) * cap
+            rows.append(r[lo:lo + c[d, g]].astype(np.int64) - base)
+            ks.append(k[lo:lo + c[d, g]])
+            assert (k[lo + c[d, g]:lo + cap] == -7).all()  # padding untouched
+        rows, ks = np.concatenate(rows), np.concatenate(ks)
+        assert np.array_equal(np.sort(rows), np.nonzero(owner == d)[0])  # every owner-d row exactly once
+        assert np.array_equal(ks, keys[rows])  # each with its own key
+
+
+def test_partition_grouped_overflow_flags_and_stays_in_bounds():
+    n, parts, cap = 300000, 4, 1024  # far too small: most rows dropped
+    G = ccj.OWNER_GROUPS
+    keys = O.uniform_keys(1, 0, n, 1 << 40)
+    fp = ccj.GroupedOwnerPartitioner(n, parts, cap)
+    ok = torch.full((parts * G * cap + 64,), -7, dtype=torch.int64, device="cuda")
+    orow = torch.zeros(parts * G * cap + 64, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(parts * G, dtype=torch.int64, device="cuda")
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    fp(torch.from_numpy(keys).cuda(), 0, ok, orow, cnt, st)
+    torch.cuda.synchronize()
+    assert int(st.item()) & ccj.FLAG_PART_OVERFLOW
+    assert (ok[parts * G * cap:].cpu().numpy() == -7).all()
+    kk = ok[:parts * G * cap].cpu().numpy()
+    for d in range(parts):  # what was kept of destination d is owner-d keys only
+        seg = kk[d * G * cap:(d + 1) * G * cap]
+        assert (np_owner(seg[seg != -7], parts) == d).all()
+
+
 def test_segment_chunk_counts():
     cap, chunk = 4096, 1024
     cnt = torch.tensor([0, 1, 1024, 1025, 4096, 5000], dtype=torch.int64, device="cuda")
@@ -144,3 +195,23 @@ def test_sharded_probe_pipelined_one_rank(pg1, batches):
     sp._resize(2048)
     assert sp.step(keys, 0, verify=True) == want
     assert sp.last_exact
+
+
+def test_bench_sharded_line():
+    """bench.py's N > 1 step (bench_multi) end to end on one GPU (--sharded: a one-rank RCCL group),
+    at a small size: the JSON line of the driver's contract, L1 + L2 exact."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from test_dist_cpu import free_port
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
+    p = subprocess.run([sys.executable, "bench.py", "--sharded", "--steps", "2", "--warmup", "1", "--no-cpu",
+                        "--n-build-per-gpu", str(1 << 22), "--n-probe", str(1 << 24), "--batches", "4"],
+                       cwd=root, capture_output=True, text=True, timeout=600, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 1 and line["scaling"] == "weak" and line["value"] > 0
+    assert line["parity"]["l1_ok"] and line["parity"]["l2_ok"], line["parity"]
+    assert 0 < line["roofline"]["frac"] < 1
