@@ -485,6 +485,173 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
   if (dropped && status) atomicOr(status, CCJ_FLAG_PART_OVERFLOW);
 }
 
+// A uniform value the compiler cannot fold (keeps the prologue's sink stores below real stores).
+__device__ __forceinline__ uint32_t opaque_u32(uint32_t x) {
+  asm volatile("" : "+s"(x));
+  return x;
+}
+// A lane value the compiler must recompute from here on (rematerialises addresses derived from it).
+__device__ __forceinline__ uint32_t opaque_v32(uint32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+// slot_split_pipe: slot_split_fixed's tile work software-pipelined so that a tile's stores drain
+// while the next tile is ranked.  Per iteration (tile t, the previous tile's image in LDS):
+//   load keys of t + 1 | rank t (LDS atomics) | barrier | scan t + reservation atomics t |
+//   store the previous tile's image | barrier | t's run table | barrier | t's image
+// The keys of t + 1 and the reservation atomics are issued BEFORE the stores, so neither wait
+// (vmcnt counts in issue order) has to drain the stores; every load and store is
+// unconditional (a clamped tile, a per-XCD sink position for inactive lanes), so the waits the
+// compiler derives are the same on every path (a prologue issues the sink stores of "tile -1").
+template <bool COUNTS, int THREADS, int MAXP, int PER>
+__global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, uint64_t n, uint32_t shift,
+                                                                uint32_t parts, uint64_t n_tiles, uint32_t *cur,
+                                                                uint64_t cap, uint64_t ovf_base, uint64_t ovf_cap,
+                                                                int64_t *out_k, uint32_t *out_r, uint32_t *status,
+                                                                const uint32_t *counts, uint32_t chunk, uint2 *runs,
+                                                                uint32_t *ovf_runs, uint32_t row_base, uint64_t sink) {
+  constexpr uint32_t kTileKeys = (uint32_t)THREADS * PER;
+  static_assert(MAXP <= THREADS, "one partition per thread in the scan");
+  __shared__ int64_t s_k[kTileKeys];
+  __shared__ uint32_t s_i[kTileKeys];  // tile-local row | partition << 16
+  __shared__ uint32_t s_hist[MAXP], s_loc[MAXP];
+  // per partition, for the stores: {dest - image index (u64), segment end, overflow end} (image
+  // indices) and the overflow area's dest - image index: two LDS reads per stored key
+  __shared__ uint4 s_rec[MAXP];
+  __shared__ uint64_t s_oadj[MAXP];
+  __shared__ uint32_t s_wsum[THREADS / 64], s_tot;
+  __shared__ uint32_t s_ccnt[COUNTS ? THREADS : 1];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t g = blockIdx.x & 7u, bpg = gridDim.x >> 3;
+  const uint32_t mask = parts - 1;
+  const uint64_t tend = (g + 1) * n_tiles / 8;
+  uint64_t tile = g * n_tiles / 8 + (blockIdx.x >> 3);
+  if (tile >= tend) return;
+  const uint64_t sink_pos = sink + g * 8;
+  if (tid < MAXP) s_hist[tid] = 0;
+  auto tile_rows = [&](uint64_t t) { return (uint32_t)(n - t * kTileKeys < kTileKeys ? n - t * kTileKeys : kTileKeys); };
+  auto load = [&](uint64_t t, int64_t(&kk)[PER], uint32_t &cp) {
+    const uint64_t tt = t < tend ? t : tend - 1;  // the last prefetch re-reads a valid tile
+    const uint64_t t0 = tt * kTileKeys;
+    const uint32_t tn = tile_rows(tt);
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      const uint32_t li = (uint32_t)it * THREADS + tid;
+      kk[it] = __builtin_nontemporal_load(keys + t0 + (li < tn ? li : 0u));
+    }
+    if (COUNTS) {
+      const uint64_t c0 = t0 / chunk, nc = (t0 + tn - 1) / chunk - c0 + 1;
+      cp = counts[c0 + (tid < nc ? tid : 0u)];  // masked where used
+    }
+  };
+  uint32_t have_prev = opaque_u32(0u), p_tl = 0;
+  uint64_t p_t0 = 0;
+  auto stores = [&]() {
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      const uint32_t q = (uint32_t)it * THREADS + tid;
+      const int64_t k = s_k[q];
+      const uint32_t si = s_i[q], d = (si >> 16) & (uint32_t)(MAXP - 1);
+      const uint4 rc = s_rec[d];
+      const uint64_t oadj = s_oadj[d];
+      const bool act = have_prev && q < p_tl && q < rc.w;
+      const uint64_t dest = !act ? sink_pos : q < rc.z ? (rc.x | (uint64_t)rc.y << 32) + q : oadj + q;
+      out_k[dest] = k;
+      out_r[dest] = row_base + (uint32_t)(p_t0 + (si & 0xFFFFu));
+      __builtin_amdgcn_sched_barrier(0);  // keep the LDS reads of later entries below (registers)
+    }
+  };
+  bool dropped = false;
+  auto step = [&](uint64_t t, int64_t(&kc)[PER], uint32_t cc, int64_t(&kn)[PER], uint32_t &cn) {
+    load(t + bpg, kn, cn);  // kn held the previous tile's keys, already in its image: a whole step of latency
+    const uint64_t t0 = t * kTileKeys;
+    const uint32_t tn = tile_rows(t);
+    uint32_t live = 0;
+    if (COUNTS) {
+      const uint64_t c0 = t0 / chunk, nc = (t0 + tn - 1) / chunk - c0 + 1;
+      s_ccnt[tid] = tid < nc ? cc : 0u;
+      __syncthreads();
+#pragma unroll
+      for (int it = 0; it < PER; ++it) {
+        const uint32_t li = (uint32_t)it * THREADS + tid;
+        const uint64_t pos = t0 + li, c = pos / chunk;
+        live |= (li < tn && pos - c * chunk < s_ccnt[c - c0] ? 1u : 0u) << it;
+      }
+    } else {
+#pragma unroll
+      for (int it = 0; it < PER; ++it) live |= ((uint32_t)it * THREADS + tid < tn ? 1u : 0u) << it;
+    }
+    uint32_t dr[PER];  // partition | rank in it << 10 (one register per key: no spills at 11 keys)
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      const uint32_t d = (uint32_t)(murmurhash64((uint64_t)kc[it]) >> shift) & mask;
+      dr[it] = d | ((live >> it) & 1u ? atomicAdd(&s_hist[d], 1u) : 0u) << 10;
+    }
+    __syncthreads();
+    const uint32_t h = tid < parts ? s_hist[tid] : 0u;
+    if (tid < MAXP) s_hist[tid] = 0;  // for the next tile (ranked after two more barriers)
+    const uint32_t incl = wave_incl_scan(h);
+    if (lane == 63) s_wsum[wave] = incl;
+    uint32_t r = 0;
+    if (h) r = atomicAdd(&cur[(uint64_t)g * parts + opaque_v32(tid)], h);  // awaited after the stores are issued
+    stores();
+    __syncthreads();  // the previous image is read; s_wsum is complete
+    uint32_t wpre = 0;
+    for (uint32_t w = 0; w < wave; ++w) wpre += s_wsum[w];
+    const uint32_t ptid = opaque_v32(tid);  // recomputed addresses instead of registers held all loop
+    if (ptid < parts) {
+      const uint32_t loc = wpre + incl - h;
+      s_loc[tid] = loc;
+      const uint64_t seg = (uint64_t)ptid * 8 + g;
+      const uint32_t lim = r >= cap ? 0u : (uint32_t)(cap - r < h ? cap - r : h);
+      uint32_t olim = 0, r2 = 0;
+      if (lim < h) {  // the rest of the run goes to the shared overflow area (key skew)
+        const uint32_t extra = h - lim;
+        r2 = atomicAdd(&cur[(uint64_t)parts * 8], extra);
+        olim = r2 >= ovf_cap ? 0u : (uint32_t)(ovf_cap - r2 < extra ? ovf_cap - r2 : extra);
+        dropped |= olim < extra;
+      }
+      const uint64_t dadj = seg * cap + r - loc;  // mod 2^64: + the image index gives the dest
+      s_rec[tid] = make_uint4((uint32_t)dadj, (uint32_t)(dadj >> 32), loc + lim, loc + lim + olim);
+      s_oadj[tid] = ovf_base + r2 - (loc + lim);
+      if (runs) {
+        runs[t * parts + tid] = make_uint2((uint32_t)(seg * cap + r), lim | olim << 16);
+        if (olim) ovf_runs[t * parts + tid] = (uint32_t)(ovf_base + r2);
+      }
+    }
+    if (tid == THREADS - 1) s_tot = wpre + incl;
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      if ((live >> it) & 1u) {
+        const uint32_t d = dr[it] & 1023u;
+        const uint32_t pos = s_loc[d] + (dr[it] >> 10);
+        s_k[pos] = kc[it];
+        s_i[pos] = ((uint32_t)it * THREADS + tid) | d << 16;
+      }
+    }
+    p_tl = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tot);
+    p_t0 = t0;
+    have_prev = 1u;
+  };
+  int64_t kA[PER], kB[PER];
+  uint32_t cA = 0, cB = 0;
+  load(tile, kA, cA);
+  stores();  // "tile -1": all to the sink, so the loop is entered with the waits it has inside
+  for (;;) {
+    step(tile, kA, cA, kB, cB);
+    tile += bpg;
+    if (tile >= tend) break;
+    step(tile, kB, cB, kA, cA);
+    tile += bpg;
+    if (tile >= tend) break;
+  }
+  __syncthreads();
+  stores();
+  if (dropped && status) atomicOr(status, CCJ_FLAG_PART_OVERFLOW);
+}
+
 }  // namespace
 
 uint64_t slot_seg_cap(uint64_t n, const SlotPlan &pl, uint32_t chunk) {
@@ -530,7 +697,27 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
   if (shift == ~0u) shift = pl.window_bits;  // the slot split: partition = home slot >> window bits
   const uint64_t n_tiles = (n + tile - 1) / tile;
   const unsigned grid = wgs ? (wgs + 7) / 8 * 8 : cus;  // wgs: leave CUs to kernels of other streams
-#define CCJ_SPLIT_LAUNCH(C, MAXP, P)                                                                                \
+  // the pipelined form needs 64 positions of the overflow area as its sink (8 per XCD group)
+  if (ovf_cap >= 128 && ccj_tune_int("CCJ_SPLIT_PIPE", 1)) {
+    const uint64_t oc = ovf_cap - 64, sink = ovf_base + oc;
+#define CCJ_PIPE_LAUNCH(C, MAXP, P)                                                                                   \
+  hipLaunchKernelGGL((slot_split_pipe<C, kSplitThreads, MAXP, P>), dim3(grid), dim3(kSplitThreads), 0, s, keys, n,      \
+                     shift, parts, n_tiles, cursors, cap, ovf_base, oc, out_keys, out_rows, status, counts, chunk, runs, \
+                     ovf_runs, row_base, sink)
+    if (parts > kSplitParts / 2) {
+      if (counts) CCJ_PIPE_LAUNCH(true, kSplitParts, 10);
+      else CCJ_PIPE_LAUNCH(false, kSplitParts, 10);
+    } else if (per == 10) {
+      if (counts) CCJ_PIPE_LAUNCH(true, kSplitParts / 2, 10);
+      else CCJ_PIPE_LAUNCH(false, kSplitParts / 2, 10);
+    } else {
+      if (counts) CCJ_PIPE_LAUNCH(true, kSplitParts / 2, kSplitPer);
+      else CCJ_PIPE_LAUNCH(false, kSplitParts / 2, kSplitPer);
+    }
+#undef CCJ_PIPE_LAUNCH
+    return hipGetLastError();
+  }
+#define CCJ_SPLIT_LAUNCH(C, MAXP, P)                                                                              \
   hipLaunchKernelGGL((slot_split_fixed<C, kSplitThreads, MAXP, P>), dim3(grid), dim3(kSplitThreads), 0, s, keys, n,      \
                      shift, parts, n_tiles, cursors, cap, ovf_base, ovf_cap, out_keys, out_rows, status, ablate,         \
                      counts, chunk, runs, ovf_runs, row_base)
