@@ -78,6 +78,9 @@ struct ProbeParams {
   uint64_t swz_chunks;   // chunks dealt to XCDs in contiguous ranges (0: all); the overflow area's
                          // chunks follow in plain order so they do not unbalance the XCDs' shares
   uint32_t xcd_swizzle;  // 1: consecutive chunks go to the same XCD (L2 reuse of partitioned input)
+  // probe_walk's emit: kEmitWave = per-wave placement; else the chunk's output staged in LDS in row
+  // order and written with 16-byte buffer stores of this cache policy (aux bits: 2 nt, 16 sc1)
+  uint32_t emit_pol;
   uint32_t ablate;       // timing-only ablations (tuning build only: CCJ_ABLATE)
   unsigned long long *stats;  // tuning build only (CCJ_STATS): per-phase cycle sums of the walk
   // Ordered probe (ccj_probe_ordered): round words per position (walk) / per row (emit input)
@@ -85,6 +88,7 @@ struct ProbeParams {
   const uint32_t *in_w;
 };
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;
+constexpr uint32_t kEmitWave = 0xFFFFFFFFu;
 
 // Launchers (ccj_kernels.hip).  Return hipError_t of the launch.
 hipError_t launch_probe(int kind, const ProbeParams &p, hipStream_t s);
@@ -163,7 +167,10 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
                                    uint32_t *out_rows, uint32_t *status, hipStream_t s,
                                    const uint32_t *counts = nullptr, uint32_t chunk = 0, uint2 *runs = nullptr,
                                    uint32_t *ovf_runs = nullptr, uint32_t row_base = 0, uint32_t shift = ~0u,
-                                   uint32_t wgs = 0);
+                                   uint32_t wgs = 0, void *sink = nullptr);
+// Bytes of device memory the split writes its inactive lanes' stores to when the overflow area
+// cannot hold them (launch_slot_split_fixed's `sink`; 8 XCD groups x 8 positions of key + row).
+constexpr size_t kSplitSinkBytes = 8 * 8 * 16;
 size_t partition_grouped_workspace(uint32_t parts);
 uint64_t partition_grouped_sub_cap(uint64_t n, uint32_t parts, uint32_t chunk);
 hipError_t launch_partition_grouped(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t row_base,

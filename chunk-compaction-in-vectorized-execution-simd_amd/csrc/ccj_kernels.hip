@@ -1367,6 +1367,88 @@ __device__ __forceinline__ void walk_finish(const ProbeParams &p, SM &sm, uint64
   if (p.status && overflow) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
 }
 
+// Workgroup emit (p.emit_pol != kEmitWave; needs HOME's u32 counts): when no row of the chunk has
+// more than one match and the chunk fits its output, the chunk's matches are compacted in LDS in
+// row order (keys in place in sm.key, row positions in sm.hc; every entry moves down, so one
+// barrier between reading and writing suffices) and written from c * cap with 16-byte buffer
+// stores of cache policy p.emit_pol: 4 sel or 2 payload entries per lane instead of one.
+// Returns false (nothing written) when the per-wave emit must run instead.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// The compacted chunk (sel in sm.hc, payload in sm.key, tot entries) as 16-byte stores.  A last
+// partial group writes past the count inside the chunk's own cap region (cap is a multiple of 4),
+// which holds no data of the chunk's consumers.
+template <int AUX, uint32_t kThreads>
+__device__ __forceinline__ void emit_wg_stores(const ProbeParams &p, WalkShared<true> &sm, uint64_t obase, uint32_t tot) {
+  const uint32_t tid = threadIdx.x;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(p.out_sel + obase, (short)0, (int)(p.cap * 4), 0x00020000);
+  for (uint32_t q = tid; q * 4 < tot; q += kThreads) {
+    const u32x4 v = *reinterpret_cast<const u32x4 *>(&sm.hc[4 * q]);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)(16 * q), 0, AUX);
+  }
+  if (p.out_payload) {
+    const auto rp = __builtin_amdgcn_make_buffer_rsrc(p.out_payload + obase, (short)0, (int)(p.cap * 8), 0x00020000);
+    for (uint32_t q = tid; q * 2 < tot; q += kThreads) {
+      const u32x4 v = *reinterpret_cast<const u32x4 *>(&sm.key[2 * q]);
+      __builtin_amdgcn_raw_buffer_store_b128(v, rp, (int)(16 * q), 0, AUX);
+    }
+  }
+}
+template <uint32_t kWaveRows, int NW>
+__device__ __forceinline__ bool walk_emit_wg(const ProbeParams &p, WalkShared<true> &sm, uint64_t c, uint32_t w0,
+                                             uint32_t wend, uint32_t lane, uint32_t wave, uint32_t *s_wtot) {
+  constexpr int kJ = (int)(kWaveRows / kWave);
+  uint32_t lsum = 0, multi = 0;
+  uint32_t n[kJ];
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) {
+    const uint32_t i = w0 + (uint32_t)j * kWave + lane;
+    n[j] = i < wend ? sm.hc[i] : 0u;
+    lsum += n[j];
+    multi |= n[j] > 1u ? 1u : 0u;
+  }
+  const uint32_t wtot = (uint32_t)__shfl((int)wave_incl_scan(lsum), kWave - 1);
+  const uint32_t wmulti = wave_or(multi);
+  if (lane == 0) s_wtot[wave] = wtot | (wmulti ? 0x80000000u : 0u);
+  __syncthreads();
+  uint32_t base = 0, tot = 0, any_multi = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    const uint32_t x = s_wtot[w];
+    any_multi |= x >> 31;
+    base += (uint32_t)w < wave ? (x & 0x7FFFFFFFu) : 0u;
+    tot += x & 0x7FFFFFFFu;
+  }
+  if (any_multi || tot > p.cap) return false;
+  int64_t k[kJ];
+  uint32_t t[kJ];
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) {
+    const uint32_t i = w0 + (uint32_t)j * kWave + lane;
+    const uint64_t bm = __ballot(n[j] != 0u);
+    t[j] = base + lane_prefix(bm);
+    base += (uint32_t)__popcll(bm);
+    k[j] = sm.key[i & (kMaxChunk - 1)];
+  }
+  __syncthreads();  // every key read before any entry moves down
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) {
+    if (n[j]) {
+      sm.key[t[j]] = k[j];
+      sm.hc[t[j]] = w0 + (uint32_t)j * kWave + lane;
+    }
+  }
+  __syncthreads();
+  const uint64_t obase = c * p.cap;
+  switch (p.emit_pol) {  // the buffer stores' cache bits are an immediate
+    case 2: emit_wg_stores<2, kWave * NW>(p, sm, obase, tot); break;
+    case 16: emit_wg_stores<16, kWave * NW>(p, sm, obase, tot); break;
+    case 18: emit_wg_stores<18, kWave * NW>(p, sm, obase, tot); break;
+    default: emit_wg_stores<0, kWave * NW>(p, sm, obase, tot); break;
+  }
+  if (threadIdx.x == 0) sm.total = tot;
+  return true;
+}
+
 // MM (the ordered probe, ccj_probe_ordered): instead of counts, each row leaves its Next-round
 // word W = mm | L << 26 (bit r of mm: the row matches in round r; L: occupied slots walked = its
 // rounds, the reference's Next calls for it; L > 26: bit 31 | L, the chunk re-walks round by
@@ -1492,6 +1574,16 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk(ProbeParams p) {
       if (i < wend) __builtin_nontemporal_store((uint32_t)sm.hc[i], p.out_w + base + i);
     }
     return;
+  }
+  if constexpr (HOME) {
+    if (p.emit_pol != kEmitWave) {
+      __shared__ uint32_t s_wtot[NW];
+      wave_lds_sync();
+      if (walk_emit_wg<kWaveRows, NW>(p, sm, c, w0, wend, lane, wave, s_wtot)) {
+        walk_finish(p, sm, c, lane, lane_rounds, 0u, t0, t1, t2, steps);
+        return;
+      }
+    }
   }
   const uint32_t overflow = walk_emit<kWaveRows>(p, sm, c, w0, wend, lane);
   walk_finish(p, sm, c, lane, lane_rounds, overflow, t0, t1, t2, steps);

@@ -247,7 +247,9 @@ __global__ void grouped_counts(const uint32_t *cur, uint32_t parts, uint64_t *ou
 }
 }  // namespace
 
-size_t partition_grouped_workspace(uint32_t parts) { return ((size_t)parts * 8 + 1) * 4; }
+// cursors, then the pipelined split's sink
+static size_t grouped_cursor_bytes(uint32_t parts) { return (((size_t)parts * 8 + 1) * 4 + 255) & ~(size_t)255; }
+size_t partition_grouped_workspace(uint32_t parts) { return grouped_cursor_bytes(parts) + kSplitSinkBytes; }
 
 uint64_t partition_grouped_sub_cap(uint64_t n, uint32_t parts, uint32_t chunk) {
   // tile group g takes tiles [g * n_tiles / 8, (g + 1) * n_tiles / 8): at most ceil(n_tiles / 8)
@@ -278,7 +280,8 @@ hipError_t launch_partition_grouped(const int64_t *keys, uint64_t n, uint32_t pa
   }();
   const uint32_t wgs = (uint32_t)ccj_tune_int("CCJ_OWNER_WGS", (int)half);
   hipError_t e = launch_slot_split_fixed(keys, n, pl, sub_cap, 0, 0, cur, out_keys, out_rows, status, s, nullptr, 0,
-                                         nullptr, nullptr, row_base, shift, wgs);
+                                         nullptr, nullptr, row_base, shift, wgs,
+                                         (char *)ws + grouped_cursor_bytes(parts));
   if (e) return e;
   hipLaunchKernelGGL(grouped_counts, dim3((parts * 8 + 255) / 256), dim3(256), 0, s, cur, parts, out_counts);
   return hipGetLastError();
@@ -504,13 +507,15 @@ __device__ __forceinline__ uint32_t opaque_v32(uint32_t x) {
 // (vmcnt counts in issue order) has to drain the stores; every load and store is
 // unconditional (a clamped tile, a per-XCD sink position for inactive lanes), so the waits the
 // compiler derives are the same on every path (a prologue issues the sink stores of "tile -1").
+// The sink: 64 positions at the end of the overflow area, or caller memory (kSplitSinkBytes).
 template <bool COUNTS, int THREADS, int MAXP, int PER>
 __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, uint64_t n, uint32_t shift,
                                                                 uint32_t parts, uint64_t n_tiles, uint32_t *cur,
                                                                 uint64_t cap, uint64_t ovf_base, uint64_t ovf_cap,
                                                                 int64_t *out_k, uint32_t *out_r, uint32_t *status,
                                                                 const uint32_t *counts, uint32_t chunk, uint2 *runs,
-                                                                uint32_t *ovf_runs, uint32_t row_base, uint64_t sink) {
+                                                                uint32_t *ovf_runs, uint32_t row_base, int64_t *sink_k,
+                                                                uint32_t *sink_r) {
   constexpr uint32_t kTileKeys = (uint32_t)THREADS * PER;
   static_assert(MAXP <= THREADS, "one partition per thread in the scan");
   __shared__ int64_t s_k[kTileKeys];
@@ -528,7 +533,8 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
   const uint64_t tend = (g + 1) * n_tiles / 8;
   uint64_t tile = g * n_tiles / 8 + (blockIdx.x >> 3);
   if (tile >= tend) return;
-  const uint64_t sink_pos = sink + g * 8;
+  sink_k += g * 8;  // inactive lanes store here (8 positions per XCD group)
+  sink_r += g * 8;
   if (tid < MAXP) s_hist[tid] = 0;
   auto tile_rows = [&](uint64_t t) { return (uint32_t)(n - t * kTileKeys < kTileKeys ? n - t * kTileKeys : kTileKeys); };
   auto load = [&](uint64_t t, int64_t(&kk)[PER], uint32_t &cp) {
@@ -556,9 +562,9 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
       const uint4 rc = s_rec[d];
       const uint64_t oadj = s_oadj[d];
       const bool act = have_prev && q < p_tl && q < rc.w;
-      const uint64_t dest = !act ? sink_pos : q < rc.z ? (rc.x | (uint64_t)rc.y << 32) + q : oadj + q;
-      out_k[dest] = k;
-      out_r[dest] = row_base + (uint32_t)(p_t0 + (si & 0xFFFFu));
+      const uint64_t dest = q < rc.z ? (rc.x | (uint64_t)rc.y << 32) + q : oadj + q;
+      *(act ? out_k + dest : sink_k) = k;
+      *(act ? out_r + dest : sink_r) = row_base + (uint32_t)(p_t0 + (si & 0xFFFFu));
       __builtin_amdgcn_sched_barrier(0);  // keep the LDS reads of later entries below (registers)
     }
   };
@@ -675,7 +681,7 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
                                    uint64_t ovf_base, uint64_t ovf_cap, uint32_t *cursors, int64_t *out_keys,
                                    uint32_t *out_rows, uint32_t *status, hipStream_t s, const uint32_t *counts,
                                    uint32_t chunk, uint2 *runs, uint32_t *ovf_runs, uint32_t row_base,
-                                   uint32_t shift, uint32_t wgs) {
+                                   uint32_t shift, uint32_t wgs, void *sink) {
   const uint32_t parts = 1u << (pl.lo_bits + pl.hi_bits);
   // counts: a tile's chunks (tile / chunk + 2 at most) fit one count per thread
   if (counts && (chunk == 0 || slot_split_tile_keys(parts) / chunk + 2 > (uint32_t)kSplitThreads))
@@ -697,13 +703,16 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
   if (shift == ~0u) shift = pl.window_bits;  // the slot split: partition = home slot >> window bits
   const uint64_t n_tiles = (n + tile - 1) / tile;
   const unsigned grid = wgs ? (wgs + 7) / 8 * 8 : cus;  // wgs: leave CUs to kernels of other streams
-  // the pipelined form needs 64 positions of the overflow area as its sink (8 per XCD group)
-  if (ovf_cap >= 128 && ccj_tune_int("CCJ_SPLIT_PIPE", 1)) {
-    const uint64_t oc = ovf_cap - 64, sink = ovf_base + oc;
+  // the pipelined form needs a sink for its inactive lanes' stores: 64 positions of the overflow
+  // area (8 per XCD group), or the caller's kSplitSinkBytes
+  if ((ovf_cap >= 128 || sink) && ccj_tune_int("CCJ_SPLIT_PIPE", 1)) {
+    const uint64_t oc = sink ? ovf_cap : ovf_cap - 64;
+    int64_t *sink_k = sink ? (int64_t *)sink : out_keys + ovf_base + oc;
+    uint32_t *sink_r = sink ? (uint32_t *)((char *)sink + kSplitSinkBytes / 16 * 8) : out_rows + ovf_base + oc;
 #define CCJ_PIPE_LAUNCH(C, MAXP, P)                                                                                   \
   hipLaunchKernelGGL((slot_split_pipe<C, kSplitThreads, MAXP, P>), dim3(grid), dim3(kSplitThreads), 0, s, keys, n,      \
                      shift, parts, n_tiles, cursors, cap, ovf_base, oc, out_keys, out_rows, status, counts, chunk, runs, \
-                     ovf_runs, row_base, sink)
+                     ovf_runs, row_base, sink_k, sink_r)
     if (parts > kSplitParts / 2) {
       if (counts) CCJ_PIPE_LAUNCH(true, kSplitParts, 10);
       else CCJ_PIPE_LAUNCH(false, kSplitParts, 10);
