@@ -626,7 +626,7 @@ OrderedLayout ordered_layout(const ccj_table *t, uint64_t n_rows, uint32_t chunk
   O.L = part_layout(t, n_rows, chunk);
   if (O.L.pl.lo_bits == 0) return O;
   O.partitioned = true;
-  O.tile = ccj::slot_split_tile_keys(1u << (O.L.pl.lo_bits + O.L.pl.hi_bits));
+  O.tile = ccj::slot_split_tile_keys(1u << (O.L.pl.lo_bits + O.L.pl.hi_bits), true);
   O.n_tiles = (n_rows + O.tile - 1) / O.tile;
   size_t off = 0;
   auto take = [&](size_t bytes) {
@@ -693,12 +693,18 @@ int ccj_probe_ordered(const ccj_table *t, const ccj_probe_args *a, void *ws, siz
   q.n_chunks = L.positions / a->chunk + (L.positions % a->chunk ? 1 : 0);
   q.xcd_swizzle = 1;
   q.out_w = w_pos;
+  // distinct build keys: a row matches in at most one round, so 16-bit words carry it (halves the
+  // words' three HBM crossings: walk -> unsplit -> emit)
+  const uint32_t w16 = t->info.max_dup <= 1 && ccj_tune_int("CCJ_W16", 1) ? 1u : 0u;
+  q.w16 = w16;
   HIP_TRY(ccj::launch_ordered_walk(q, s), "ordered walk");
   // 3. the words back into row order, one split tile per workgroup
-  HIP_TRY(ccj::launch_unsplit_words(runs, ovf_runs, row_map, w_pos, w_row, a->n_rows, L.parts, O.tile, a->status, s),
+  HIP_TRY(ccj::launch_unsplit_words(runs, ovf_runs, row_map, w_pos, w_row, a->n_rows, L.parts, O.tile, a->status, s,
+                                    w16 != 0),
           "unsplit");
   // 4. per chunk: the reference's per-Next stream from its rows' words (probe_chunks' emit)
   p.in_w = w_row;
+  p.w16 = w16;
   p.xcd_swizzle = 0;
   HIP_TRY(ccj::launch_ordered_emit(p, s), "ordered emit");
   return CCJ_OK;

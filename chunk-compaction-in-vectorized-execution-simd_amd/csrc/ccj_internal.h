@@ -86,6 +86,9 @@ struct ProbeParams {
   // Ordered probe (ccj_probe_ordered): round words per position (walk) / per row (emit input)
   uint32_t *out_w;
   const uint32_t *in_w;
+  // 1: the round words are 16-bit, L << 7 | the row's match round (127: none) — tables whose keys
+  // are distinct (max_dup 1), where a row matches in at most one round
+  uint32_t w16;
 };
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 constexpr uint32_t kEmitWave = 0xFFFFFFFFu;
@@ -98,8 +101,8 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s);
 // workgroup; the reference-order emit of each chunk from its rows' words (p.in_w).
 hipError_t launch_ordered_walk(const ProbeParams &p, hipStream_t s);
 hipError_t launch_unsplit_words(const uint2 *runs, const uint32_t *ovf_runs, const uint32_t *row_map,
-                                const uint32_t *w_pos, uint32_t *w_row, uint64_t n, uint32_t parts, uint32_t tile,
-                                uint32_t *status, hipStream_t s);
+                                const void *w_pos, void *w_row, uint64_t n, uint32_t parts, uint32_t tile,
+                                uint32_t *status, hipStream_t s, bool w16);
 hipError_t launch_ordered_emit(const ProbeParams &p, hipStream_t s);
 // C5 payload columns of a finished probe: out_cols[q][slot] = payload row of pos[slot], column q.
 hipError_t launch_gather_payload(const ProbeParams &p, const uint32_t *pos, hipStream_t s);
@@ -161,7 +164,7 @@ uint64_t slot_seg_cap(uint64_t n, const SlotPlan &pl, uint32_t chunk);
 // cursors[parts * 8] = rows that went to the overflow area [ovf_base, ovf_base + ovf_cap).
 // counts: live rows per input chunk.  runs (optional; the ordered probe): per (tile, partition)
 // {segment position of the run, segment length | overflow-area length << 16}; ovf_runs: the
-// overflow-area position where that length is non-zero.  Tiles are slot_split_tile_keys(parts) keys.
+// overflow-area position where that length is non-zero.  Tiles are slot_split_tile_keys(parts, runs) keys.
 hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPlan &pl, uint64_t cap,
                                    uint64_t ovf_base, uint64_t ovf_cap, uint32_t *cursors, int64_t *out_keys,
                                    uint32_t *out_rows, uint32_t *status, hipStream_t s,
@@ -176,7 +179,7 @@ uint64_t partition_grouped_sub_cap(uint64_t n, uint32_t parts, uint32_t chunk);
 hipError_t launch_partition_grouped(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t row_base,
                                     uint64_t sub_cap, int64_t *out_keys, uint32_t *out_rows, uint64_t *out_counts,
                                     uint32_t *status, void *ws, hipStream_t s);
-uint32_t slot_split_tile_keys(uint32_t parts);
+uint32_t slot_split_tile_keys(uint32_t parts, bool runs = false);
 hipError_t launch_partition_fixed(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t row_base, uint64_t seg_cap,
                                   int64_t *out_keys, uint32_t *out_rows, uint64_t *out_counts, uint32_t *status,
                                   void *ws, hipStream_t s);

@@ -130,6 +130,22 @@ constexpr int kMaxFastRounds = 32;  // rounds recorded by the windowed path (bit
 // a row of more than 26 rounds is kMmLong | rounds.
 constexpr uint32_t kMmRounds = 26;
 constexpr uint32_t kMmLong = 0x80000000u;
+// 16-bit form (ProbeParams::w16, distinct build keys: at most one match round per row):
+// min(L, 511) << 7 | the match round (127: none).  A row of more than 26 rounds only needs its L
+// (its chunk re-walks), so its round field is 127.
+__device__ __forceinline__ uint16_t round_word16(uint32_t w) {
+  if (w & kMmLong) {
+    const uint32_t r = w & ~kMmLong;
+    return (uint16_t)((r < 511u ? r : 511u) << 7 | 127u);
+  }
+  const uint32_t mm = w & ((1u << kMmRounds) - 1u);
+  return (uint16_t)((w >> kMmRounds) << 7 | (mm ? (uint32_t)__builtin_ctz(mm) : 127u));
+}
+__device__ __forceinline__ uint32_t round_word32(uint16_t h) {
+  const uint32_t r = (uint32_t)h >> 7, m = h & 127u;
+  if (r > kMmRounds) return kMmLong | r;
+  return (m < 127u ? 1u << m : 0u) | r << kMmRounds;
+}
 constexpr int kWalkRows = 2;  // rows per lane walked concurrently (loads in flight)
 
 constexpr int kEmitRows = 4;    // row groups per lane whose sel loads are issued together in the emit
@@ -1571,7 +1587,10 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk(ProbeParams p) {
 #pragma unroll
     for (int j = 0; j < (int)(kWaveRows / kWave); ++j) {
       const uint32_t i = w0 + (uint32_t)j * kWave + lane;
-      if (i < wend) __builtin_nontemporal_store((uint32_t)sm.hc[i], p.out_w + base + i);
+      if (i < wend) {
+        if (p.w16) __builtin_nontemporal_store(round_word16((uint32_t)sm.hc[i]), (uint16_t *)p.out_w + base + i);
+        else __builtin_nontemporal_store((uint32_t)sm.hc[i], p.out_w + base + i);
+      }
     }
     return;
   }
@@ -1622,7 +1641,8 @@ __global__ __launch_bounds__(kBlock) void emit_ordered(ProbeParams p) {
     w[q] = 0;
     if (i < count) {
       key[q] = __builtin_nontemporal_load(p.keys + base + i);
-      w[q] = __builtin_nontemporal_load(p.in_w + base + i);
+      w[q] = p.w16 ? round_word32(__builtin_nontemporal_load((const uint16_t *)p.in_w + base + i))
+                   : __builtin_nontemporal_load(p.in_w + base + i);
     }
   }
   for (uint32_t q = tid; q < kMaxFastRounds * 32; q += kBlock) s_off[q] = 0u;
@@ -1745,18 +1765,19 @@ __global__ __launch_bounds__(kBlock) void emit_ordered(ProbeParams p) {
 constexpr int kUnsplitThreads = 1024;
 constexpr uint32_t kUnsplitMaxTile = 13u * kUnsplitThreads;  // the split's largest tile (13 keys per thread)
 
+template <typename W>
 __global__ __launch_bounds__(kUnsplitThreads) void unsplit_words(const uint2 *runs, const uint32_t *ovf_runs,
-                                                                 const uint32_t *row_map, const uint32_t *w_pos,
-                                                                 uint32_t *w_row, uint64_t n, uint32_t parts,
+                                                                 const uint32_t *row_map, const W *w_pos,
+                                                                 W *w_row, uint64_t n, uint32_t parts,
                                                                  uint32_t tile, uint32_t *status) {
-  __shared__ uint32_t s_img[kUnsplitMaxTile];
+  __shared__ W s_img[kUnsplitMaxTile];
   __shared__ uint32_t s_loc[kUnsplitThreads + 1];
   __shared__ uint2 s_run[kUnsplitThreads];
   __shared__ uint32_t s_wsum[kUnsplitThreads / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint64_t t = blockIdx.x, t0 = t * tile;
   const uint32_t tn = (uint32_t)(n - t0 < tile ? n - t0 : tile);
-  for (uint32_t i = tid; i < tn; i += kUnsplitThreads) s_img[i] = 0u;
+  for (uint32_t i = tid; i < tn; i += kUnsplitThreads) s_img[i] = 0;
   const uint2 r = tid < parts ? runs[t * parts + tid] : make_uint2(0u, 0u);
   const uint32_t len = (r.y & 0xFFFFu) + (r.y >> 16);
   uint32_t incl = wave_incl_scan(len);
@@ -1939,13 +1960,17 @@ hipError_t launch_ordered_walk(const ProbeParams &p, hipStream_t s) {
 }
 
 hipError_t launch_unsplit_words(const uint2 *runs, const uint32_t *ovf_runs, const uint32_t *row_map,
-                                const uint32_t *w_pos, uint32_t *w_row, uint64_t n, uint32_t parts, uint32_t tile,
-                                uint32_t *status, hipStream_t s) {
+                                const void *w_pos, void *w_row, uint64_t n, uint32_t parts, uint32_t tile,
+                                uint32_t *status, hipStream_t s, bool w16) {
   if (n == 0) return hipSuccess;
   if (tile > kUnsplitMaxTile || parts > (uint32_t)kUnsplitThreads) return hipErrorInvalidValue;
   const uint64_t n_tiles = (n + tile - 1) / tile;
-  hipLaunchKernelGGL(unsplit_words, dim3((unsigned)n_tiles), dim3(kUnsplitThreads), 0, s, runs, ovf_runs, row_map,
-                     w_pos, w_row, n, parts, tile, status);
+  if (w16)
+    hipLaunchKernelGGL(unsplit_words<uint16_t>, dim3((unsigned)n_tiles), dim3(kUnsplitThreads), 0, s, runs, ovf_runs,
+                       row_map, (const uint16_t *)w_pos, (uint16_t *)w_row, n, parts, tile, status);
+  else
+    hipLaunchKernelGGL(unsplit_words<uint32_t>, dim3((unsigned)n_tiles), dim3(kUnsplitThreads), 0, s, runs, ovf_runs,
+                       row_map, (const uint32_t *)w_pos, (uint32_t *)w_row, n, parts, tile, status);
   return hipGetLastError();
 }
 

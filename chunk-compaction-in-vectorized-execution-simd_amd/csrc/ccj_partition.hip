@@ -508,7 +508,7 @@ __device__ __forceinline__ uint32_t opaque_v32(uint32_t x) {
 // unconditional (a clamped tile, a per-XCD sink position for inactive lanes), so the waits the
 // compiler derives are the same on every path (a prologue issues the sink stores of "tile -1").
 // The sink: 64 positions at the end of the overflow area, or caller memory (kSplitSinkBytes).
-template <bool COUNTS, int THREADS, int MAXP, int PER>
+template <bool COUNTS, int THREADS, int MAXP, int PER, bool RUNS>
 __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, uint64_t n, uint32_t shift,
                                                                 uint32_t parts, uint64_t n_tiles, uint32_t *cur,
                                                                 uint64_t cap, uint64_t ovf_base, uint64_t ovf_cap,
@@ -621,7 +621,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
       const uint64_t dadj = seg * cap + r - loc;  // mod 2^64: + the image index gives the dest
       s_rec[tid] = make_uint4((uint32_t)dadj, (uint32_t)(dadj >> 32), loc + lim, loc + lim + olim);
       s_oadj[tid] = ovf_base + r2 - (loc + lim);
-      if (runs) {
+      if constexpr (RUNS) {  // (a compile-time switch: the C2 kernel carries no run-record state)
         runs[t * parts + tid] = make_uint2((uint32_t)(seg * cap + r), lim | olim << 16);
         if (olim) ovf_runs[t * parts + tid] = (uint32_t)(ovf_base + r2);
       }
@@ -675,7 +675,11 @@ static int split_per(uint32_t parts) {
   return parts > kSplitParts / 2 && per > 10 ? 10 : per;
 }
 
-uint32_t slot_split_tile_keys(uint32_t parts) { return (uint32_t)kSplitThreads * (uint32_t)split_per(parts); }
+// With run records (the ordered probe) the pipelined split holds 10 keys per thread: at 11 its
+// 128 VGPRs spill the run-record pointers, and every reload waits for the stores in flight.
+uint32_t slot_split_tile_keys(uint32_t parts, bool runs) {
+  return (uint32_t)kSplitThreads * (runs ? 10u : (uint32_t)split_per(parts));
+}
 
 hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPlan &pl, uint64_t cap,
                                    uint64_t ovf_base, uint64_t ovf_cap, uint32_t *cursors, int64_t *out_keys,
@@ -684,7 +688,7 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
                                    uint32_t shift, uint32_t wgs, void *sink) {
   const uint32_t parts = 1u << (pl.lo_bits + pl.hi_bits);
   // counts: a tile's chunks (tile / chunk + 2 at most) fit one count per thread
-  if (counts && (chunk == 0 || slot_split_tile_keys(parts) / chunk + 2 > (uint32_t)kSplitThreads))
+  if (counts && (chunk == 0 || slot_split_tile_keys(parts, runs != nullptr) / chunk + 2 > (uint32_t)kSplitThreads))
     return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(cursors, 0, ((size_t)parts * 8 + 1) * 4, s);
   if (e || n == 0) return e;
@@ -698,8 +702,8 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
     return (unsigned)(n >= 8 ? n / 8 * 8 : 8);
   }();
   const uint32_t ablate = (uint32_t)ccj_tune_int("CCJ_ABLATE", 0);  // timing-only (tuning build)
-  const int per = split_per(parts);
-  const uint32_t tile = slot_split_tile_keys(parts);
+  const int per = runs ? 10 : split_per(parts);
+  const uint32_t tile = slot_split_tile_keys(parts, runs != nullptr);
   if (shift == ~0u) shift = pl.window_bits;  // the slot split: partition = home slot >> window bits
   const uint64_t n_tiles = (n + tile - 1) / tile;
   const unsigned grid = wgs ? (wgs + 7) / 8 * 8 : cus;  // wgs: leave CUs to kernels of other streams
@@ -710,9 +714,16 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
     int64_t *sink_k = sink ? (int64_t *)sink : out_keys + ovf_base + oc;
     uint32_t *sink_r = sink ? (uint32_t *)((char *)sink + kSplitSinkBytes / 16 * 8) : out_rows + ovf_base + oc;
 #define CCJ_PIPE_LAUNCH(C, MAXP, P)                                                                                   \
-  hipLaunchKernelGGL((slot_split_pipe<C, kSplitThreads, MAXP, P>), dim3(grid), dim3(kSplitThreads), 0, s, keys, n,      \
-                     shift, parts, n_tiles, cursors, cap, ovf_base, oc, out_keys, out_rows, status, counts, chunk, runs, \
-                     ovf_runs, row_base, sink_k, sink_r)
+  do {                                                                                                              \
+    if (runs)                                                                                                       \
+      hipLaunchKernelGGL((slot_split_pipe<C, kSplitThreads, MAXP, P, true>), dim3(grid), dim3(kSplitThreads), 0, s,  \
+                         keys, n, shift, parts, n_tiles, cursors, cap, ovf_base, oc, out_keys, out_rows, status,     \
+                         counts, chunk, runs, ovf_runs, row_base, sink_k, sink_r);                                   \
+    else                                                                                                            \
+      hipLaunchKernelGGL((slot_split_pipe<C, kSplitThreads, MAXP, P, false>), dim3(grid), dim3(kSplitThreads), 0, s, \
+                         keys, n, shift, parts, n_tiles, cursors, cap, ovf_base, oc, out_keys, out_rows, status,     \
+                         counts, chunk, runs, ovf_runs, row_base, sink_k, sink_r);                                   \
+  } while (0)
     if (parts > kSplitParts / 2) {
       if (counts) CCJ_PIPE_LAUNCH(true, kSplitParts, 10);
       else CCJ_PIPE_LAUNCH(false, kSplitParts, 10);
