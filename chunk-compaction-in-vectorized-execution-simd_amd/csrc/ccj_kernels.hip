@@ -1849,6 +1849,8 @@ struct GatherParams {
   const int64_t *pay;
   uint32_t stride;
   int64_t *cols[CCJ_MAX_PAYLOAD_COLS];
+  uint32_t shift;  // timing only (tuning build, CCJ_GATHER_SHIFT): row = position >> shift
+  uint32_t ablate; // timing only (tuning build, CCJ_GATHER_ABLATE): 1 = no column stores
 };
 
 template <int NP, bool VEC>
@@ -1906,12 +1908,12 @@ __global__ __launch_bounds__(256) void gather_payload_quad(GatherParams g) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t j = base + u * 64 + r0;
-      if (j < n) v[u] = reinterpret_cast<const longlong2 *>(g.pay + (uint64_t)g.pos[ob + j] * g.stride)[q];
+      if (j < n) v[u] = reinterpret_cast<const longlong2 *>(g.pay + (uint64_t)(g.pos[ob + j] >> g.shift) * g.stride)[q];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t j = base + u * 64 + r0;
-      if (j < n) {
+      if (j < n && (!CCJ_ABLATED(g.ablate, 1u) || (v[u].x ^ v[u].y) == 0x5A5A5A5A5A5A5A5All)) {
         __builtin_nontemporal_store(v[u].x, c0 + ob + j);
         __builtin_nontemporal_store(v[u].y, c1 + ob + j);
       }
@@ -1940,6 +1942,8 @@ hipError_t launch_gather_payload(const ProbeParams &p, const uint32_t *pos, hipS
   g.pay = p.pay;
   g.stride = p.pay_stride;
   for (uint32_t q = 0; q < p.n_pay; ++q) g.cols[q] = p.out_cols[q];
+  g.shift = (uint32_t)ccj_tune_int("CCJ_GATHER_SHIFT", 0);
+  g.ablate = (uint32_t)ccj_tune_int("CCJ_GATHER_ABLATE", 0);
   switch (p.n_pay) {
     case 1: return launch_gather_np<1>(g, p.n_chunks, s);
     case 2: return launch_gather_np<2>(g, p.n_chunks, s);
