@@ -532,7 +532,13 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   if (L.pl.lo_bits && !exact && !a->status)
     return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: the fixed-capacity split needs args->status");
   hipStream_t s = (hipStream_t)stream;
-  int64_t *pkeys = (int64_t *)ws;
+  // With one output slot per position (cap == chunk) the partitioned keys are written straight
+  // into out_payload: a matched row's payload is its key (an LP match means slot value == key), so
+  // the walk writes payloads only for chunks where some row missed (in place, compacted).
+  const bool alias = a->out_payload && p.cap == a->chunk && p.n_pay == 0 && !a->out_pos &&
+                     t->info.kind == CCJ_TABLE_LP && t->info.size >= 16 && ccj_tune_int("CCJ_KEYS_IN_OUT", 1);
+  int64_t *pkeys = alias ? a->out_payload : (int64_t *)ws;
+  p.keys_in_out = alias ? 1u : 0u;
   void *rest = (char *)ws + align256(L.positions * 8);
   const uint64_t out_chunks = L.positions / a->chunk + (L.positions % a->chunk ? 1 : 0);
   if (L.pl.lo_bits == 0) {  // the whole table is one window: identity order

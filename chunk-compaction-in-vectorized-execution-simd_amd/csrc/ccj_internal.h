@@ -81,6 +81,9 @@ struct ProbeParams {
   // probe_walk's emit: kEmitWave = per-wave placement; else the chunk's output staged in LDS in row
   // order and written with 16-byte buffer stores of this cache policy (aux bits: 2 nt, 16 sc1)
   uint32_t emit_pol;
+  // 1: keys IS out_payload (ccj_probe_partitioned, cap == chunk): the split wrote every row's key
+  // at its own output position, so a chunk whose rows all match once already holds its payload
+  uint32_t keys_in_out;
   uint32_t ablate;       // timing-only ablations (tuning build only: CCJ_ABLATE)
   unsigned long long *stats;  // tuning build only (CCJ_STATS): per-phase cycle sums of the walk
   // Ordered probe (ccj_probe_ordered): round words per position (walk) / per row (emit input)

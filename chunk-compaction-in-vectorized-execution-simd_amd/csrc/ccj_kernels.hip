@@ -1394,14 +1394,15 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // partial group writes past the count inside the chunk's own cap region (cap is a multiple of 4),
 // which holds no data of the chunk's consumers.
 template <int AUX, uint32_t kThreads>
-__device__ __forceinline__ void emit_wg_stores(const ProbeParams &p, WalkShared<true> &sm, uint64_t obase, uint32_t tot) {
+__device__ __forceinline__ void emit_wg_stores(const ProbeParams &p, WalkShared<true> &sm, uint64_t obase, uint32_t tot,
+                                               bool pay) {
   const uint32_t tid = threadIdx.x;
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(p.out_sel + obase, (short)0, (int)(p.cap * 4), 0x00020000);
   for (uint32_t q = tid; q * 4 < tot; q += kThreads) {
     const u32x4 v = *reinterpret_cast<const u32x4 *>(&sm.hc[4 * q]);
     __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)(16 * q), 0, AUX);
   }
-  if (p.out_payload) {
+  if (pay) {
     const auto rp = __builtin_amdgcn_make_buffer_rsrc(p.out_payload + obase, (short)0, (int)(p.cap * 8), 0x00020000);
     for (uint32_t q = tid; q * 2 < tot; q += kThreads) {
       const u32x4 v = *reinterpret_cast<const u32x4 *>(&sm.key[2 * q]);
@@ -1411,7 +1412,8 @@ __device__ __forceinline__ void emit_wg_stores(const ProbeParams &p, WalkShared<
 }
 template <uint32_t kWaveRows, int NW>
 __device__ __forceinline__ bool walk_emit_wg(const ProbeParams &p, WalkShared<true> &sm, uint64_t c, uint32_t w0,
-                                             uint32_t wend, uint32_t lane, uint32_t wave, uint32_t *s_wtot) {
+                                             uint32_t wend, uint32_t lane, uint32_t wave, uint32_t *s_wtot,
+                                             uint32_t phys) {
   constexpr int kJ = (int)(kWaveRows / kWave);
   uint32_t lsum = 0, multi = 0;
   uint32_t n[kJ];
@@ -1455,11 +1457,14 @@ __device__ __forceinline__ bool walk_emit_wg(const ProbeParams &p, WalkShared<tr
   }
   __syncthreads();
   const uint64_t obase = c * p.cap;
+  // keys_in_out and every row matched once: the payload column already holds the chunk's output
+  // (the split wrote each key at its position); only sel is written
+  const bool pay = p.out_payload && !(p.keys_in_out && tot == phys);
   switch (p.emit_pol) {  // the buffer stores' cache bits are an immediate
-    case 2: emit_wg_stores<2, kWave * NW>(p, sm, obase, tot); break;
-    case 16: emit_wg_stores<16, kWave * NW>(p, sm, obase, tot); break;
-    case 18: emit_wg_stores<18, kWave * NW>(p, sm, obase, tot); break;
-    default: emit_wg_stores<0, kWave * NW>(p, sm, obase, tot); break;
+    case 2: emit_wg_stores<2, kWave * NW>(p, sm, obase, tot, pay); break;
+    case 16: emit_wg_stores<16, kWave * NW>(p, sm, obase, tot, pay); break;
+    case 18: emit_wg_stores<18, kWave * NW>(p, sm, obase, tot, pay); break;
+    default: emit_wg_stores<0, kWave * NW>(p, sm, obase, tot, pay); break;
   }
   if (threadIdx.x == 0) sm.total = tot;
   return true;
@@ -1598,7 +1603,7 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk(ProbeParams p) {
     if (p.emit_pol != kEmitWave) {
       __shared__ uint32_t s_wtot[NW];
       wave_lds_sync();
-      if (walk_emit_wg<kWaveRows, NW>(p, sm, c, w0, wend, lane, wave, s_wtot)) {
+      if (walk_emit_wg<kWaveRows, NW>(p, sm, c, w0, wend, lane, wave, s_wtot, phys)) {
         walk_finish(p, sm, c, lane, lane_rounds, 0u, t0, t1, t2, steps);
         return;
       }
