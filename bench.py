@@ -44,8 +44,8 @@ METRIC = "probe tuples/sec + achieved HBM GB/s, 1B-row int64 join at 1/2/4/8 GPU
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
 SEED = 42
 PATH_KERNELS = {
-    "partitioned": "ccj_probe_partitioned (slot_split_fixed + probe_walk<3>)",
-    "ordered": "ccj_probe_ordered (slot_split_fixed with runs + probe_walk<3,MM> + unsplit_words + probe_chunks<LP,2,FROM_W>)",
+    "partitioned": "ccj_probe_partitioned, CCJ_PART_ROWS (slot_split_pipe writing keys + rows into the outputs, probe_walk<3>)",
+    "ordered": "ccj_probe_ordered (slot_split_pipe with runs + probe_walk<3,MM> + unsplit_words + emit_ordered, 16-bit round words)",
     "chunk": "ccj_probe (probe_chunks<LP,2>)",
 }
 
@@ -464,9 +464,14 @@ def main():
     log(f"[setup] table {table.size} slots, max_rounds {table.max_rounds}, keys {n_probe}: "
         f"{time.perf_counter() - t0:.1f} s")
 
+    # C2 (distinct build keys, one output slot per position): CCJ_PART_ROWS — out_sel receives each
+    # match's original row, and the split writes every position's key and row straight into the
+    # output columns (ccj.h), so the walk only compacts chunks with misses
+    rows_mode = not c5 and int(table.max_dup) <= 1
+
     def step(path=args.path):
         if path == "partitioned":  # no host check inside the timed region: status is read after it
-            table.probe_partitioned(keys, chunk, out=out_p, part=part, stream=stream, retry=False)
+            table.probe_partitioned(keys, chunk, out=out_p, part=part, stream=stream, retry=False, rows=rows_mode)
         elif path == "ordered":  # L3 through the partitioned layout (status read after the timing)
             table.probe_ordered(keys, chunk, out=out_o, ws=ws_o, stream=stream, retry=False)
         else:
@@ -504,9 +509,12 @@ def main():
         if status & ccj.FLAG_PART_OVERFLOW:
             raise SystemExit("bench: fixed-capacity partition overflowed on uniform keys")
         out_p["n_chunks"] = (part["positions"] + chunk - 1) // chunk
-        rm = part["row_map"].to(torch.int64) + rank * n_probe
-        matches, l2 = ccj.result_checksum(out_p, chunk, row_map=rm, stream=stream)
-        del rm
+        if rows_mode:  # sel = the original row
+            matches, l2 = ccj.result_checksum(out_p, 0, row_base=rank * n_probe, stream=stream)
+        else:
+            rm = part["row_map"].to(torch.int64) + rank * n_probe
+            matches, l2 = ccj.result_checksum(out_p, chunk, row_map=rm, stream=stream)
+            del rm
     else:
         res0 = out_o if args.path == "ordered" else out
         status = int(res0["status"].item())
@@ -526,9 +534,12 @@ def main():
         o_ms = sum(a.elapsed_time(b) for a, b in ev2) / len(ev2)
         if other == "partitioned":
             out_p["n_chunks"] = (part["positions"] + chunk - 1) // chunk
-            rm = part["row_map"].to(torch.int64) + rank * n_probe
-            om, ol2 = ccj.result_checksum(out_p, chunk, row_map=rm, stream=stream)
-            del rm
+            if rows_mode:
+                om, ol2 = ccj.result_checksum(out_p, 0, row_base=rank * n_probe, stream=stream)
+            else:
+                rm = part["row_map"].to(torch.int64) + rank * n_probe
+                om, ol2 = ccj.result_checksum(out_p, chunk, row_map=rm, stream=stream)
+                del rm
             o_par = {"status_flags": int(out_p["status"].item()), "matches": om, "l2": hex(ol2)}
         else:
             res = out_o if other == "ordered" else out
@@ -610,7 +621,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          # measured DRAM bytes (whole 128-B lines per random slot read) per second
                          "traffic_GBps": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
-                         "kernel": (("ccj_probe_partitioned (slot_split_fixed + probe_win<3> with positions + "
+                         "kernel": (("ccj_probe_partitioned (slot_split_pipe + probe_win<3> with positions + "
                                      "gather_payload_quad)") if c5 and args.path == "partitioned" else
                                     "probe_chunks<LP,2> + gather_payload_quad" if c5 else PATH_KERNELS[args.path]),
                          "kernel_ms": kern_ms, "rocprof_kernels_ms": kernels_ms,

@@ -523,9 +523,14 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   if ((a->out_pos || a->n_payload_cols) && t->info.size < 16)
     return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: positions / payload columns need a table of >= 16 slots");
   if (a->n_rows >= (1ull << 32)) return fail(CCJ_ERR_LIMIT, "ccj_probe_partitioned: n_rows must be < 2^32");
-  if (flags & ~CCJ_PART_EXACT) return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: unknown flags");
+  if (flags & ~(CCJ_PART_EXACT | CCJ_PART_ROWS)) return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: unknown flags");
+  const bool rows = (flags & CCJ_PART_ROWS) != 0;
+  if (rows && (!a->out_payload || p.cap != a->chunk || t->info.max_dup > 1 || a->out_pos || a->n_payload_cols ||
+               t->info.kind != CCJ_TABLE_LP || t->info.size < 16))
+    return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: CCJ_PART_ROWS needs an LP table of >= 16 slots with distinct "
+                                 "keys, cap == chunk, out_payload, and no positions / payload columns");
   if (a->n_rows == 0) return CCJ_OK;
-  if (!out_row_map || !ws || ws_bytes < ccj_probe_partitioned_workspace_size(t, a->n_rows, a->chunk))
+  if ((!out_row_map && !rows) || !ws || ws_bytes < ccj_probe_partitioned_workspace_size(t, a->n_rows, a->chunk))
     return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: missing row map or workspace too small");
   const PartLayout L = part_layout(t, a->n_rows, a->chunk);
   const bool exact = (flags & CCJ_PART_EXACT) != 0;
@@ -535,10 +540,14 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   // With one output slot per position (cap == chunk) the partitioned keys are written straight
   // into out_payload: a matched row's payload is its key (an LP match means slot value == key), so
   // the walk writes payloads only for chunks where some row missed (in place, compacted).
-  const bool alias = a->out_payload && p.cap == a->chunk && p.n_pay == 0 && !a->out_pos &&
-                     t->info.kind == CCJ_TABLE_LP && t->info.size >= 16 && ccj_tune_int("CCJ_KEYS_IN_OUT", 1);
+  // With CCJ_PART_ROWS the split likewise writes each position's original row into out_sel.
+  const bool alias = rows || (a->out_payload && p.cap == a->chunk && p.n_pay == 0 && !a->out_pos &&
+                              t->info.kind == CCJ_TABLE_LP && t->info.size >= 16 &&
+                              ccj_tune_int("CCJ_KEYS_IN_OUT", 1));
   int64_t *pkeys = alias ? a->out_payload : (int64_t *)ws;
   p.keys_in_out = alias ? 1u : 0u;
+  p.rows_in_sel = rows ? 1u : 0u;
+  if (rows) out_row_map = a->out_sel;
   void *rest = (char *)ws + align256(L.positions * 8);
   const uint64_t out_chunks = L.positions / a->chunk + (L.positions % a->chunk ? 1 : 0);
   if (L.pl.lo_bits == 0) {  // the whole table is one window: identity order

@@ -84,6 +84,9 @@ struct ProbeParams {
   // 1: keys IS out_payload (ccj_probe_partitioned, cap == chunk): the split wrote every row's key
   // at its own output position, so a chunk whose rows all match once already holds its payload
   uint32_t keys_in_out;
+  // 1 (CCJ_PART_ROWS, with keys_in_out): out_sel holds each match's original row, written by the
+  // split at every position; the walk only compacts chunks with misses
+  uint32_t rows_in_sel;
   uint32_t ablate;       // timing-only ablations (tuning build only: CCJ_ABLATE)
   unsigned long long *stats;  // tuning build only (CCJ_STATS): per-phase cycle sums of the walk
   // Ordered probe (ccj_probe_ordered): round words per position (walk) / per row (emit input)

@@ -1437,8 +1437,15 @@ __device__ __forceinline__ bool walk_emit_wg(const ProbeParams &p, WalkShared<tr
     tot += x & 0x7FFFFFFFu;
   }
   if (any_multi || tot > p.cap) return false;
+  const uint64_t obase = c * p.cap;
+  // rows_in_sel (keys_in_out too): the split wrote every position's original row into out_sel
+  // and its key into out_payload, so a chunk whose rows all matched once is complete as it is
+  if (p.rows_in_sel && tot == phys) {
+    if (threadIdx.x == 0) sm.total = tot;
+    return true;
+  }
   int64_t k[kJ];
-  uint32_t t[kJ];
+  uint32_t t[kJ], rid[kJ];
 #pragma unroll
   for (int j = 0; j < kJ; ++j) {
     const uint32_t i = w0 + (uint32_t)j * kWave + lane;
@@ -1446,17 +1453,18 @@ __device__ __forceinline__ bool walk_emit_wg(const ProbeParams &p, WalkShared<tr
     t[j] = base + lane_prefix(bm);
     base += (uint32_t)__popcll(bm);
     k[j] = sm.key[i & (kMaxChunk - 1)];
+    rid[j] = i;
+    if (p.rows_in_sel && n[j]) rid[j] = p.out_sel[obase + i];  // the row the split stored there
   }
-  __syncthreads();  // every key read before any entry moves down
+  __syncthreads();  // every key (and row) read before any entry moves down
 #pragma unroll
   for (int j = 0; j < kJ; ++j) {
     if (n[j]) {
       sm.key[t[j]] = k[j];
-      sm.hc[t[j]] = w0 + (uint32_t)j * kWave + lane;
+      sm.hc[t[j]] = rid[j];
     }
   }
   __syncthreads();
-  const uint64_t obase = c * p.cap;
   // keys_in_out and every row matched once: the payload column already holds the chunk's output
   // (the split wrote each key at its position); only sel is written
   const bool pay = p.out_payload && !(p.keys_in_out && tot == phys);
@@ -1600,7 +1608,7 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk(ProbeParams p) {
     return;
   }
   if constexpr (HOME) {
-    if (p.emit_pol != kEmitWave) {
+    if (p.emit_pol != kEmitWave || p.rows_in_sel) {  // (rows_in_sel: only the workgroup emit maps rows)
       __shared__ uint32_t s_wtot[NW];
       wave_lds_sync();
       if (walk_emit_wg<kWaveRows, NW>(p, sm, c, w0, wend, lane, wave, s_wtot, phys)) {

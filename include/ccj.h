@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CCJ_ABI_VERSION 6
+#define CCJ_ABI_VERSION 7  /* 7: CCJ_PART_ROWS; keys of cap == chunk partitioned probes go to out_payload */
 
 enum ccj_status {
   CCJ_OK = 0,
@@ -193,6 +193,14 @@ int ccj_probe_visits(const ccj_table *table, const int64_t *d_keys, const uint32
  * out_pos (table position of every match) and payload columns (C5: gathered after the walk) are
  * produced as by ccj_probe, for tables of >= 16 slots. */
 #define CCJ_PART_EXACT 1u
+/* flags & CCJ_PART_ROWS: out_sel receives the ORIGINAL row of every match (u32, row of args->keys)
+ * instead of its position inside the chunk, and out_row_map may be NULL.  LP tables of >= 16
+ * slots with distinct keys (max_dup 1), cap == chunk, out_payload set, no out_pos / payload
+ * columns.  The split then writes each position's key into out_payload and its row into out_sel
+ * (position p IS output slot p of its chunk: an LP match's payload is the probe key), and the walk
+ * only compacts the chunks where some row missed.  Without the flag, when cap == chunk the keys
+ * still go to out_payload (the workspace's key region is then left untouched). */
+#define CCJ_PART_ROWS 2u
 uint64_t ccj_probe_partitioned_positions(const ccj_table *table, uint64_t n_rows, uint32_t chunk);
 size_t ccj_probe_partitioned_workspace_size(const ccj_table *table, uint64_t n_rows, uint32_t chunk);
 int ccj_probe_partitioned(const ccj_table *table, const ccj_probe_args *args, uint32_t flags,

@@ -178,6 +178,45 @@ def test_partitioned_probe_l1_l2(n_build, cf, n_probe, rng, exact):
         assert np.array_equal(np.sort(rm), np.arange(n_probe, dtype=np.uint32))
 
 
+@pytest.mark.parametrize("n_build,n_probe,rng", [(1 << 20, 1 << 22, 1 << 20), (1 << 20, 1 << 22, 3 << 19),
+                                                (5000, 70000, 20000), (100, 5000, 100), (1 << 16, 1000, 1 << 18)])
+@pytest.mark.parametrize("exact", [False, True])
+def test_partitioned_probe_rows_mode(n_build, n_probe, rng, exact):
+    """CCJ_PART_ROWS (distinct keys, cap == chunk): the split writes every position's key into
+    out_payload and its original row into out_sel; the walk compacts only the chunks with misses.
+    rng == n_build: every row matches (no chunk is touched by the walk's emit); larger ranges mix
+    full chunks and compacted ones.  Exact L1 + L2 with sel read as global rows, and every output
+    pair (row, payload) is the row's own key."""
+    table = ccj.Table.reference(ccj.LP, n_build, 1, ccj.LAYOUT_DEVICE)
+    keys = ccj.gen_uniform_keys(n_probe, 37, rng)
+    out = table.probe_partitioned(keys, 2048, exact=exact, rows=True)
+    torch.cuda.synchronize()
+    assert int(out["status"].item()) == 0 and out["row_map"] is None
+    assert ccj.result_checksum(out, 0) == O.count_uniform(37, 0, n_probe, rng, n_build, 1)
+    cnt = out["count"][:out["n_chunks"]].cpu().numpy().view(np.uint32).astype(np.int64)
+    cap = out["cap"]
+    idx = (np.arange(len(cnt))[:, None] * cap + np.arange(2048)[None, :])[np.arange(2048)[None, :] < cnt[:, None]]
+    sel = out["sel"].cpu().numpy().view(np.uint32)[idx].astype(np.int64)
+    pay = out["payload"].cpu().numpy()[idx]
+    k = keys.cpu().numpy()
+    assert np.array_equal(pay, k[sel])  # payload = the matched row's key
+    assert len(np.unique(sel)) == len(sel)  # distinct keys: each row at most once
+
+
+def test_partitioned_probe_payload_aliasing_off_matches_on():
+    """cap == chunk without CCJ_PART_ROWS: the keys go straight to out_payload; the outputs (per chunk
+    counts, sel, payload) are the same multiset as with the workspace key column (cap > chunk)."""
+    table = ccj.Table.reference(ccj.LP, 1 << 16, 1, ccj.LAYOUT_DEVICE)
+    keys = ccj.gen_uniform_keys(1 << 20, 41, 3 << 15)
+    a = table.probe_partitioned(keys, 2048)
+    b = table.probe_partitioned(keys, 2048, cap=4096)
+    torch.cuda.synchronize()
+    assert a["cap"] == 2048 and b["cap"] == 4096
+    want = O.count_uniform(41, 0, 1 << 20, 3 << 15, 1 << 16, 1)
+    assert ccj.result_checksum(a, 2048, row_map=a["row_map"].to(torch.int64)) == want
+    assert ccj.result_checksum(b, 2048, row_map=b["row_map"].to(torch.int64)) == want
+
+
 @pytest.mark.parametrize("n_build,cf,n_probe,rng", [(1 << 20, 1, 1 << 22, 1 << 20), (1 << 16, 3, 300000, 1 << 17),
                                                     (5000, 1, 70000, 20000), (4096, 64, 100000, 8192),
                                                     (3, 1, 5000, 6), (1 << 19, 2, 1 << 21, 3 << 19)])
