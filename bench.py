@@ -45,6 +45,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
 SEED = 42
 PATH_KERNELS = {
     "partitioned": "ccj_probe_partitioned, CCJ_PART_ROWS (slot_split_pipe writing keys + rows into the outputs, probe_walk<3>)",
+    "rank": "ccj_probe_partitioned, CCJ_PART_ROWS | CCJ_PART_RANK (slot_split_pipe + probe_rank: the window's occupancy "
+            "bitmap + rank in LDS, keys from the compact array; rank_finish) — opt-in, A/B",
     "ordered": "ccj_probe_ordered (slot_split_pipe with runs + probe_walk<3,MM> + unsplit_words + emit_ordered, 16-bit round words)",
     "chunk": "ccj_probe (probe_chunks<LP,2>)",
 }
@@ -472,6 +474,9 @@ def main():
     def step(path=args.path):
         if path == "partitioned":  # no host check inside the timed region: status is read after it
             table.probe_partitioned(keys, chunk, out=out_p, part=part, stream=stream, retry=False, rows=rows_mode)
+        elif path == "rank":  # the rank walk (CCJ_PART_RANK, opt-in: A/B beside the headline)
+            table.probe_partitioned(keys, chunk, out=out_p, part=part, stream=stream, retry=False, rows=rows_mode,
+                                    rank=True)
         elif path == "ordered":  # L3 through the partitioned layout (status read after the timing)
             table.probe_ordered(keys, chunk, out=out_o, ws=ws_o, stream=stream, retry=False)
         else:
@@ -521,6 +526,8 @@ def main():
         matches, l2 = ccj.result_checksum(res0, chunk, row_base=rank * n_probe, stream=stream)
     # the other paths, timed the same way (reported beside the headline)
     others = [] if c5 or args.no_other else [q for q in ("ordered", "chunk", "partitioned") if q != args.path]
+    if args.path == "partitioned" and not c5:
+        others.append("rank")  # A/B: the rank walk on the same split, same run
     other_runs = {}
     for other in others:
         step(other)
@@ -532,7 +539,7 @@ def main():
             b.record(stream)
         stream.synchronize()
         o_ms = sum(a.elapsed_time(b) for a, b in ev2) / len(ev2)
-        if other == "partitioned":
+        if other in ("partitioned", "rank"):
             out_p["n_chunks"] = (part["positions"] + chunk - 1) // chunk
             if rows_mode:
                 om, ol2 = ccj.result_checksum(out_p, 0, row_base=rank * n_probe, stream=stream)
@@ -632,7 +639,7 @@ def main():
             "other_paths": [{
                 "path": o, "ms_per_step": o_ms, "value": n_probe / (o_ms * 1e-3),
                 "frac": alg_bytes / (o_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                "parity": "L3 (reference order)" if o != "partitioned" else "L1/L2",
+                "parity": "L3 (reference order)" if o not in ("partitioned", "rank") else "L1/L2",
                 "kernel": PATH_KERNELS[o], "check": o_par} for o, (o_ms, o_par) in other_runs.items()],
         }
         print(json.dumps(line), flush=True)

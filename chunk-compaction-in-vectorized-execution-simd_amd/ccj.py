@@ -24,6 +24,7 @@ LAYOUT_REFERENCE, LAYOUT_DEVICE = 0, 1
 FLAG_CAP_OVERFLOW, FLAG_ROUND_OVERFLOW, FLAG_BAD_INPUT, FLAG_PART_OVERFLOW = 1, 2, 4, 8
 PART_EXACT = 1
 PART_ROWS = 2  # out_sel = the original row of every match (ccj.h CCJ_PART_ROWS)
+PART_RANK = 4  # the rank walk (LDS window index) instead of the slot-array walk (ccj.h CCJ_PART_RANK)
 
 _lib = None
 
@@ -307,7 +308,8 @@ class Table:
                     n_rows=n_rows, chunk=chunk)
 
     def probe_partitioned(self, keys, chunk: int, out=None, part=None, stream=None, exact: bool = False,
-                          retry: bool = True, counts=None, rows: bool = False, **alloc_kw):
+                          retry: bool = True, counts=None, rows: bool = False, rank: bool = False,
+                          **alloc_kw):
         """Slot-range-partitioned probe (ccj_probe_partitioned): L1/L2 results of probe(); out_sel
         indexes the partitioned layout and part["row_map"] maps a live position back to its row.
         The default one-pass split may overflow a segment under heavy key skew
@@ -316,7 +318,8 @@ class Table:
         (fixed-capacity segments, e.g. the multi-GPU exchange's receive buffers); with counts an
         overflow is left to the caller (the exact split takes no counts).  rows=True
         (CCJ_PART_ROWS: LP, distinct keys, cap == chunk): out_sel holds the original row of every
-        match instead of its position (result_checksum(out, 0) then needs no row map)."""
+        match instead of its position (result_checksum(out, 0) then needs no row map).
+        rank=True (CCJ_PART_RANK): the rank walk where it applies (LP, distinct keys, cap == chunk)."""
         n = keys.numel()
         if part is None:
             part = self.alloc_partitioned(n, chunk)
@@ -330,7 +333,8 @@ class Table:
             raise CCJError("probe output buffers smaller than the partitioned layout needs")
         a = self._args(keys, chunk, None, counts, out)
         a.out_round_counts = None  # no Next boundaries in partition order
-        flags = (PART_EXACT if exact else 0) | (PART_ROWS if rows else 0)
+        sw = PART_RANK if rank else 0
+        flags = (PART_EXACT if exact else 0) | (PART_ROWS if rows else 0) | sw
         row_map = None if rows else _ptr(part["row_map"])
         check(lib().ccj_probe_partitioned(self._h, C.byref(a), flags, row_map, _ptr(part["ws"]),
                                           part["ws_bytes"], _stream(stream)), "ccj_probe_partitioned")
@@ -344,7 +348,7 @@ class Table:
             if st & FLAG_PART_OVERFLOW:
                 out["status"].fill_(st & ~FLAG_PART_OVERFLOW)
                 torch.cuda.synchronize()  # the fill ran on torch's stream, the re-run goes on `stream`
-                check(lib().ccj_probe_partitioned(self._h, C.byref(a), PART_EXACT | (PART_ROWS if rows else 0),
+                check(lib().ccj_probe_partitioned(self._h, C.byref(a), PART_EXACT | (PART_ROWS if rows else 0) | sw,
                                                   row_map, _ptr(part["ws"]), part["ws_bytes"], _stream(stream)),
                       "ccj_probe_partitioned")
                 out["exact_retry"] = True

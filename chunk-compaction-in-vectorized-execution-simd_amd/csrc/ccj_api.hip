@@ -114,6 +114,37 @@ int upload(void **dst, const void *src, size_t bytes, const char *what) {
   return CCJ_OK;
 }
 
+// The rank walk's window index (ccj_rank.hip), built on the device from the finished slot array for
+// tables the partitioned probe splits into windows the LDS can hold (<= 2^19 slots).  Build-time
+// work like the table itself (main.cpp:62-68 times neither).  Without it the slot-array walk runs.
+int build_rank_index(ccj_table *t, hipStream_t s) {
+  const ccj::SlotPlan pl = ccj::slot_plan(t->info.size, CCJ_TABLE_LP);
+  const uint64_t size = t->info.size;
+  if (pl.lo_bits == 0 || !ccj::rank_walk_fits(pl.window_bits) || size % 128 || size > (1ull << 32)) return CCJ_OK;
+  const uint64_t words = size / 64;
+  uint32_t *cnt = nullptr;
+  hipError_t e = hipMalloc((void **)&t->d_occ, words * 8);
+  if (e == hipSuccess) e = hipMalloc((void **)&t->d_pre, words / 2 * 4);
+  if (e == hipSuccess) e = hipMalloc((void **)&cnt, words * 4);
+  const uint64_t nck = t->info.n_keys + 32;  // occupied slots <= keys; 4-key windows read past the last
+  if (e == hipSuccess) e = hipMalloc((void **)&t->d_ckeys, nck * 8);
+  if (e == hipSuccess) e = ccj::launch_fill(t->d_ckeys, nck, -1, s);
+  if (e == hipSuccess) e = ccj::launch_rank_index(t->d_table, size, t->d_occ, t->d_pre, cnt, s);
+  if (e == hipSuccess) e = ccj::launch_rank_compact_keys(t->d_table, size, t->d_occ, t->d_pre, t->d_ckeys, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (cnt) (void)hipFree(cnt);
+  if (e != hipSuccess) {
+    for (void *q : {(void *)t->d_occ, (void *)t->d_pre, (void *)t->d_ckeys})
+      if (q) (void)hipFree(q);
+    t->d_occ = nullptr;
+    t->d_pre = nullptr;
+    t->d_ckeys = nullptr;
+    return hip_fail(e, "LP window index");
+  }
+  t->rank_wbits = pl.window_bits;
+  return CCJ_OK;
+}
+
 int build_lp_host(const int64_t *keys, uint64_t n, ccj_table **out) {
   const uint64_t size = lp_num_slots(n);
   if (size > (1ull << 32)) return fail(CCJ_ERR_LIMIT, "LP table larger than 2^32 slots");
@@ -147,6 +178,12 @@ int build_lp_host(const int64_t *keys, uint64_t n, ccj_table **out) {
   t->d_row = (uint32_t *)d;
   t->info.d_table = t->d_table;
   (void)hipGetDevice(&t->device);
+  rc = build_rank_index(t.get(), nullptr);
+  if (rc) {
+    (void)hipFree(t->d_table);
+    (void)hipFree(t->d_row);
+    return rc;
+  }
   *out = t.release();
   return CCJ_OK;
 }
@@ -307,6 +344,10 @@ int build_lp_device(const int64_t *d_keys, uint64_t n, hipStream_t s, uint64_t k
   t->info.max_dup = dup ? dup : 1;
   t->info.d_table = t->d_table;
   (void)hipGetDevice(&t->device);
+  if (int rc = build_rank_index(t.get(), s)) {
+    cleanup();
+    return rc;
+  }
   *out = t.release();
   return CCJ_OK;
 }
@@ -426,6 +467,9 @@ int ccj_table_free(ccj_table *t) {
   if (t->d_bucket) (void)hipFree(t->d_bucket);
   if (t->d_row) (void)hipFree(t->d_row);
   if (t->d_pay) (void)hipFree(t->d_pay);
+  if (t->d_occ) (void)hipFree(t->d_occ);
+  if (t->d_pre) (void)hipFree(t->d_pre);
+  if (t->d_ckeys) (void)hipFree(t->d_ckeys);
   delete t;
   return CCJ_OK;
 }
@@ -506,7 +550,9 @@ size_t ccj_probe_partitioned_workspace_size(const ccj_table *t, uint64_t n_rows,
   // partitioned keys (positions) + the fixed split's cursors, or the exact split's pass scratch
   const size_t fixed = align256(((uint64_t)L.parts * 8 + 1) * 4);
   const size_t exact = ccj::slot_partition_workspace(n_rows, L.pl);
-  return align256(L.positions * 8) + (fixed > exact ? fixed : exact);
+  // + the rank walk's per-block hit masks, hit counts and partition counters
+  const size_t rank = t->d_ckeys && L.pl.lo_bits ? ccj::rank_workspace(L.positions, L.parts) : 0;
+  return align256(L.positions * 8) + align256(fixed > exact ? fixed : exact) + rank;
 }
 
 int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t flags, uint32_t *out_row_map,
@@ -523,7 +569,7 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   if ((a->out_pos || a->n_payload_cols) && t->info.size < 16)
     return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: positions / payload columns need a table of >= 16 slots");
   if (a->n_rows >= (1ull << 32)) return fail(CCJ_ERR_LIMIT, "ccj_probe_partitioned: n_rows must be < 2^32");
-  if (flags & ~(CCJ_PART_EXACT | CCJ_PART_ROWS)) return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: unknown flags");
+  if (flags & ~(CCJ_PART_EXACT | CCJ_PART_ROWS | CCJ_PART_RANK)) return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: unknown flags");
   const bool rows = (flags & CCJ_PART_ROWS) != 0;
   if (rows && (!a->out_payload || p.cap != a->chunk || t->info.max_dup > 1 || a->out_pos || a->n_payload_cols ||
                t->info.kind != CCJ_TABLE_LP || t->info.size < 16))
@@ -581,6 +627,20 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
 #ifdef CCJ_TUNING
   p.ablate = (uint32_t)ccj_tune_int("CCJ_ABLATE", 0);
 #endif
+  // The rank walk (CCJ_PART_RANK, ccj_rank.hip): the window index in LDS, candidate keys from the
+  // compact array.  Distinct keys (a row matches at most once), the keys in out_payload (cap ==
+  // chunk), blocks of 512 rows inside chunks, the index built for this window size.
+  const bool rank = !exact && L.pl.lo_bits && L.ovf_base && t->d_ckeys && t->rank_wbits == L.pl.window_bits &&
+                    p.keys_in_out && t->info.max_dup <= 1 && p.n_pay == 0 && !p.out_pos && !p.out_rounds &&
+                    a->chunk % ccj::kRankChunkMultiple == 0 && ((flags & CCJ_PART_RANK) || ccj_tune_int("CCJ_RANK", 0));
+  if (rank) {
+    const ccj::RankIndex ix{t->d_occ, t->d_pre, t->d_ckeys, t->rank_wbits};
+    const size_t fixed = align256(((uint64_t)L.parts * 8 + 1) * 4);
+    const size_t exact_ws = ccj::slot_partition_workspace(a->n_rows, L.pl);
+    void *rws = (char *)rest + align256(fixed > exact_ws ? fixed : exact_ws);
+    HIP_TRY(ccj::launch_probe_rank(p, ix, rws, s), "rank walk launch");
+    return CCJ_OK;
+  }
   if (p.n_pay == 0) {
 #ifdef CCJ_TUNING
     // CCJ_STATS: per-phase cycle sums of the walk's waves, printed per launch (tuning only)

@@ -18,6 +18,13 @@ struct ccj_table {
   int64_t *d_pay = nullptr;     // position-major payload rows [positions][n_pay]
   uint32_t n_pay = 0;
   int device = 0;
+  // LP window index of the rank walk (ccj_rank.hip; absent: the slot-array walk): occupancy bits,
+  // occupied slots before each 64-slot word, occupied slots' keys in slot order; built for windows
+  // of rank_wbits slots
+  uint64_t *d_occ = nullptr;
+  uint32_t *d_pre = nullptr;
+  int64_t *d_ckeys = nullptr;
+  uint32_t rank_wbits = 0;
 };
 
 namespace ccj {
@@ -95,6 +102,8 @@ struct ProbeParams {
   // 1: the round words are 16-bit, L << 7 | the row's match round (127: none) — tables whose keys
   // are distinct (max_dup 1), where a row matches in at most one round
   uint32_t w16;
+  // probe_walk: first chunk of the launch (blockIdx.x + chunk0; the rank walk's overflow-area pass)
+  uint64_t chunk0;
 };
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 constexpr uint32_t kEmitWave = 0xFFFFFFFFu;
@@ -189,6 +198,22 @@ uint32_t slot_split_tile_keys(uint32_t parts, bool runs = false);
 hipError_t launch_partition_fixed(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t row_base, uint64_t seg_cap,
                                   int64_t *out_keys, uint32_t *out_rows, uint64_t *out_counts, uint32_t *status,
                                   void *ws, hipStream_t s);
+// Rank walk (ccj_rank.hip): the LP window index in LDS, keys from the compact key array.
+struct RankIndex {
+  const uint64_t *occ;
+  const uint32_t *pre;
+  const int64_t *ckeys;
+  uint32_t wbits;
+};
+bool rank_walk_fits(uint32_t window_bits);
+constexpr uint32_t kRankChunkMultiple = 512;
+// occ + cnt (per-word occupied counts, scratch) on the device, pre = exclusive scan of cnt
+hipError_t launch_rank_index(const int64_t *slots, uint64_t n_slots, uint64_t *occ, uint32_t *pre, uint32_t *cnt,
+                             hipStream_t s);
+hipError_t launch_rank_compact_keys(const int64_t *slots, uint64_t n_slots, const uint64_t *occ, const uint32_t *pre,
+                                    int64_t *ckeys, hipStream_t s);
+size_t rank_workspace(uint64_t positions, uint32_t parts);
+hipError_t launch_probe_rank(const ProbeParams &p, const RankIndex &ix, void *ws, hipStream_t s);
 hipError_t launch_segment_chunk_counts(const uint64_t *counts, uint32_t n_segs, uint64_t seg_cap, uint32_t chunk,
                                        uint32_t *out, uint32_t *status, hipStream_t s);
 hipError_t launch_partition(const int64_t *keys, uint64_t n, uint32_t parts, uint64_t row_base, int64_t *out_keys,

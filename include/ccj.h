@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CCJ_ABI_VERSION 7  /* 7: CCJ_PART_ROWS; keys of cap == chunk partitioned probes go to out_payload */
+#define CCJ_ABI_VERSION 8  /* 8: CCJ_PART_RANK (LDS window index walk); 7: CCJ_PART_ROWS */
 
 enum ccj_status {
   CCJ_OK = 0,
@@ -201,6 +201,16 @@ int ccj_probe_visits(const ccj_table *table, const int64_t *d_keys, const uint32
  * only compacts the chunks where some row missed.  Without the flag, when cap == chunk the keys
  * still go to out_payload (the workspace's key region is then left untouched). */
 #define CCJ_PART_ROWS 2u
+/* flags & CCJ_PART_RANK: the RANK WALK instead of the slot-array walk (LP tables of distinct keys,
+ * cap == chunk, chunk a multiple of 512, windows of <= 2^19 slots; otherwise the flag is ignored).
+ * Each partition's window index (occupancy bitmap + occupied-slot rank per 128 slots, built with
+ * the table) is held in LDS, so a row's run [home, first empty) costs no memory read and its
+ * candidate keys come from the table's compact key array (occupied slots' keys in slot order).
+ * Same matches, same per-chunk row order.  Measured at C2: fewer L2 requests per row
+ * (1.11 vs 1.22), half the HBM lines and 22 % lower L2 latency, but one 768-thread workgroup per
+ * CU (the 80 KiB index) keeps half as many requests in flight: 9.9 ms against 7.4 for the slot
+ * walk.  Not the default. */
+#define CCJ_PART_RANK 4u
 uint64_t ccj_probe_partitioned_positions(const ccj_table *table, uint64_t n_rows, uint32_t chunk);
 size_t ccj_probe_partitioned_workspace_size(const ccj_table *table, uint64_t n_rows, uint32_t chunk);
 int ccj_probe_partitioned(const ccj_table *table, const ccj_probe_args *args, uint32_t flags,
