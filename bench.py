@@ -526,7 +526,7 @@ def main():
         matches, l2 = ccj.result_checksum(res0, chunk, row_base=rank * n_probe, stream=stream)
     # the other paths, timed the same way (reported beside the headline)
     others = [] if c5 or args.no_other else [q for q in ("ordered", "chunk", "partitioned") if q != args.path]
-    if args.path == "partitioned" and not c5:
+    if args.path == "partitioned" and not c5 and not args.no_other:
         others.append("rank")  # A/B: the rank walk on the same split, same run
     other_runs = {}
     for other in others:
