@@ -63,6 +63,7 @@ EXPORTS = ["ccj_last_error", "ccj_abi_version", "ccj_device_init", "ccj_table_bu
            "ccj_probe", "ccj_gen_uniform_keys", "ccj_probe_cost", "ccj_result_checksum",
            "ccj_compact_workspace_size", "ccj_compact", "ccj_partition_workspace_size", "ccj_partition_by_owner",
            "ccj_result_checksum_mapped", "ccj_gen_reference_keys", "ccj_table_set_payload",
+           "ccj_table_build_rank_index",
            "ccj_probe_partitioned_workspace_size", "ccj_probe_partitioned", "ccj_probe_partitioned_positions",
            "ccj_pipeline_create",
            "ccj_pipeline_run", "ccj_pipeline_free", "ccj_pipeline_checksum", "ccj_partition_by_owner_fixed",
@@ -103,6 +104,7 @@ def lib():
         L.ccj_table_get_info.argtypes = [vp, C.POINTER(TableInfo)]
         L.ccj_table_free.argtypes = [vp]
         L.ccj_table_set_payload.argtypes = [vp, vp, C.c_uint32, vp]
+        L.ccj_table_build_rank_index.argtypes = [vp, vp]
         L.ccj_probe_partitioned_workspace_size.restype = C.c_size_t
         L.ccj_probe_partitioned_workspace_size.argtypes = [vp, u64, C.c_uint32]
         L.ccj_probe_partitioned_positions.restype = u64
@@ -263,6 +265,10 @@ class Table:
         check(lib().ccj_table_set_payload(self._h, _ptr(d_payload), n_cols, _stream(stream)), "ccj_table_set_payload")
         self.n_payload_cols = n_cols
 
+    def build_rank_index(self, stream=None):
+        """The rank walk's window index (ccj_table_build_rank_index; CCJ_PART_RANK needs it)."""
+        check(lib().ccj_table_build_rank_index(self._h, _stream(stream)), "ccj_table_build_rank_index")
+
     def probe_cost(self, keys, stream=None):
         """(table words examined, matches) over a key column — roofline accounting."""
         import torch
@@ -321,6 +327,8 @@ class Table:
         match instead of its position (result_checksum(out, 0) then needs no row map).
         rank=True (CCJ_PART_RANK): the rank walk where it applies (LP, distinct keys, cap == chunk)."""
         n = keys.numel()
+        if rank and part is None:
+            self.build_rank_index(stream)  # before the workspace is sized (it grows with the index)
         if part is None:
             part = self.alloc_partitioned(n, chunk)
         if part["n_rows"] != n or part["chunk"] != chunk:

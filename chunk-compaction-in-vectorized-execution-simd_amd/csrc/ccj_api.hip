@@ -117,10 +117,16 @@ int upload(void **dst, const void *src, size_t bytes, const char *what) {
 // The rank walk's window index (ccj_rank.hip), built on the device from the finished slot array for
 // tables the partitioned probe splits into windows the LDS can hold (<= 2^19 slots).  Build-time
 // work like the table itself (main.cpp:62-68 times neither).  Without it the slot-array walk runs.
-int build_rank_index(ccj_table *t, hipStream_t s) {
+bool rank_index_applies(const ccj_table *t) {
   const ccj::SlotPlan pl = ccj::slot_plan(t->info.size, CCJ_TABLE_LP);
   const uint64_t size = t->info.size;
-  if (pl.lo_bits == 0 || !ccj::rank_walk_fits(pl.window_bits) || size % 128 || size > (1ull << 32)) return CCJ_OK;
+  return t->info.kind == CCJ_TABLE_LP && pl.lo_bits && ccj::rank_walk_fits(pl.window_bits) && size % 128 == 0 &&
+         size <= (1ull << 32);
+}
+int build_rank_index(ccj_table *t, hipStream_t s) {
+  if (!rank_index_applies(t) || t->d_ckeys) return CCJ_OK;
+  const ccj::SlotPlan pl = ccj::slot_plan(t->info.size, CCJ_TABLE_LP);
+  const uint64_t size = t->info.size;
   const uint64_t words = size / 64;
   uint32_t *cnt = nullptr;
   hipError_t e = hipMalloc((void **)&t->d_occ, words * 8);
@@ -178,12 +184,6 @@ int build_lp_host(const int64_t *keys, uint64_t n, ccj_table **out) {
   t->d_row = (uint32_t *)d;
   t->info.d_table = t->d_table;
   (void)hipGetDevice(&t->device);
-  rc = build_rank_index(t.get(), nullptr);
-  if (rc) {
-    (void)hipFree(t->d_table);
-    (void)hipFree(t->d_row);
-    return rc;
-  }
   *out = t.release();
   return CCJ_OK;
 }
@@ -344,10 +344,6 @@ int build_lp_device(const int64_t *d_keys, uint64_t n, hipStream_t s, uint64_t k
   t->info.max_dup = dup ? dup : 1;
   t->info.d_table = t->d_table;
   (void)hipGetDevice(&t->device);
-  if (int rc = build_rank_index(t.get(), s)) {
-    cleanup();
-    return rc;
-  }
   *out = t.release();
   return CCJ_OK;
 }
@@ -458,6 +454,11 @@ int ccj_table_set_payload(ccj_table *t, const int64_t *d_payload, uint32_t n_col
   t->d_pay = (int64_t *)d;
   t->n_pay = n_cols;
   return CCJ_OK;
+}
+
+int ccj_table_build_rank_index(ccj_table *t, ccj_stream stream) {
+  if (!t) return fail(CCJ_ERR_INVALID, "ccj_table_build_rank_index: null table");
+  return build_rank_index(t, (hipStream_t)stream);
 }
 
 int ccj_table_free(ccj_table *t) {
@@ -633,6 +634,8 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   const bool rank = !exact && L.pl.lo_bits && L.ovf_base && t->d_ckeys && t->rank_wbits == L.pl.window_bits &&
                     p.keys_in_out && t->info.max_dup <= 1 && p.n_pay == 0 && !p.out_pos && !p.out_rounds &&
                     a->chunk % ccj::kRankChunkMultiple == 0 && ((flags & CCJ_PART_RANK) || ccj_tune_int("CCJ_RANK", 0));
+  if ((flags & CCJ_PART_RANK) && !t->d_ckeys && rank_index_applies(t))
+    return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: CCJ_PART_RANK needs ccj_table_build_rank_index first");
   if (rank) {
     const ccj::RankIndex ix{t->d_occ, t->d_pre, t->d_ckeys, t->rank_wbits};
     const size_t fixed = align256(((uint64_t)L.parts * 8 + 1) * 4);

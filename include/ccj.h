@@ -103,6 +103,12 @@ int ccj_table_get_info(const ccj_table *table, ccj_table_info *info);
  * extension the BASELINE config asks for. */
 int ccj_table_set_payload(ccj_table *table, const int64_t *d_payload, uint32_t n_cols, ccj_stream stream);
 int ccj_table_free(ccj_table *table);
+/* The rank walk's window index (CCJ_PART_RANK): occupancy bits, occupied-slot ranks per 128 slots
+ * and the occupied slots' keys in slot order, built on the device from the finished LP table
+ * (size/8 + size/32 + n_keys*8 bytes: 560 MiB at C2).  A no-op for tables the rank walk does not
+ * serve (chaining, one window, windows > 2^19 slots).  Build-time work, like the table.  Call it
+ * before sizing the partitioned workspace (ccj_probe_partitioned_workspace_size grows with it). */
+int ccj_table_build_rank_index(ccj_table *table, ccj_stream stream);
 
 /* ---- probe -------------------------------------------------------------------------------- */
 /* Batched form of Probe + the whole `while (HasNext()) Next(...)` loop
@@ -209,7 +215,7 @@ int ccj_probe_visits(const ccj_table *table, const int64_t *d_keys, const uint32
  * Same matches, same per-chunk row order.  Measured at C2: fewer L2 requests per row
  * (1.11 vs 1.22), half the HBM lines and 22 % lower L2 latency, but one 768-thread workgroup per
  * CU (the 80 KiB index) keeps half as many requests in flight: 9.9 ms against 7.4 for the slot
- * walk.  Not the default. */
+ * walk.  Not the default.  Needs ccj_table_build_rank_index (CCJ_ERR_INVALID without it). */
 #define CCJ_PART_RANK 4u
 uint64_t ccj_probe_partitioned_positions(const ccj_table *table, uint64_t n_rows, uint32_t chunk);
 size_t ccj_probe_partitioned_workspace_size(const ccj_table *table, uint64_t n_rows, uint32_t chunk);

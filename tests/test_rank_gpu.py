@@ -142,3 +142,14 @@ def test_rank_walk_segmented_counts():
     want = (int(live.sum()), O.l2_sum(pos[live].astype(np.uint64), keys_h[live]))
     assert ccj.result_checksum(out, chunk, row_map=out["row_map"].to(torch.int64)) == want
     table.free()
+
+
+def test_rank_walk_needs_the_index():
+    """CCJ_PART_RANK on a table without its window index is refused (the index is opt-in, built by
+    ccj_table_build_rank_index), not silently replaced by the slot walk."""
+    table = ccj.Table.reference(ccj.LP, 1 << 18, 1, ccj.LAYOUT_DEVICE)
+    keys = ccj.gen_uniform_keys(1 << 20, 3, 1 << 18)
+    part = table.alloc_partitioned(keys.numel(), 2048)
+    with pytest.raises(ccj.CCJError):
+        table.probe_partitioned(keys, 2048, part=part, rank=True)
+    table.free()
