@@ -1482,12 +1482,15 @@ __device__ __forceinline__ bool walk_emit_wg(const ProbeParams &p, WalkShared<tr
 // word W = mm | L << 26 (bit r of mm: the row matches in round r; L: occupied slots walked = its
 // rounds, the reference's Next calls for it; L > 26: bit 31 | L, the chunk re-walks round by
 // round), written to p.out_w at the row's position; no emit.
-template <int R, bool HOME, int NW = 4, bool MM = false>
+// LN: lanes per row (2: 32-byte windows, 4: 64-byte windows; 16 bytes per lane either way).
+template <int R, bool HOME, int NW = 4, bool MM = false, int LN = 2>
 __global__ __launch_bounds__(kWave * NW) void probe_walk(ProbeParams p) {
   constexpr uint32_t kWaveRows = kMaxChunk / NW;  // rows per wave
   __shared__ WalkShared<HOME> sm;
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
-  const uint32_t sub = lane & 1u;
+  constexpr uint32_t kWin = 2 * LN;  // slots per window
+  constexpr uint32_t kRowsPer = kWave / LN;  // rows per wave instruction
+  const uint32_t sub = lane & (LN - 1);
   unsigned long long t0, t1, t2;
   uint32_t steps = 0;
   CCJ_STAMP(t0);
@@ -1502,8 +1505,8 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk(ProbeParams p) {
   }
   walk_stage<kWaveRows, HOME>(p, sm, base, w0, wend, lane);
   CCJ_STAMP(t1);
-  const uint32_t last_start = p.mask - 3u;  // table size - 4 (size >= 16)
-  const uint32_t pair = lane >> 1;
+  const uint32_t last_start = p.mask - (kWin - 1);  // table size - window (size >= 16)
+  const uint32_t pair = lane / LN;
   int64_t key[R];
   uint32_t row[R], cur[R], cnt[R], r0[R];
   uint32_t need = 0, lane_rounds = 0;
@@ -1521,9 +1524,9 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk(ProbeParams p) {
   for (int k = 0; k < R; ++k) {
     key[k] = 0;
     cur[k] = 0;
-    start(k, w0 + (uint32_t)k * (kWave / 2) + pair);
+    start(k, w0 + (uint32_t)k * kRowsPer + pair);
   }
-  uint32_t next = w0 + (uint32_t)R * (kWave / 2);  // wave-uniform: the wave's next unwalked row
+  uint32_t next = w0 + (uint32_t)R * kRowsPer;  // wave-uniform: the wave's next unwalked row
   while (__ballot(need != 0u) != 0ull) {
     ++steps;
     int64_t v0[R], v1[R];
@@ -1531,7 +1534,7 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk(ProbeParams p) {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       uint32_t s = cur[k] < last_start ? cur[k] : last_start;
-      const uint32_t lim = (s & ~15u) + 12u;  // the window ends at its 128-byte line
+      const uint32_t lim = (s & ~15u) + (16u - kWin);  // the window ends at its 128-byte line
       s = s < lim ? s : lim;
       st[k] = s;
       // Unconditional loads: a load under `if (need)` made the compiler wait for each row's load
@@ -1554,13 +1557,14 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk(ProbeParams p) {
     for (int k = 0; k < R; ++k) {
       uint32_t e = ((v0[k] == -1) ? 1u : 0u) | ((v1[k] == -1) ? 2u : 0u);
       uint32_t m = ((v0[k] == key[k]) ? 1u : 0u) | ((v1[k] == key[k]) ? 2u : 0u);
-      uint32_t em = (e | m << 4) << (2 * sub);
+      uint32_t em = (e | m << kWin) << (2 * sub);
       em |= (uint32_t)__builtin_amdgcn_mov_dpp((int)em, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+      if (LN == 4) em |= (uint32_t)__builtin_amdgcn_mov_dpp((int)em, 0x4E, 0xF, 0xF, false);  // quad_perm 2,3,0,1
       if ((need >> k) & 1u) {
         const uint32_t off = cur[k] - st[k];
-        const uint32_t ee = (em & 15u) >> off;
-        const uint32_t f = (uint32_t)__builtin_ctz(ee | (16u >> off));  // run end (or window end) past cur
-        const uint32_t hits = ((em >> 4) >> off) & ((1u << f) - 1u);
+        const uint32_t ee = (em & ((1u << kWin) - 1u)) >> off;
+        const uint32_t f = (uint32_t)__builtin_ctz(ee | ((1u << kWin) >> off));  // run end (or window end) past cur
+        const uint32_t hits = ((em >> kWin) >> off) & ((1u << f) - 1u);
         if (MM) cnt[k] |= r0[k] < kMmRounds ? hits << r0[k] : 0u;  // rounds >= 26 end as long rows
         else cnt[k] += (uint32_t)__builtin_popcount(hits);
         if (ee) {
@@ -1569,8 +1573,8 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk(ProbeParams p) {
           if (MM) cnt[k] = r <= kMmRounds ? (cnt[k] & ((1u << kMmRounds) - 1u)) | r << kMmRounds : kMmLong | r;
           done |= 1u << k;
         } else {
-          r0[k] += 4u - off;
-          cur[k] = (st[k] + 4u) & p.mask;
+          r0[k] += kWin - off;
+          cur[k] = (st[k] + kWin) & p.mask;
         }
       }
     }
@@ -1584,7 +1588,7 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk(ProbeParams p) {
       tot += (uint32_t)__popcll(bm) << b;
     }
     if (tot) {
-      pre = (uint32_t)__builtin_amdgcn_mov_dpp((int)pre, 0xA0, 0xF, 0xF, false);  // the pair's even lane's
+      pre = (uint32_t)__builtin_amdgcn_mov_dpp((int)pre, LN == 4 ? 0x00 : 0xA0, 0xF, 0xF, false);  // the row's first lane's
       uint32_t rb = next + pre;
 #pragma unroll
       for (int k = 0; k < R; ++k) {
@@ -1848,7 +1852,13 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
   if (p.out_pos) {
     hipLaunchKernelGGL((probe_win<3>), g, b, 0, s, p);  // C5: match positions too
   } else {
-    hipLaunchKernelGGL((probe_walk<3, true>), g, b, 0, s, p);
+    // 64-byte windows (4 lanes per row: 1.109 instead of 1.169 window reads per row in a host
+    // simulation of the C2 table) measured slower, same box: 13.42 / 14.35 ms per C2 step against
+    // 13.24 / 13.22 (half the rows per load instruction); tuning build only (CCJ_WALK_LANES=4)
+    if (ccj_tune_int("CCJ_WALK_LANES", 2) == 4)
+      hipLaunchKernelGGL((probe_walk<3, true, 4, false, 4>), g, b, 0, s, p);
+    else
+      hipLaunchKernelGGL((probe_walk<3, true>), g, b, 0, s, p);
   }
   return hipGetLastError();
 }
