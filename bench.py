@@ -193,8 +193,6 @@ def bench_c3(args, dev, stream):
         table = ccj.Table.reference(ccj.CHAIN, n_build, 1, ccj.LAYOUT_DEVICE, stream=stream)
         keys = ccj.gen_c3_keys(n_probe, SEED, n_build, 1, stream=stream)
         if part_mode:  # bucket-range split + L2-resident chain walk; one compactor input per chunk
-            if not c5 and not args.no_other:  # the rank walk is timed beside the headline (A/B)
-                table.build_rank_index(stream=stream)
             part = table.alloc_partitioned(n_probe, chunk)
             out = table.alloc_outputs(part["positions"], chunk, rounds=False)
             out["max_rounds"] = 1

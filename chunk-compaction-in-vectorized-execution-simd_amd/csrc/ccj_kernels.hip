@@ -1152,11 +1152,11 @@ __global__ __launch_bounds__(kFlatThreads) void probe_chain_win(ProbeParams p) {
   while (__ballot(need != 0u) != 0ull) {
     longlong2 v[R];
 #pragma unroll
-    for (int k = 0; k < R; ++k) {
-      if ((need >> k) & 1u) {
-        v[k] = ((fresh >> k) & 1u) ? p.bucket[cur[k]]
-                                   : *reinterpret_cast<const longlong2 *>(p.table + (cur[k] & ~1u));
-      }
+    for (int k = 0; k < R; ++k) {  // unconditional (an idle row reads bucket 0): no wait per load
+      const bool nd = (need >> k) & 1u, fr = (fresh >> k) & 1u;
+      const longlong2 *src = nd && !fr ? reinterpret_cast<const longlong2 *>(p.table + (cur[k] & ~1u))
+                                       : p.bucket + (nd ? cur[k] : 0u);
+      v[k] = *src;
     }
     uint32_t hits[R], n = 0, done = 0;
 #pragma unroll
@@ -1655,14 +1655,32 @@ __global__ __launch_bounds__(kBlock) void emit_ordered(ProbeParams p) {
   int64_t key[kQ];
   uint32_t w[kQ];
 #pragma unroll
-  for (int q = 0; q < kQ; ++q) {  // every load in flight first
+  for (int q = 0; q < kQ; ++q) {  // every load in flight first: unconditional (row 0 past the
+    // count), since a load under `if` made the compiler wait for each before the next
     const uint32_t i = (uint32_t)q * kBlock + tid;
-    key[q] = 0;
-    w[q] = 0;
-    if (i < count) {
-      key[q] = __builtin_nontemporal_load(p.keys + base + i);
-      w[q] = p.w16 ? round_word32(__builtin_nontemporal_load((const uint16_t *)p.in_w + base + i))
-                   : __builtin_nontemporal_load(p.in_w + base + i);
+    key[q] = __builtin_nontemporal_load(p.keys + base + (i < count ? i : 0u));
+  }
+  if (p.w16) {  // (the width branch outside the loads: one inside made each load wait for its use)
+    uint16_t h[kQ];
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      const uint32_t i = (uint32_t)q * kBlock + tid;
+      h[q] = __builtin_nontemporal_load((const uint16_t *)p.in_w + base + (i < count ? i : 0u));
+    }
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) w[q] = round_word32(h[q]);
+  } else {
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      const uint32_t i = (uint32_t)q * kBlock + tid;
+      w[q] = __builtin_nontemporal_load(p.in_w + base + (i < count ? i : 0u));
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) {
+    if ((uint32_t)q * kBlock + tid >= count) {
+      key[q] = 0;
+      w[q] = 0;
     }
   }
   for (uint32_t q = tid; q < kMaxFastRounds * 32; q += kBlock) s_off[q] = 0u;
@@ -1813,20 +1831,39 @@ __global__ __launch_bounds__(kUnsplitThreads) void unsplit_words(const uint2 *ru
   __syncthreads();
   const uint32_t total = s_loc[parts];
   bool bad = false;
-  for (uint32_t j = tid; j < total; j += kUnsplitThreads) {
-    uint32_t lo = 0, hi = parts;  // the last d with s_loc[d] <= j
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (s_loc[mid] <= j) lo = mid;
-      else hi = mid;
+  // kU entries per thread per pass, all their loads in flight together (a load under `if`, or one
+  // waiting on the previous entry's, made each entry two dependent round trips)
+  constexpr uint32_t kU = 4;
+  for (uint32_t j0 = tid; j0 < total; j0 += kU * kUnsplitThreads) {
+    uint64_t pos[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      uint32_t j = j0 + u * kUnsplitThreads;
+      j = j < total ? j : total - 1;  // (a repeat of the last entry: the same word to the same row)
+      uint32_t lo = 0, hi = parts;    // the last d with s_loc[d] <= j
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_loc[mid] <= j) lo = mid;
+        else hi = mid;
+      }
+      const uint32_t o = j - s_loc[lo];
+      const uint2 rr = s_run[lo];
+      const uint32_t lim = rr.y & 0xFFFFu;
+      pos[u] = o < lim ? (uint64_t)rr.x + o : (uint64_t)ovf_runs[t * parts + lo] + (o - lim);
     }
-    const uint32_t o = j - s_loc[lo];
-    const uint2 rr = s_run[lo];
-    const uint32_t lim = rr.y & 0xFFFFu;
-    const uint64_t pos = o < lim ? (uint64_t)rr.x + o : (uint64_t)ovf_runs[t * parts + lo] + (o - lim);
-    const uint64_t local = (uint64_t)row_map[pos] - t0;
-    if (local < tn) s_img[local] = w_pos[pos];
-    else bad = true;
+    uint32_t rm[kU];
+    W wv[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      rm[u] = row_map[pos[u]];
+      wv[u] = w_pos[pos[u]];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint64_t local = (uint64_t)rm[u] - t0;
+      if (local < tn) s_img[local] = wv[u];
+      else bad = true;
+    }
   }
   if (bad && status) atomicOr(status, CCJ_FLAG_BAD_INPUT);
   __syncthreads();
@@ -1930,12 +1967,19 @@ __global__ __launch_bounds__(256) void gather_payload_quad(GatherParams g) {
   const uint32_t q = threadIdx.x & 3u, r0 = threadIdx.x >> 2;  // 64 rows per block step
   int64_t *c0 = s_cols[2 * q], *c1 = s_cols[2 * q + 1];
   for (uint32_t base = 0; base < n; base += 64 * U) {
-    longlong2 v[U];
+    // the U positions, then the U rows: each phase's loads in flight together (loads under `if`
+    // made the compiler wait for every position and row before the next)
+    uint32_t ps[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t j = base + u * 64 + r0;
-      if (j < n) v[u] = reinterpret_cast<const longlong2 *>(g.pay + (uint64_t)(g.pos[ob + j] >> g.shift) * g.stride)[q];
+      ps[u] = g.pos[ob + (j < n ? j : 0u)];
     }
+    __builtin_amdgcn_sched_barrier(0);  // every position load issued before the first row load
+    longlong2 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = reinterpret_cast<const longlong2 *>(g.pay + (uint64_t)(ps[u] >> g.shift) * g.stride)[q];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t j = base + u * 64 + r0;

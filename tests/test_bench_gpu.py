@@ -1,0 +1,63 @@
+"""bench.py end to end at small sizes, one process per workload: the JSON line of the driver's
+contract for every workload and path (C2 partitioned with the rank-walk A/B and the reference-order
+paths beside it, C2 ordered, C3 with compaction, C5 with payload columns, the main.cpp pipeline),
+with the bench's own full-size-style parity checks green.  Catches a broken bench path before the
+driver's round-end run does."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SMALL = ["--steps", "2", "--warmup", "1", "--no-cpu", "--n-build", str(1 << 21), "--n-probe", str(1 << 24)]
+
+
+def run_bench(*extra):
+    p = subprocess.run([sys.executable, "bench.py", *SMALL, *extra], cwd=ROOT, capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["value"] > 0 and line["n_gpus"] == 1 and line["higher_is_better"]
+    assert "roofline" in line and line["roofline"]["frac"] > 0
+    return line
+
+
+def test_bench_c2_with_other_paths():
+    line = run_bench()
+    par = line["parity"]
+    assert par["status_flags"] == 0 and par["l1_ok"] and par["l2_ok"]
+    paths = {o["path"]: o for o in line["other_paths"]}
+    assert set(paths) == {"ordered", "chunk", "rank"}
+    for o in paths.values():
+        assert o["check"]["status_flags"] == 0 and o["check"]["l1_ok"] and o["check"]["l2_ok"]
+    assert paths["ordered"]["check"]["equals_chunk_path_l3"]
+
+
+def test_bench_c2_ordered_headline():
+    line = run_bench("--path", "ordered", "--no-other")
+    assert line["path"] == "ordered" and line["parity"]["l1_ok"] and line["parity"]["l2_ok"]
+
+
+def test_bench_c3():
+    line = run_bench("--workload", "c3")
+    par = line["parity"]
+    assert par["status_flags"] == 0 and par["l1_ok"] and par["l2_ok"] and par["compaction_keeps_all"]
+
+
+def test_bench_c5():
+    line = run_bench("--workload", "c5")
+    par = line["parity"]
+    assert par["status_flags"] == 0 and par["l1_ok"] and par["l2_ok"] and par["payload_cols_ok"]
+
+
+def test_bench_pipeline():
+    p = subprocess.run([sys.executable, "bench.py", "--workload", "pipeline", "--steps", "2", "--warmup", "1",
+                        "--no-cpu", "--pipe-lhs", "2000000", "--pipe-rhs", "200000"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["value"] > 0
