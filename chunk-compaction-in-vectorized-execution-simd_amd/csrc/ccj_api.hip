@@ -777,7 +777,8 @@ int ccj_probe_ordered(const ccj_table *t, const ccj_probe_args *a, void *ws, siz
   q.w16 = w16;
   HIP_TRY(ccj::launch_ordered_walk(q, s), "ordered walk");
   // 3. the words back into row order, one split tile per workgroup
-  HIP_TRY(ccj::launch_unsplit_words(runs, ovf_runs, row_map, w_pos, w_row, a->n_rows, L.parts, O.tile, a->status, s,
+  HIP_TRY(ccj::launch_unsplit_words(runs, ovf_runs, reinterpret_cast<const uint16_t *>(row_map), w_pos, w_row,
+                                    a->n_rows, L.parts, O.tile, a->status, s,
                                     w16 != 0),
           "unsplit");
   // 4. per chunk: the reference's per-Next stream from its rows' words (probe_chunks' emit)

@@ -115,7 +115,7 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s);
 // round word at its position (p.out_w); the words back into row order, one split tile per
 // workgroup; the reference-order emit of each chunk from its rows' words (p.in_w).
 hipError_t launch_ordered_walk(const ProbeParams &p, hipStream_t s);
-hipError_t launch_unsplit_words(const uint2 *runs, const uint32_t *ovf_runs, const uint32_t *row_map,
+hipError_t launch_unsplit_words(const uint2 *runs, const uint32_t *ovf_runs, const uint16_t *row_loc,
                                 const void *w_pos, void *w_row, uint64_t n, uint32_t parts, uint32_t tile,
                                 uint32_t *status, hipStream_t s, bool w16);
 hipError_t launch_ordered_emit(const ProbeParams &p, hipStream_t s);
@@ -180,6 +180,7 @@ uint64_t slot_seg_cap(uint64_t n, const SlotPlan &pl, uint32_t chunk);
 // counts: live rows per input chunk.  runs (optional; the ordered probe): per (tile, partition)
 // {segment position of the run, segment length | overflow-area length << 16}; ovf_runs: the
 // overflow-area position where that length is non-zero.  Tiles are slot_split_tile_keys(parts, runs) keys.
+// With runs, out_rows receives each position's row INSIDE ITS TILE as uint16_t (the unsplit's input).
 hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPlan &pl, uint64_t cap,
                                    uint64_t ovf_base, uint64_t ovf_cap, uint32_t *cursors, int64_t *out_keys,
                                    uint32_t *out_rows, uint32_t *status, hipStream_t s,

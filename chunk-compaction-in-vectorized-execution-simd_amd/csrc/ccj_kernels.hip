@@ -1792,9 +1792,10 @@ __global__ __launch_bounds__(kBlock) void emit_ordered(ProbeParams p) {
 // Ordered probe, step 3: the round words of one split tile back into row order.  The split
 // recorded where each (tile, partition) run went (runs / ovf_runs); the tile's runs are numbered
 // consecutively (an exclusive scan of their lengths), every thread takes entries j = tid, tid +
-// 1024, ... (consecutive positions inside a run: coalesced reads of the row map and the words),
+// 1024, ... (consecutive positions inside a run: coalesced reads of the rows and the words),
 // finds j's partition by a binary search over the scan, and drops the word into an LDS image of
-// the tile at row - t0; the image is written out whole.  Rows that were not live stay 0.
+// the tile at the row the split recorded there (16 bits: the row inside its tile); the image is
+// written out whole.  Rows that were not live stay 0.
 // C2: 4.6 ms, 22.5 GiB of DRAM traffic (the runs' partial lines: ~2x the 8 B read per row) =
 // 5.2 TB/s.  One binary search per thread over kPer consecutive entries (each load instruction then
 // spans ~kPer * 64 entries) measured 13.6 ms; tiles read in the split's XCD order 4.66 ms.
@@ -1803,7 +1804,7 @@ constexpr uint32_t kUnsplitMaxTile = 13u * kUnsplitThreads;  // the split's larg
 
 template <typename W>
 __global__ __launch_bounds__(kUnsplitThreads) void unsplit_words(const uint2 *runs, const uint32_t *ovf_runs,
-                                                                 const uint32_t *row_map, const W *w_pos,
+                                                                 const uint16_t *row_loc, const W *w_pos,
                                                                  W *w_row, uint64_t n, uint32_t parts,
                                                                  uint32_t tile, uint32_t *status) {
   __shared__ W s_img[kUnsplitMaxTile];
@@ -1853,13 +1854,12 @@ __global__ __launch_bounds__(kUnsplitThreads) void unsplit_words(const uint2 *ru
     W wv[kU];
 #pragma unroll
     for (uint32_t u = 0; u < kU; ++u) {
-      rm[u] = row_map[pos[u]];
+      rm[u] = row_loc[pos[u]];
       wv[u] = w_pos[pos[u]];
     }
 #pragma unroll
     for (uint32_t u = 0; u < kU; ++u) {
-      const uint64_t local = (uint64_t)rm[u] - t0;
-      if (local < tn) s_img[local] = wv[u];
+      if (rm[u] < tn) s_img[rm[u]] = wv[u];
       else bad = true;
     }
   }
@@ -2031,7 +2031,7 @@ hipError_t launch_ordered_walk(const ProbeParams &p, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_unsplit_words(const uint2 *runs, const uint32_t *ovf_runs, const uint32_t *row_map,
+hipError_t launch_unsplit_words(const uint2 *runs, const uint32_t *ovf_runs, const uint16_t *row_loc,
                                 const void *w_pos, void *w_row, uint64_t n, uint32_t parts, uint32_t tile,
                                 uint32_t *status, hipStream_t s, bool w16) {
   if (n == 0) return hipSuccess;
@@ -2039,10 +2039,10 @@ hipError_t launch_unsplit_words(const uint2 *runs, const uint32_t *ovf_runs, con
   const uint64_t n_tiles = (n + tile - 1) / tile;
   if (w16)
     hipLaunchKernelGGL(unsplit_words<uint16_t>, dim3((unsigned)n_tiles), dim3(kUnsplitThreads), 0, s, runs, ovf_runs,
-                       row_map, (const uint16_t *)w_pos, (uint16_t *)w_row, n, parts, tile, status);
+                       row_loc, (const uint16_t *)w_pos, (uint16_t *)w_row, n, parts, tile, status);
   else
     hipLaunchKernelGGL(unsplit_words<uint32_t>, dim3((unsigned)n_tiles), dim3(kUnsplitThreads), 0, s, runs, ovf_runs,
-                       row_map, (const uint32_t *)w_pos, (uint32_t *)w_row, n, parts, tile, status);
+                       row_loc, (const uint32_t *)w_pos, (uint32_t *)w_row, n, parts, tile, status);
   return hipGetLastError();
 }
 

@@ -480,7 +480,10 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
       if ((o < lim || o - lim < s_olim[d]) && !CCJ_ABLATED(ablate, 0x10u)) {  // (0x10: timing only, no stores)
         const uint64_t dest = o < lim ? s_dst[d] + o : ovf_base + s_ovf[d] + (o - lim);
         out_k[dest] = k;  // plain stores: the L2 merges neighbouring runs' partial lines
-        out_r[dest] = row_base + (uint32_t)(t0 + (si & 0xFFFFu));  // (non-temporal stores measured the same)
+        if (runs)  // the ordered probe: the row inside its tile, 16 bits (the unsplit reads half the bytes)
+          reinterpret_cast<uint16_t *>(out_r)[dest] = (uint16_t)(si & 0xFFFFu);
+        else
+          out_r[dest] = row_base + (uint32_t)(t0 + (si & 0xFFFFu));  // (non-temporal stores measured the same)
       }
     }
     __syncthreads();
@@ -564,7 +567,10 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
       const bool act = have_prev && q < p_tl && q < rc.w;
       const uint64_t dest = q < rc.z ? (rc.x | (uint64_t)rc.y << 32) + q : oadj + q;
       *(act ? out_k + dest : sink_k) = k;
-      *(act ? out_r + dest : sink_r) = row_base + (uint32_t)(p_t0 + (si & 0xFFFFu));
+      if constexpr (RUNS)  // the ordered probe: the row inside its tile, 16 bits
+        *(act ? reinterpret_cast<uint16_t *>(out_r) + dest : reinterpret_cast<uint16_t *>(sink_r)) = (uint16_t)(si & 0xFFFFu);
+      else
+        *(act ? out_r + dest : sink_r) = row_base + (uint32_t)(p_t0 + (si & 0xFFFFu));
       __builtin_amdgcn_sched_barrier(0);  // keep the LDS reads of later entries below (registers)
     }
   };
