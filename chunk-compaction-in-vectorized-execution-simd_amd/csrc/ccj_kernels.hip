@@ -1639,6 +1639,9 @@ __global__ __launch_bounds__(kBlock) void emit_ordered(ProbeParams p) {
   constexpr int kQ = kMaxChunk / kBlock;  // 8 rows per thread
   __shared__ uint32_t s_off[kMaxFastRounds * 32];
   __shared__ uint32_t s_red[3 * kChunkWaves];
+  // the chunk's output in its final (round-major) order, written out with whole 16-byte stores
+  __shared__ __attribute__((aligned(16))) uint32_t s_osel[kMaxChunk];
+  __shared__ __attribute__((aligned(16))) int64_t s_opay[kMaxChunk];
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   const uint64_t c = blockIdx.x;
   const uint64_t base = c * p.chunk;
@@ -1757,7 +1760,11 @@ __global__ __launch_bounds__(kBlock) void emit_ordered(ProbeParams p) {
       }
       if (rounds > p.max_rounds) flags |= CCJ_FLAG_ROUND_OVERFLOW;
     }
-    // Emit: group j's matches of round r go to s_off[r][j] + their ballot prefix.
+    // Emit: group j's matches of round r go to s_off[r][j] + their ballot prefix — into the LDS
+    // image of the chunk's output when it fits (every chunk of a distinct-key table), then out with
+    // 16-byte stores (per (round, group) stores left most lanes of each store instruction idle);
+    // otherwise straight to memory.
+    const bool img = total <= kMaxChunk && total <= p.cap && p.cap % 4 == 0 && !CCJ_ABLATED(p.ablate, 1u);
 #pragma unroll
     for (int q = 0; q < kQ; ++q) {
       const uint32_t j = (uint32_t)q * kChunkWaves + wave;
@@ -1769,11 +1776,32 @@ __global__ __launch_bounds__(kBlock) void emit_ordered(ProbeParams p) {
           const uint64_t mb = __ballot(bit);
           if (bit && !CCJ_ABLATED(p.ablate, 1u)) {
             const uint64_t o = (uint64_t)s_off[r * 32 + j] + lane_prefix(mb);
-            if (o < p.cap) {
+            if (img) {
+              s_osel[o] = i;
+              s_opay[o] = key[q];
+            } else if (o < p.cap) {
               __builtin_nontemporal_store(i, p.out_sel + obase + o);
               if (p.out_payload) __builtin_nontemporal_store(key[q], p.out_payload + obase + o);
             }
           }
+        }
+      }
+    }
+    if (img) {
+      __syncthreads();
+      const uint32_t tot = (uint32_t)total;
+      // a last partial group writes past the count inside the chunk's own cap region (no consumer
+      // reads there); the buffer records stop every store at the cap
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(p.out_sel + obase, (short)0, (int)(p.cap * 4), 0x00020000);
+      for (uint32_t g = tid; g * 4 < tot; g += kBlock) {
+        const u32x4 v = *reinterpret_cast<const u32x4 *>(&s_osel[4 * g]);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)(16 * g), 0, 2);
+      }
+      if (p.out_payload) {
+        const auto rp = __builtin_amdgcn_make_buffer_rsrc(p.out_payload + obase, (short)0, (int)(p.cap * 8), 0x00020000);
+        for (uint32_t g = tid; g * 2 < tot; g += kBlock) {
+          const u32x4 v = *reinterpret_cast<const u32x4 *>(&s_opay[2 * g]);
+          __builtin_amdgcn_raw_buffer_store_b128(v, rp, (int)(16 * g), 0, 2);
         }
       }
     }
