@@ -1131,11 +1131,30 @@ __device__ __forceinline__ void walk_chunk(const ProbeParams &p, uint64_t c, uin
   const uint32_t total = s_cnt;
   const uint32_t staged = total < kFlatStage ? total : kFlatStage;
   if (!(CCJ_ABLATED(p.ablate, 1u))) {
-    for (uint32_t o = tid; o < staged && o < p.cap; o += kFlatThreads) {
+    // 16-byte stores (4 sel / 2 payload / 4 position entries per lane; round 2d) for the whole
+    // groups when the chunk's region is 16-byte aligned (cap a multiple of 4), single entries else
+    typedef long long i64x2 __attribute__((ext_vector_type(2)));
+    const uint32_t lim = staged < p.cap ? staged : (uint32_t)p.cap;
+    const uint32_t vec = p.cap % 4 == 0 ? (lim & ~3u) : 0u;  // entries written by the vector stores
+    for (uint32_t g = tid; 4 * g < vec; g += kFlatThreads) {
+      const u32x4 sv = {s_sel[4 * g], s_sel[4 * g + 1], s_sel[4 * g + 2], s_sel[4 * g + 3]};
+      __builtin_nontemporal_store(sv, reinterpret_cast<u32x4 *>(p.out_sel + obase + 4 * g));
+      if (POS) {
+        const u32x4 pv = *reinterpret_cast<const u32x4 *>(&s_pos[4 * g]);
+        __builtin_nontemporal_store(pv, reinterpret_cast<u32x4 *>(p.out_pos + obase + 4 * g));
+      }
+    }
+    if (p.out_payload) {
+      for (uint32_t g = tid; 2 * g < vec; g += kFlatThreads) {
+        const i64x2 kv = {s_key[s_sel[2 * g]], s_key[s_sel[2 * g + 1]]};
+        __builtin_nontemporal_store(kv, reinterpret_cast<i64x2 *>(p.out_payload + obase + 2 * g));
+      }
+    }
+    for (uint32_t o = vec + tid; o < lim; o += kFlatThreads) {  // the rest, one entry per lane
       const uint32_t r = s_sel[o];
       __builtin_nontemporal_store(r, p.out_sel + obase + o);
-      if (p.out_payload) __builtin_nontemporal_store(s_key[r], p.out_payload + obase + o);
       if (POS) __builtin_nontemporal_store(s_pos[o], p.out_pos + obase + o);
+      if (p.out_payload) __builtin_nontemporal_store(s_key[r], p.out_payload + obase + o);
     }
   }
   if (tid == 0) {
@@ -1150,7 +1169,7 @@ __global__ __launch_bounds__(kFlatThreads) void probe_win(ProbeParams p) {
   __shared__ uint32_t s_cnt, s_rounds, s_next;
   __shared__ int64_t s_key[kMaxChunk];
   __shared__ uint16_t s_sel[kFlatStage];  // chunk rows fit 16 bits
-  __shared__ uint32_t s_pos[kFlatStage];  // every match's table position
+  __shared__ __attribute__((aligned(16))) uint32_t s_pos[kFlatStage];  // every match's table position
   uint64_t c = blockIdx.x;
   if (p.xcd_swizzle) {
     const uint64_t n8 = (p.swz_chunks ? p.swz_chunks : p.n_chunks) & ~7ull;
