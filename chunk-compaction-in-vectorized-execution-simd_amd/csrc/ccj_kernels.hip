@@ -1677,6 +1677,20 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk(ProbeParams p) {
   CCJ_STAMP(t2);
   if (MM) {  // the rows' round words, coalesced at their positions
     wave_lds_sync();
+    if (p.w16 && kWaveRows == 8 * kWave && w0 + kWaveRows <= p.chunk) {
+      // 8 words per lane in one 16-byte store (rows past wend write don't-care words inside the
+      // chunk's own positions, which no run points at; a wave whose rows pass the chunk's end —
+      // chunks under 2048 — stores word by word)
+      const uint32_t i0 = w0 + 8 * lane;
+      uint32_t h[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        h[t] = (uint32_t)round_word16((uint32_t)sm.hc[i0 + 2 * t]) |
+               (uint32_t)round_word16((uint32_t)sm.hc[i0 + 2 * t + 1]) << 16;
+      const u32x4 v = {h[0], h[1], h[2], h[3]};
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>((uint16_t *)p.out_w + base + i0));
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < (int)(kWaveRows / kWave); ++j) {
       const uint32_t i = w0 + (uint32_t)j * kWave + lane;
@@ -1908,7 +1922,7 @@ __global__ __launch_bounds__(kUnsplitThreads) void unsplit_words(const uint2 *ru
                                                                  const uint16_t *row_loc, const W *w_pos,
                                                                  W *w_row, uint64_t n, uint32_t parts,
                                                                  uint32_t tile, uint32_t *status) {
-  __shared__ W s_img[kUnsplitMaxTile];
+  __shared__ __attribute__((aligned(16))) W s_img[kUnsplitMaxTile];
   __shared__ uint32_t s_loc[kUnsplitThreads + 1];
   __shared__ uint2 s_run[kUnsplitThreads];
   __shared__ uint32_t s_wsum[kUnsplitThreads / 64];
@@ -1966,7 +1980,13 @@ __global__ __launch_bounds__(kUnsplitThreads) void unsplit_words(const uint2 *ru
   }
   if (bad && status) atomicOr(status, CCJ_FLAG_BAD_INPUT);
   __syncthreads();
-  for (uint32_t i = tid; i < tn; i += kUnsplitThreads) __builtin_nontemporal_store(s_img[i], w_row + t0 + i);
+  // 16-byte stores where the tile's rows start 16-byte aligned (round 2d), single words for the rest
+  constexpr uint32_t kPer16 = 16 / sizeof(W);
+  const uint32_t vec = ((t0 * sizeof(W)) % 16 == 0) ? tn / kPer16 * kPer16 : 0u;
+  for (uint32_t g = tid; g * kPer16 < vec; g += kUnsplitThreads)
+    __builtin_nontemporal_store(*reinterpret_cast<const u32x4 *>(&s_img[g * kPer16]),
+                                reinterpret_cast<u32x4 *>(w_row + t0 + g * kPer16));
+  for (uint32_t i = vec + tid; i < tn; i += kUnsplitThreads) __builtin_nontemporal_store(s_img[i], w_row + t0 + i);
 }
 
 hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
