@@ -315,13 +315,27 @@ __global__ __launch_bounds__(kBlock) void probe_chunks(ProbeParams p) {
 
   // Stage (Probe: linear_probing_ht.cpp:45-49 / chaining_ht.cpp:46-50): keys through sel -> LDS.
   // Thread (wave, lane) stages rows j = 4q + wave, i.e. exactly the rows its lane owns: act bit q.
+  // Every load in flight first (round 2d: under `if (i < count)` each row group's sel and key loads
+  // waited for the previous group's): clamped indexes, the results masked afterwards.
+  constexpr int kQs = (int)(kMaxChunk / kBlock);
   uint32_t act = 0;
-  for (uint32_t i = tid, q = 0; i < nj * kWave; i += kBlock, ++q) {
+  uint32_t rv[kQs];
+  int64_t kv[kQs];
+#pragma unroll
+  for (int q = 0; q < kQs; ++q) {
+    const uint32_t i = tid + (uint32_t)q * kBlock;
+    rv[q] = count ? phys_row(p, base, i < count ? i : 0u) : 0u;  // (no sel entry is read past the count)
+  }
+#pragma unroll
+  for (int q = 0; q < kQs; ++q) kv[q] = p.keys[base + (rv[q] < phys ? rv[q] : 0u)];
+#pragma unroll
+  for (int q = 0; q < kQs; ++q) {
+    const uint32_t i = tid + (uint32_t)q * kBlock;
+    if (i >= nj * kWave) break;
     int64_t k = 0;
     if (i < count) {
-      const uint32_t r = phys_row(p, base, i);
-      if (r < phys) {
-        k = p.keys[base + r];
+      if (rv[q] < phys) {
+        k = kv[q];
         act |= 1u << q;
       } else {
         flags |= CCJ_FLAG_BAD_INPUT;
