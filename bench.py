@@ -2,7 +2,9 @@
 """bench.py — probe throughput of the MI355X hash-join hot path (BASELINE.json metric).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c5|pipeline] [--no-cpu]
-  N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+  N > 1: `python bench.py --gpus N` starts its own N rank processes (torch.distributed.run as a child
+  process, before any GPU call in this one) and forwards rank 0's JSON line; launched by an outside
+  torchrun (WORLD_SIZE set) it runs as that rank directly.
 
 Step = one pass of the hot path over one batch:
   c2 (default; BASELINE configs[1]): LP table of 2^26 reference-generator keys (2 GiB, alpha 1/4),
@@ -63,9 +65,14 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5", "pipeline"])
     ap.add_argument("--batches", type=int, default=4, help="N > 1: exchange batches per step (pipelined)")
-    ap.add_argument("--group", type=int, default=16,
-                    help="N > 1: received batches per local probe (each local probe sweeps the whole table)")
-    ap.add_argument("--sharded", action="store_true", help="run the N > 1 protocol even at N = 1 (rehearsal)")
+    ap.add_argument("--group", type=int, default=None,
+                    help="N > 1: received batches per local probe (each local probe sweeps the whole table); "
+                         "default ccj_dist.GROUP")
+    ap.add_argument("--ops-module", default=None,
+                    help=argparse.SUPPRESS)  # tests only: a module whose make_ops() replaces the HIP ops (CPU, gloo)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"], help=argparse.SUPPRESS)
+    ap.add_argument("--sharded", action="store_true",
+                    help="run the N > 1 protocol (through the same self-launcher) even at N = 1 (rehearsal)")
     ap.add_argument("--pipe-lhs", type=int, default=20000000)
     ap.add_argument("--pipe-rhs", type=int, default=2000000)
     ap.add_argument("--pipe-joins", type=int, default=3)
@@ -405,15 +412,61 @@ class _StdoutToStderr:
         os.close(self.saved)
 
 
+def free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(args):
+    """--gpus N > 1 without an outside launcher: run torch.distributed.run as a CHILD process (this
+    process never touches the GPU: no exec after a GPU call), one rank per GPU, and forward rank 0's
+    single JSON line to stdout; everything else the ranks print goes to stderr.  Exit status: the
+    launcher's (non-zero if any rank failed), or 1 if no JSON line came back."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"[launch] {' '.join(cmd)}")
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver (RCCL)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    lines = []
+    for line in p.stdout:
+        t = line.strip()
+        if t.startswith("{") and '"metric"' in t:
+            try:
+                lines.append(json.loads(t))
+                continue
+            except ValueError:
+                pass
+        sys.stderr.write(line)
+    rc = p.wait()
+    if lines:
+        print(json.dumps(lines[-1]), flush=True)
+    if rc == 0 and not lines:
+        log("[launch] no JSON line from rank 0")
+        rc = 1
+    return rc
+
+
 def main():
     args = parse()
     if args.workload == "pipeline":  # runs the C++ driver in child processes
         return bench_pipeline(args)
+    if (args.gpus > 1 or args.sharded) and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args)  # before any GPU call in this process (--sharded: one rank too)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    if args.ops_module:  # tests: the N > 1 step on CPU tensors with gloo (no GPU)
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        return bench_multi(args, world, rank, local, torch.device("cpu"), None, dist)
     torch.cuda.set_device(local)
     ccj.device_init(local)
     dist = None
@@ -423,9 +476,9 @@ def main():
             if world == 1:
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
                 os.environ.setdefault("MASTER_PORT", "29533")
-                dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
+                dist.init_process_group(args.backend, rank=0, world_size=1, device_id=torch.device("cuda", local))
             else:
-                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+                dist.init_process_group(args.backend, device_id=torch.device("cuda", local))
             dist.barrier()  # creates the communicator (and its banner) now
     dev = torch.device("cuda", local)
     stream = torch.cuda.Stream(device=dev)
@@ -653,50 +706,75 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
     """C4 (BASELINE configs[3]): each rank owns 1/N of a build side of 2^27 * N reference keys
     (owner = top log2(N) hash bits; 2^30 in total at N = 8) and probes 2^30 keys of its own (weak
     scaling; --scaling strong: 2^30 / N each); a step = batched owner partition + RCCL
-    all-to-all of (key, u32 row) + local probe, pipelined on three streams (ccj_dist.ShardedProbe)."""
+    all-to-all of (key, u32 row) + local probe, pipelined on three streams (ccj_dist.ShardedProbe).
+    The line reports, per step and for the slowest rank, the busy time of each of the three streams
+    (partition, exchange, local probe) and the bytes this rank sends over xGMI."""
     import ccj_dist
+    ops = None
+    if args.ops_module:  # tests: CPU ops object (gloo), no HIP
+        import importlib.util
+        spec = importlib.util.spec_from_file_location("bench_ops", args.ops_module)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        ops = mod.make_ops(rank)
     n_build_total = args.n_build_per_gpu * world
     n_probe = args.n_probe if args.scaling == "weak" else args.n_probe // world
     chunk = args.chunk
+    group = args.group or ccj_dist.GROUP
     t0 = time.perf_counter()
-    with torch.cuda.stream(stream):
-        sp = ccj_dist.ShardedProbe(n_build_total, 1, n_probe, chunk, world, rank, stream=stream,
-                                   batches=args.batches, group=args.group)
-        keys = ccj.gen_uniform_keys(n_probe, SEED, n_build_total, first_row=rank * n_probe, stream=stream)
-    torch.cuda.synchronize()
+    if ops is None:
+        with torch.cuda.stream(stream):
+            sp = ccj_dist.ShardedProbe(n_build_total, 1, n_probe, chunk, world, rank, stream=stream,
+                                       batches=args.batches, group=group)
+            keys = ccj.gen_uniform_keys(n_probe, SEED, n_build_total, first_row=rank * n_probe, stream=stream)
+    else:
+        sp = ccj_dist.ShardedProbe(n_build_total, 1, n_probe, chunk, world, rank, batches=args.batches, ops=ops,
+                                   group=group)
+        keys = ops.probe_keys(SEED, rank * n_probe, n_probe, n_build_total)
+    o = sp.ops
+    o.synchronize()
     log(f"[rank {rank}] setup {time.perf_counter() - t0:.1f} s, local build {sp.n_build_local}, "
-        f"{sp.batches} batches, segment capacity {sp.seg_cap}")
+        f"{sp.batches} batches in groups of {sp.group}, segment capacity {sp.seg_cap}")
     for _ in range(args.warmup):
         sp.step(keys, rank * n_probe)
-    torch.cuda.synchronize()
+    o.synchronize()
     dist.barrier()
-    torch.cuda.synchronize()
-    sp.probe_events.clear()
+    o.synchronize()
+    sp.reset_timing()
     exact_before = sp.exact_steps
     t0 = time.perf_counter()
     for _ in range(args.steps):
         sp.step(keys, rank * n_probe, timing=True)
-    torch.cuda.synchronize()
+    o.synchronize()
     dist.barrier()
     wall = time.perf_counter() - t0
-    t = torch.tensor([wall], device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall = float(t.item())
-    # local probe time per step: the slowest rank's (the roofline's kernel time)
-    pm = torch.tensor([sum(a.elapsed_time(b) for a, b in sp.probe_events) / args.steps], device=dev)
-    dist.all_reduce(pm, op=dist.ReduceOp.MAX)
-    probe_ms = float(pm.item())
+    tdev = dev if dev.type == "cuda" else torch.device("cpu")
+
+    def slowest(x):  # MAX over ranks
+        t = torch.tensor([float(x)], dtype=torch.float64, device=tdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    wall = slowest(wall)
+    phase = sp.timing_ms(args.steps)  # per step: partition / exchange / local-probe stream busy time
+    phase = {k: slowest(v) for k, v in phase.items()}
+    probe_ms = phase["local_probe_ms"]
     # timed steps redone with the exact-size protocol (every rank takes the same branch: the status
     # word is all-reduced before it, so this count is the same on all ranks)
     exact_fallback = sp.exact_steps - exact_before
     # verification (untimed): global L1 / L2 against the exact membership answer
     m, l2 = sp.step(keys, rank * n_probe, verify=True)
-    rk = sp.received_keys(sp.batches - 1)
-    examined, _ = sp.ops.probe_cost(rk, stream)
-    s_bar = examined / max(rk.numel(), 1)
-    tot = torch.tensor([m, l2 - (1 << 64) if l2 >= (1 << 63) else l2], dtype=torch.int64, device=dev)
+    examined, received = 0, 0
+    for i in range(sp.batches):  # S-bar over every received batch of the step
+        rk = sp.received_keys(i)
+        e, _ = o.probe_cost(rk, stream)
+        examined, received = examined + e, received + rk.numel()
+    tot = torch.tensor([m, l2 - (1 << 64) if l2 >= (1 << 63) else l2, examined, received], dtype=torch.int64,
+                       device=tdev)
     dist.all_reduce(tot)
     m_all, l2_all = int(tot[0].item()), int(tot[1].item()) % (1 << 64)
+    s_bar = int(tot[2].item()) / max(int(tot[3].item()), 1)
+    xgmi = sp.xgmi_bytes_per_step()
     parity = {"matches": m_all, "l2": hex(l2_all), "exact_size_fallback_steps": exact_fallback}
     if not args.no_verify and rank == 0:
         from oracle import oracle as O
@@ -705,7 +783,8 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
         parity.update(expected_matches=want_m, l1_ok=want_m == m_all, l2_ok=want_l2 == l2_all)
     m_bar = m_all / (world * n_probe)
     alg = 8 + 8 * s_bar + 12 * m_bar
-    achieved = alg * n_probe / (probe_ms * 1e-3) / 1e9
+    rows_local = int(tot[3].item()) / world  # tuples each rank probes locally per step (mean)
+    achieved = alg * rows_local / (probe_ms * 1e-3) / 1e9 if probe_ms > 0 else None
     if rank == 0:
         value = world * n_probe / (wall / args.steps)
         line = {
@@ -718,10 +797,16 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
                        "table": "linear_probing", "n_build_total": n_build_total, "n_probe_per_gpu": n_probe,
                        "chunk": chunk, "batches": sp.batches, "group": sp.group,
                        "parallelism": f"dp{world} (owner-partitioned)"},
+            # per step, slowest rank; the three streams overlap, so these are busy times, not a sum
+            "partition_ms": phase["partition_ms"], "exchange_ms": phase["exchange_ms"],
+            "local_probe_ms": probe_ms,
+            "xgmi_bytes_per_step": xgmi["sent_to_peers"], "xgmi_useful_bytes_per_step": xgmi["useful_to_peers"],
+            "xgmi_GBps_per_rank": xgmi["sent_to_peers"] / (wall / args.steps) / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": None,
                          "kernel": "ccj_probe_partitioned (local split + walk of received tuples, slowest rank)",
-                         "kernel_ms": probe_ms, "alg_bytes_per_tuple": alg, "s_bar": s_bar, "m_bar": m_bar},
+                         "kernel_ms": probe_ms, "alg_bytes_per_tuple": alg, "s_bar": s_bar, "m_bar": m_bar,
+                         "s_bar_over": "every received batch of one step, all ranks"},
             "cpu_baseline": None,
             "parity": parity,
         }
@@ -730,4 +815,4 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

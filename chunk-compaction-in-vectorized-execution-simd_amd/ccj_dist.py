@@ -38,9 +38,10 @@ import torch.distributed as dist
 # corrupts a one-rank all_to_all_single from 1 GiB up (the first wrong element sits just past
 # 512 MiB), so every exchange here is cut into batches of at most this size.
 MAX_A2A_BYTES = 384 << 20
-# Received batches probed together (one partitioned probe per group): 8 x 2^25 keys at C4.
-# One-rank rehearsal, local probe per step: groups of 2 / 4 / 8 batches 30.6 / 25.6 / 23.9 ms.
-GROUP = 8
+# Received batches probed together (one partitioned probe per group; each local probe sweeps the
+# whole local table once).  One-rank rehearsal, step time with groups of 8 / 16 / 32
+# batches: 37.4 / 36.0 / 34.8 ms; 16 keeps a probe overlapping the next group's exchange at N > 1.
+GROUP = 16
 
 
 def seg_capacity(n: int, world: int, chunk: int) -> int:
@@ -214,7 +215,7 @@ class ShardedProbe:
         self._resize(cap(self.bn))
         ev = lambda: [o.event() for _ in range(2)]  # noqa: E731
         self.ev_part, self.ev_comm, self.ev_probe = ev(), ev(), ev()
-        self.probe_events = []
+        self.probe_events, self.part_events, self.comm_events = [], [], []
         self.parts_exact = {}  # exact-size partitioners (fallback), by batch size
         self.last_exact = False
         self.exact_steps = 0  # steps redone with the exact-size protocol (on every rank alike)
@@ -258,24 +259,60 @@ class ShardedProbe:
     # Send slot s = i % 2 serves batches i, i+2, ...; receive group slot g % 2 serves groups g, g+2;
     # each reuse waits on the event of the previous user (events of the previous step included:
     # waiting on an unrecorded event is a no-op).
-    def _partition(self, keys, i):
+    def _timed(self, events, stream, timing):
+        """Events around one piece of work on `stream` (timing steps only): its busy time."""
+        if not timing:
+            return contextlib.nullcontext()
+        a, b = self.ops.event(True), self.ops.event(True)
+
+        @contextlib.contextmanager
+        def span():
+            a.record(stream)
+            yield
+            b.record(stream)
+            events.append((a, b))
+        return span()
+
+    def _partition(self, keys, i, timing=False):
         s = i % 2
         lo, n = self._batch(i)
         if n not in self.fparts:
             self.fparts[n] = self.ops.fixed_partitioner(n, self.world, self.sub_cap)
         self.pstream.wait_event(self.ev_comm[s])  # the previous all-to-all from send slot s is done
-        self.fparts[n](keys[lo:lo + n], lo, self.sk[s], self.sr[s], self.sc[s], self.status, self.pstream)
+        with self._timed(self.part_events, self.pstream, timing):
+            self.fparts[n](keys[lo:lo + n], lo, self.sk[s], self.sr[s], self.sc[s], self.status, self.pstream)
         self.ev_part[s].record(self.pstream)
 
-    def _exchange(self, i):
+    def _exchange(self, i, timing=False):
         s = i % 2
         gs, rk, rr, rc = self._recv(i)
         self.comm.wait_event(self.ev_part[s])
         if i % self.group == 0:
             self.comm.wait_event(self.ev_probe[gs])  # the previous probe of receive group slot gs is done
-        with self.ops.on(self.comm):
+        with self.ops.on(self.comm), self._timed(self.comm_events, self.comm, timing):
             exchange_fixed(self.sk[s], self.sr[s], self.sc[s], rk, rr, rc)
         self.ev_comm[s].record(self.comm)
+
+    def reset_timing(self):
+        self.probe_events.clear()
+        self.part_events.clear()
+        self.comm_events.clear()
+
+    def timing_ms(self, steps: int) -> dict:
+        """Per step (mean over the timed steps): busy time of the partition, exchange and local-probe
+        streams.  The three overlap (pipelined), so they bound the step from below, not add up."""
+        tot = lambda evs: sum(a.elapsed_time(b) for a, b in evs) / max(steps, 1)  # noqa: E731
+        return {"partition_ms": tot(self.part_events), "exchange_ms": tot(self.comm_events),
+                "local_probe_ms": tot(self.probe_events)}
+
+    def xgmi_bytes_per_step(self) -> dict:
+        """Bytes this rank sends to the other ranks per step: the fixed-capacity segments move whole
+        (equal splits: keys 8 B + u32 rows per slot, one count per sub-segment), and the expected
+        live part of them for uniform keys (12 B per tuple that changes GPU)."""
+        peers = self.world - 1
+        per_batch = peers * (self.seg_cap * 12 + self.subs * 8)
+        return {"sent_to_peers": self.batches * per_batch,
+                "useful_to_peers": self.n_probe * peers / self.world * 12}
 
     def _group_range(self, g):
         return g * self.group, min((g + 1) * self.group, self.batches) - 1
@@ -325,13 +362,13 @@ class ShardedProbe:
             self.status.zero_()
         self.stream.wait_stream(cur)
         self.pstream.wait_stream(cur)
-        self._partition(keys, 0)
-        self._exchange(0)
+        self._partition(keys, 0, timing)
+        self._exchange(0, timing)
         m, l2 = 0, 0
         for i in range(self.batches):
             if i + 1 < self.batches:
-                self._partition(keys, i + 1)
-                self._exchange(i + 1)
+                self._partition(keys, i + 1, timing)
+                self._exchange(i + 1, timing)
             if i % self.group == self.group - 1 or i == self.batches - 1:  # group i // group complete
                 g = i // self.group
                 self._probe(g, timing)

@@ -8,7 +8,9 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -571,6 +573,8 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
     return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: positions / payload columns need a table of >= 16 slots");
   if (a->n_rows >= (1ull << 32)) return fail(CCJ_ERR_LIMIT, "ccj_probe_partitioned: n_rows must be < 2^32");
   if (flags & ~(CCJ_PART_EXACT | CCJ_PART_ROWS | CCJ_PART_RANK)) return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: unknown flags");
+  if ((flags & CCJ_PART_RANK) && !t->d_ckeys && rank_index_applies(t))  // refused before any launch
+    return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: CCJ_PART_RANK needs ccj_table_build_rank_index first");
   const bool rows = (flags & CCJ_PART_ROWS) != 0;
   if (rows && (!a->out_payload || p.cap != a->chunk || t->info.max_dup > 1 || a->out_pos || a->n_payload_cols ||
                t->info.kind != CCJ_TABLE_LP || t->info.size < 16))
@@ -634,8 +638,6 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   const bool rank = !exact && L.pl.lo_bits && L.ovf_base && t->d_ckeys && t->rank_wbits == L.pl.window_bits &&
                     p.keys_in_out && t->info.max_dup <= 1 && p.n_pay == 0 && !p.out_pos && !p.out_rounds &&
                     a->chunk % ccj::kRankChunkMultiple == 0 && ((flags & CCJ_PART_RANK) || ccj_tune_int("CCJ_RANK", 0));
-  if ((flags & CCJ_PART_RANK) && !t->d_ckeys && rank_index_applies(t))
-    return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: CCJ_PART_RANK needs ccj_table_build_rank_index first");
   if (rank) {
     const ccj::RankIndex ix{t->d_occ, t->d_pre, t->d_ckeys, t->rank_wbits};
     const size_t fixed = align256(((uint64_t)L.parts * 8 + 1) * 4);
@@ -702,7 +704,9 @@ OrderedLayout ordered_layout(const ccj_table *t, uint64_t n_rows, uint32_t chunk
       n_rows >= (1ull << 32))
     return O;
   O.L = part_layout(t, n_rows, chunk);
-  if (O.L.pl.lo_bits == 0) return O;
+  // the split's run records and the unsplit address positions as u32: beyond 2^32 positions
+  // (about 3.8e9 rows: segments + the n/16 overflow area) the one-pass route would wrap them
+  if (O.L.pl.lo_bits == 0 || O.L.positions >= (1ull << 32)) return O;
   O.partitioned = true;
   O.tile = ccj::slot_split_tile_keys(1u << (O.L.pl.lo_bits + O.L.pl.hi_bits), true);
   O.n_tiles = (n_rows + O.tile - 1) / O.tile;
@@ -922,15 +926,29 @@ int ccj_gen_c3_keys(int64_t *d_out, uint64_t n, uint64_t seed, uint64_t first_ro
     return fail(CCJ_ERR_INVALID, "ccj_gen_c3_keys: bad argument");
   const uint64_t n_unique = n_build / cf + (n_build % cf != 0);
   if (n_unique >= (1ull << 32)) return fail(CCJ_ERR_LIMIT, "ccj_gen_c3_keys: more than 2^32 distinct build keys");
-  // Zipf s = 1 rank table over the n_unique build keys, built once per table size (host, untimed)
-  static uint64_t cached_n = 0;
-  static uint32_t *d_zipf = nullptr;
-  if (!d_zipf || cached_n != n_unique) {
-    std::vector<uint32_t> t(ccj::kZipfBuckets + 1);
-    zipf_table(n_unique, t.data());
-    if (!d_zipf) HIP_TRY(hipMalloc((void **)&d_zipf, t.size() * sizeof(uint32_t)), "zipf table");
-    HIP_TRY(hipMemcpy(d_zipf, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice), "zipf table");
-    cached_n = n_unique;
+  // Zipf s = 1 rank table over the n_unique build keys (host, untimed): one device copy per
+  // (device, table size), made once and never overwritten, so a generator kernel still running on
+  // any stream never sees it change; the map is guarded for concurrent callers.
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev), "zipf table");
+  const uint32_t *d_zipf = nullptr;
+  {
+    static std::mutex mu;
+    static std::map<std::pair<int, uint64_t>, uint32_t *> tables;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = tables.find({dev, n_unique});
+    if (it == tables.end()) {
+      std::vector<uint32_t> t(ccj::kZipfBuckets + 1);
+      zipf_table(n_unique, t.data());
+      uint32_t *d = nullptr;
+      HIP_TRY(hipMalloc((void **)&d, t.size() * sizeof(uint32_t)), "zipf table");
+      // on the caller's stream, then waited for: the host buffer dies with this scope
+      HIP_TRY(hipMemcpyAsync(d, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice, (hipStream_t)stream),
+              "zipf table");
+      HIP_TRY(hipStreamSynchronize((hipStream_t)stream), "zipf table");
+      it = tables.emplace(std::make_pair(dev, n_unique), d).first;
+    }
+    d_zipf = it->second;
   }
   HIP_TRY(ccj::launch_gen_c3(d_out, n, seed, first_row, n_build, cf, hit_ppm, d_zipf, (hipStream_t)stream),
           "gen c3 keys");

@@ -1368,8 +1368,8 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <uint32_t kWaveRows, bool HOME>
-__device__ __forceinline__ void walk_stage(const ProbeParams &p, WalkShared<HOME> &sm, uint64_t base, uint32_t w0,
+template <uint32_t kWaveRows, bool HOME, typename SM>
+__device__ __forceinline__ void walk_stage(const ProbeParams &p, SM &sm, uint64_t base, uint32_t w0,
                                            uint32_t wend, uint32_t lane) {
   int64_t v[kWaveRows / kWave];  // all loads in flight before the first LDS write
 #pragma unroll
@@ -1480,8 +1480,8 @@ __device__ __forceinline__ void walk_finish(const ProbeParams &p, SM &sm, uint64
 // The compacted chunk (sel in sm.hc, payload in sm.key, tot entries) as 16-byte stores.  A last
 // partial group writes past the count inside the chunk's own cap region (cap is a multiple of 4),
 // which holds no data of the chunk's consumers.
-template <int AUX, uint32_t kThreads>
-__device__ __forceinline__ void emit_wg_stores(const ProbeParams &p, WalkShared<true> &sm, uint64_t obase, uint32_t tot,
+template <int AUX, uint32_t kThreads, typename SM>
+__device__ __forceinline__ void emit_wg_stores(const ProbeParams &p, SM &sm, uint64_t obase, uint32_t tot,
                                                bool pay) {
   const uint32_t tid = threadIdx.x;
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(p.out_sel + obase, (short)0, (int)(p.cap * 4), 0x00020000);
@@ -1497,8 +1497,8 @@ __device__ __forceinline__ void emit_wg_stores(const ProbeParams &p, WalkShared<
     }
   }
 }
-template <uint32_t kWaveRows, int NW>
-__device__ __forceinline__ bool walk_emit_wg(const ProbeParams &p, WalkShared<true> &sm, uint64_t c, uint32_t w0,
+template <uint32_t kWaveRows, int NW, typename SM>
+__device__ __forceinline__ bool walk_emit_wg(const ProbeParams &p, SM &sm, uint64_t c, uint32_t w0,
                                              uint32_t wend, uint32_t lane, uint32_t wave, uint32_t *s_wtot,
                                              uint32_t phys) {
   constexpr int kJ = (int)(kWaveRows / kWave);
@@ -1570,10 +1570,13 @@ __device__ __forceinline__ bool walk_emit_wg(const ProbeParams &p, WalkShared<tr
 // rounds, the reference's Next calls for it; L > 26: bit 31 | L, the chunk re-walks round by
 // round), written to p.out_w at the row's position; no emit.
 // LN: lanes per row (2: 32-byte windows, 4: 64-byte windows; 16 bytes per lane either way).
-template <int R, bool HOME, int NW = 4, bool MM = false, int LN = 2>
+template <int R, bool HOME, int NW = 4, bool MM = false, int LN = 2, bool DMA = false>
 __global__ __launch_bounds__(kWave * NW) void probe_walk(ProbeParams p) {
   constexpr uint32_t kWaveRows = kMaxChunk / NW;  // rows per wave
   __shared__ WalkShared<HOME> sm;
+  // DMA: the table windows land in LDS by LDS-DMA (global_load_lds_dwordx4, a per-lane source
+  // address), one 1 KiB slot per (wave, row k): 16 bytes per lane at lane * 16
+  __shared__ __attribute__((aligned(16))) int64_t s_win[DMA ? NW * R * 2 * kWave : 2];
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   constexpr uint32_t kWin = 2 * LN;  // slots per window
   constexpr uint32_t kRowsPer = kWave / LN;  // rows per wave instruction
@@ -1630,11 +1633,24 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk(ProbeParams p) {
       // values are never used.  Same box, C2 step: 12.28 / 12.58 ms against 12.79 / 12.58
       // predicated — the walk is bound by requests in flight per CU, not by one wave's chain.
       const uint32_t a = ((need >> k) & 1u) ? s + 2 * sub : 0u;
-      if (CCJ_ABLATED(p.ablate, 2u)) {  // timing only: no table reads
+      if constexpr (DMA) {
+        __builtin_amdgcn_global_load_lds(static_cast<const void *>(p.table + a),
+                                         (__attribute__((address_space(3))) void *)&s_win[(wave * R + k) * 2 * kWave],
+                                         16, 0, 0);
+      } else if (CCJ_ABLATED(p.ablate, 2u)) {  // timing only: no table reads
         v0[k] = sub ? -1 : key[k];
         v1[k] = -1;
       } else {
         const longlong2 x = *reinterpret_cast<const longlong2 *>(p.table + a);
+        v0[k] = x.x;
+        v1[k] = x.y;
+      }
+    }
+    if constexpr (DMA) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every window of the step has landed
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const longlong2 x = *reinterpret_cast<const longlong2 *>(&s_win[(wave * R + k) * 2 * kWave + 2 * lane]);
         v0[k] = x.x;
         v1[k] = x.y;
       }
@@ -1691,10 +1707,11 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk(ProbeParams p) {
   CCJ_STAMP(t2);
   if (MM) {  // the rows' round words, coalesced at their positions
     wave_lds_sync();
-    if (p.w16 && kWaveRows == 8 * kWave && w0 + kWaveRows <= p.chunk) {
+    if (p.w16 && kWaveRows == 8 * kWave && w0 + kWaveRows <= p.chunk && (p.chunk & 7u) == 0u) {
       // 8 words per lane in one 16-byte store (rows past wend write don't-care words inside the
       // chunk's own positions, which no run points at; a wave whose rows pass the chunk's end —
-      // chunks under 2048 — stores word by word)
+      // chunks under 2048 — stores word by word, and so does a chunk width that is not a
+      // multiple of 8, whose chunks do not start 16-byte aligned)
       const uint32_t i0 = w0 + 8 * lane;
       uint32_t h[4];
 #pragma unroll
@@ -1729,13 +1746,192 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk(ProbeParams p) {
   walk_finish(p, sm, c, lane, lane_rounds, overflow, t0, t1, t2, steps);
 }
 
+// probe_walk1<NB, MM>: probe_walk's walk with ONE lane per row and the table windows brought in by
+// LDS-DMA (global_load_lds_dwordx4, per-lane source address).  Round 3 measurements (tools/reqpath):
+// random 32-byte windows from an L2-resident window reach ~490 G/s chip-wide by LDS-DMA against
+// ~255 G/s as vector loads; probe_walk's lane pairs (3.4 VALU wave-instructions per row) and its
+// wait for every window of a step (vmcnt(0)) left it at 7.7 ms either way.  Here each wave keeps NB
+// batches of 64 rows in flight in a ring of LDS slots: per batch, two DMA instructions (lane 2p + h
+// loads half h of batch entry 2p + k's window, k = the instruction) put entry e's 32-byte window at
+// slot + (e & 1) * 1024 + (e >> 1) * 32; the
+// wave waits for the OLDEST batch only (vmcnt(2 * (NB - 1))), checks it one row per lane, and
+// refills it — rows whose run continues keep their lane, finished rows are replaced from the wave's
+// cursor — so the memory pipeline stays full while a batch is checked.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// One LDS-DMA wave-instruction: lane L's 16 bytes at `g` land at LDS byte lds + 16 * L.  Issued as
+// inline asm so that the compiler, which cannot tell which ring slot a DMA writes, does not wait for
+// every DMA in flight (vmcnt(0)) before each LDS read of the ring: the caller waits itself
+// (wait_vmcnt), and no compiler-tracked vector-memory operation may be in flight across these.
+__device__ __forceinline__ void dma16(const void *g, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds) : "memory", "m0");
+}
+constexpr uint32_t kRingSlot = 2 * 1024;  // one batch: 64 windows of 32 B, two DMA halves
+// probe_walk1's LDS: the chunk's keys and home slots / counts, and the wave's DMA ring, which the
+// emit's scratch (total, rounds, per-wave sums) overlaps once every wave's walk is over: 32 KiB at
+// NB = 1 (5 workgroups per CU), 40 KiB at NB = 2 (4 per CU)
+template <int NB, int NW>
+struct Walk1Shared {
+  int64_t key[kMaxChunk];
+  uint32_t hc[kMaxChunk];
+  union {
+    __attribute__((aligned(16))) char ring[NW * NB * kRingSlot];
+    struct {
+      uint32_t total, rounds, wtot[NW];
+    };
+  };
+};
+template <int NB, bool MM = false>
+__global__ __launch_bounds__(kWave * 4) void probe_walk1(ProbeParams p) {
+  constexpr int NW = 4;
+  constexpr uint32_t kWaveRows = kMaxChunk / NW;  // rows per wave
+  __shared__ Walk1Shared<NB, NW> sm;
+  char *const s_ring = sm.ring;
+  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  const uint64_t c = walk_chunk_index(p);
+  const uint64_t base = c * p.chunk;
+  const uint32_t phys = flat_phys(p, base);
+  const uint32_t w0 = wave * kWaveRows;
+  const uint32_t wend = phys > w0 ? (phys - w0 < kWaveRows ? phys : w0 + kWaveRows) : w0;  // wave's rows [w0, wend)
+  // (timing only, tuning build: 0x100 stages the keys of chunk c & 63 — L2-resident key lines)
+  walk_stage<kWaveRows, true>(p, sm, CCJ_ABLATED(p.ablate, 0x100u) ? (c & 63u) * p.chunk : base, w0, wend, lane);
+  char *ring = s_ring + wave * NB * kRingSlot;
+  // the ring's LDS byte address, wave-uniform (M0 of the DMAs)
+  const uint32_t ring_lds = (uint32_t)__builtin_amdgcn_readfirstlane(
+      (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)ring);
+  const uint32_t last_start = p.mask - (kWin - 1);  // table size - window (size >= 16)
+  const uint32_t half = (lane & 1u) * 2u;            // slots of the half this lane's DMA loads
+  // this lane's row in ring slot b: key, row, next unread slot, window start, rounds walked, matches
+  int64_t key[NB];
+  uint32_t row[NB], cur[NB], st[NB], r0[NB], cnt[NB];
+  uint32_t live = 0, lane_rounds = 0;
+  uint32_t next = w0;  // wave-uniform: the wave's next unwalked row
+  auto take = [&](int b, bool want) {  // lanes with `want` take the wave's next rows, in lane order
+    const uint64_t bm = __ballot(want);
+    const uint32_t i = next + lane_prefix(bm);
+    next += (uint32_t)__popcll(bm);
+    if (want) {
+      row[b] = i;
+      r0[b] = 0;
+      cnt[b] = 0;
+      if (i < wend) {
+        key[b] = sm.key[i];
+        cur[b] = sm.hc[i];
+        live |= 1u << b;
+      }
+    }
+  };
+  auto issue = [&](int b) {
+    uint32_t a = 0;  // an idle entry loads slot 0's line (every DMA is issued: fixed vmcnt depth)
+    if ((live >> b) & 1u) {
+      uint32_t s = cur[b] < last_start ? cur[b] : last_start;
+      const uint32_t lim = (s & ~15u) + (16u - kWin);  // the window ends at its 128-byte line
+      s = s < lim ? s : lim;
+      st[b] = s;
+      a = s;
+    }
+    if (CCJ_ABLATED(p.ablate, 0x200u)) a &= 0x1FFFu;  // (timing only: windows from the first 64 KiB)
+    const uint32_t a0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, 0xA0, 0xF, 0xF, false);  // quad_perm 0,0,2,2
+    const uint32_t a1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, 0xF5, 0xF, 0xF, false);  // quad_perm 1,1,3,3
+    const uint32_t slot = ring_lds + (uint32_t)b * kRingSlot;
+    dma16(p.table + a0 + half, slot);
+    dma16(p.table + a1 + half, slot + 1024u);
+  };
+  auto check = [&](int b) {
+    const char *w = ring + b * kRingSlot + (lane & 1u) * 1024 + (lane >> 1) * 32;
+    const longlong2 x0 = *reinterpret_cast<const longlong2 *>(w);
+    const longlong2 x1 = *reinterpret_cast<const longlong2 *>(w + 16);
+    if ((live >> b) & 1u) {
+      const int64_t k = key[b];
+      const uint32_t e = (x0.x == -1 ? 1u : 0u) | (x0.y == -1 ? 2u : 0u) | (x1.x == -1 ? 4u : 0u) | (x1.y == -1 ? 8u : 0u);
+      const uint32_t m = (x0.x == k ? 1u : 0u) | (x0.y == k ? 2u : 0u) | (x1.x == k ? 4u : 0u) | (x1.y == k ? 8u : 0u);
+      const uint32_t off = cur[b] - st[b];
+      const uint32_t ee = e >> off;
+      const uint32_t f = (uint32_t)__builtin_ctz(ee | ((1u << kWin) >> off));  // run end (or window end) past cur
+      const uint32_t hits = (m >> off) & ((1u << f) - 1u);
+      if (MM) cnt[b] |= r0[b] < kMmRounds ? hits << r0[b] : 0u;  // rounds >= 26 end as long rows
+      else cnt[b] += (uint32_t)__builtin_popcount(hits);
+      if (ee) {
+        const uint32_t r = r0[b] + f;  // occupied slots walked = the reference's rounds
+        lane_rounds = r > lane_rounds ? r : lane_rounds;
+        if (MM) cnt[b] = r <= kMmRounds ? (cnt[b] & ((1u << kMmRounds) - 1u)) | r << kMmRounds : kMmLong | r;
+        if (CCJ_ABLATED(p.ablate, 0x200u)) cnt[b] = 1;  // (timing only: the emit path of the real data)
+        sm.hc[row[b]] = cnt[b];
+        live &= ~(1u << b);
+      } else {
+        r0[b] += kWin - off;
+        cur[b] = (st[b] + kWin) & p.mask;
+      }
+    }
+  };
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    key[b] = 0;
+    row[b] = cur[b] = st[b] = r0[b] = cnt[b] = 0;
+    take(b, true);
+    issue(b);
+  }
+  for (bool more = true; more;) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      wait_vmcnt<2 * (NB - 1)>();  // batch b (the oldest) has landed
+      check(b);
+      take(b, ((live >> b) & 1u) == 0u);
+      if (__ballot(live != 0u) == 0ull) {  // every slot empty and no rows left
+        more = false;
+        break;
+      }
+      issue(b);
+    }
+  }
+  wait_vmcnt<0>();
+  __syncthreads();  // every wave's ring is idle: the emit's scratch may overlap it
+  if (tid == 0) {
+    sm.total = 0;
+    sm.rounds = 0;
+  }
+  __syncthreads();
+  if (MM) {  // the rows' round words, coalesced at their positions (probe_walk's MM tail)
+    if (p.w16 && kWaveRows == 8 * kWave && w0 + kWaveRows <= p.chunk && (p.chunk & 7u) == 0u) {
+      const uint32_t i0 = w0 + 8 * lane;
+      uint32_t h[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        h[t] = (uint32_t)round_word16(sm.hc[i0 + 2 * t]) | (uint32_t)round_word16(sm.hc[i0 + 2 * t + 1]) << 16;
+      const u32x4 v = {h[0], h[1], h[2], h[3]};
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>((uint16_t *)p.out_w + base + i0));
+      return;
+    }
+#pragma unroll
+    for (int j = 0; j < (int)(kWaveRows / kWave); ++j) {
+      const uint32_t i = w0 + (uint32_t)j * kWave + lane;
+      if (i < wend) {
+        if (p.w16) __builtin_nontemporal_store(round_word16(sm.hc[i]), (uint16_t *)p.out_w + base + i);
+        else __builtin_nontemporal_store(sm.hc[i], p.out_w + base + i);
+      }
+    }
+    return;
+  }
+  if (p.emit_pol != kEmitWave || p.rows_in_sel) {  // (rows_in_sel: only the workgroup emit maps rows)
+    if (walk_emit_wg<kWaveRows, NW>(p, sm, c, w0, wend, lane, wave, sm.wtot, phys)) {
+      walk_finish(p, sm, c, lane, lane_rounds, 0u, 0ull, 0ull, 0ull, 0u);
+      return;
+    }
+  }
+  const uint32_t overflow = walk_emit<kWaveRows>(p, sm, c, w0, wend, lane);
+  walk_finish(p, sm, c, lane, lane_rounds, overflow, 0ull, 0ull, 0ull, 0u);
+}
+
 // Ordered probe, step 4 (emit_ordered): one chunk per 256-thread workgroup, the reference's
 // per-Next stream from its rows' round words (p.in_w: mm | rounds << 26, or kMmLong | rounds).
 // Thread (wave, lane) owns rows q*256 + tid (q < 8), i.e. row group j = 4q + wave, lane `lane`:
 // its keys and words stay in registers, and the count / scan / emit phases are probe_chunks'
 // (per (round, row group) ballots, a round-major exclusive scan, ballot-prefix stores), so the
 // output is exactly ccj_probe's.  A chunk with a row of more than 26 rounds re-walks round by
-// round (rounds_generic).  Only s_off (4 KB) is LDS on the common path: 8 workgroups per CU.
+// round (rounds_generic).  LDS: s_off (4 KB) plus the staged output (s_osel 8 KB + s_opay 16 KB),
+// about 28 KB per workgroup: 5 workgroups per CU (round 2d: 8 before the output was staged).
 __global__ __launch_bounds__(kBlock) void emit_ordered(ProbeParams p) {
   constexpr int kQ = kMaxChunk / kBlock;  // 8 rows per thread
   __shared__ uint32_t s_off[kMaxFastRounds * 32];
@@ -2027,8 +2223,16 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
     // 13.24 / 13.22 (half the rows per load instruction); tuning build only (CCJ_WALK_LANES=4)
     if (ccj_tune_int("CCJ_WALK_LANES", 2) == 4)
       hipLaunchKernelGGL((probe_walk<3, true, 4, false, 4>), g, b, 0, s, p);
-    else
+    else if (ccj_tune_int("CCJ_WALK_DMA", 2) == 0)
       hipLaunchKernelGGL((probe_walk<3, true>), g, b, 0, s, p);
+    else if (ccj_tune_int("CCJ_WALK_DMA", 2) == 1)
+      hipLaunchKernelGGL((probe_walk<3, true, 4, false, 2, true>), g, b, 0, s, p);
+    else if (ccj_tune_int("CCJ_WALK_NB", 2) == 1)
+      hipLaunchKernelGGL((probe_walk1<1>), g, b, 0, s, p);
+    else if (ccj_tune_int("CCJ_WALK_NB", 2) == 3)
+      hipLaunchKernelGGL((probe_walk1<3>), g, b, 0, s, p);
+    else
+      hipLaunchKernelGGL((probe_walk1<2>), g, b, 0, s, p);
   }
   return hipGetLastError();
 }

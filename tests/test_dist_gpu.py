@@ -198,20 +198,24 @@ def test_sharded_probe_pipelined_one_rank(pg1, batches):
 
 
 def test_bench_sharded_line():
-    """bench.py's N > 1 step (bench_multi) end to end on one GPU (--sharded: a one-rank RCCL group),
-    at a small size: the JSON line of the driver's contract, L1 + L2 exact."""
+    """bench.py's N > 1 step (bench_multi) end to end on one GPU through bench.py's own launcher
+    (--gpus 1 --sharded, no outside torchrun: a one-rank RCCL group in a child process), at a small
+    size: exactly one JSON line of the driver's contract with the N > 1 diagnostics, L1 + L2 exact."""
     import json
     import os
     import subprocess
     import sys
-    from test_dist_cpu import free_port
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
-    p = subprocess.run([sys.executable, "bench.py", "--sharded", "--steps", "2", "--warmup", "1", "--no-cpu",
-                        "--n-build-per-gpu", str(1 << 22), "--n-probe", str(1 << 24), "--batches", "4"],
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--sharded", "--steps", "2", "--warmup", "1",
+                        "--no-cpu", "--n-build-per-gpu", str(1 << 22), "--n-probe", str(1 << 24), "--batches", "4"],
                        cwd=root, capture_output=True, text=True, timeout=600, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
-    line = json.loads(p.stdout.strip().splitlines()[-1])
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout
+    line = json.loads(lines[0])
     assert line["n_gpus"] == 1 and line["scaling"] == "weak" and line["value"] > 0
     assert line["parity"]["l1_ok"] and line["parity"]["l2_ok"], line["parity"]
     assert 0 < line["roofline"]["frac"] < 1
+    assert line["local_probe_ms"] > 0 and line["partition_ms"] > 0 and line["exchange_ms"] >= 0
+    assert line["xgmi_bytes_per_step"] == 0  # one rank: nothing crosses xGMI
