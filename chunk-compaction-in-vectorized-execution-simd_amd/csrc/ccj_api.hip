@@ -271,6 +271,23 @@ int build_chain_host(const int64_t *keys, uint64_t n, ccj_table **out) {
     }
     t->d_bucket = (int64_t *)d;
   }
+  if (longest < 0xFFFFu) {  // 8-byte records {start | len << 32 | fp(first key) << 48}
+    std::vector<uint64_t> rec(size);
+    for (uint64_t b = 0; b < size; ++b) {
+      const uint64_t lo = off[b], len = off[b + 1] - off[b];
+      const uint64_t fp = len ? ccj::bucket_fp(ccj::murmurhash64((uint64_t)chain[lo])) : 0u;
+      rec[b] = lo | len << 32 | fp << 48;
+    }
+    rc = upload(&d, rec.data(), rec.size() * sizeof(uint64_t), "chain bucket records (8 B)");
+    if (rc) {
+      (void)hipFree(t->d_table);
+      (void)hipFree(t->d_off);
+      (void)hipFree(t->d_row);
+      (void)hipFree(t->d_bucket);
+      return rc;
+    }
+    t->d_bucket8 = (uint64_t *)d;
+  }
   t->info.d_table = t->d_table;
   t->info.d_bucket_off = t->d_off;
   (void)hipGetDevice(&t->device);
@@ -468,6 +485,7 @@ int ccj_table_free(ccj_table *t) {
   if (t->d_table) (void)hipFree(t->d_table);
   if (t->d_off) (void)hipFree(t->d_off);
   if (t->d_bucket) (void)hipFree(t->d_bucket);
+  if (t->d_bucket8) (void)hipFree(t->d_bucket8);
   if (t->d_row) (void)hipFree(t->d_row);
   if (t->d_pay) (void)hipFree(t->d_pay);
   if (t->d_occ) (void)hipFree(t->d_occ);
@@ -488,6 +506,7 @@ int fill_probe_params(const ccj_table *t, const ccj_probe_args *a, ccj::ProbePar
   p.table = t->d_table;
   p.off = t->d_off;
   p.bucket = reinterpret_cast<const longlong2 *>(t->d_bucket);
+  p.bucket8 = ccj_tune_int("CCJ_BUCKET8", 1) ? t->d_bucket8 : nullptr;
   p.mask = (uint32_t)(t->info.size - 1);
   p.keys = a->keys;
   p.sel = a->sel;

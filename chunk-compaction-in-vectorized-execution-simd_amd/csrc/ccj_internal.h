@@ -13,6 +13,9 @@ struct ccj_table {
   int64_t *d_table = nullptr;   // LP slots / chain keys
   uint32_t *d_off = nullptr;    // chain CSR offsets (size + 1)
   int64_t *d_bucket = nullptr;  // chain: per bucket {start | len << 32, first chain key} (16 B)
+  // chain: per bucket {start | len << 32 | fp << 48} (8 B): fp = the first key's fingerprint
+  // (bucket_fp), len < 2^16 (absent when a chain is longer: the 16-byte records serve alone)
+  uint64_t *d_bucket8 = nullptr;
   uint32_t *d_row = nullptr;    // table position -> build tuple index (LP: kNoRow for empty slots)
   uint64_t positions = 0;       // allocated positions (LP slots / chain keys, padded)
   int64_t *d_pay = nullptr;     // position-major payload rows [positions][n_pay]
@@ -39,6 +42,9 @@ __host__ __device__ __forceinline__ uint64_t murmurhash64(uint64_t x) {
   return x;
 }
 
+// Fingerprint of a chain key for the 8-byte bucket records: hash bits far above any bucket index.
+__host__ __device__ __forceinline__ uint32_t bucket_fp(uint64_t h) { return (uint32_t)(h >> 48); }
+
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr uint32_t kMaxChunk = 2048;
@@ -50,6 +56,10 @@ struct ProbeParams {
   // chain only, optional: bucket records {start | len << 32, first key} — one 16-byte load gives
   // the chain's range and its round-0 candidate (most chains at load 1/2 have one key)
   const longlong2 *bucket;
+  // chain only, optional: 8-byte bucket records {start | len << 32 | fp << 48} (the partitioned
+  // walk): a key whose fingerprint differs from fp is not the chain's first key, so most misses end
+  // at the record, and a partition's records take half the L2
+  const uint64_t *bucket8;
   uint32_t mask;  // size - 1 (size <= 2^32)
   const int64_t *keys;
   const uint32_t *sel;

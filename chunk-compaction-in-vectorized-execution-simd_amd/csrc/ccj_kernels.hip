@@ -1220,13 +1220,16 @@ __global__ __launch_bounds__(kFlatThreads) void probe_chain_win(ProbeParams p) {
   }
   __syncthreads();
   int64_t key[R];
-  uint32_t row[R], cur[R], lim[R];
+  uint32_t row[R], cur[R], lim[R], kfp[R];
   uint32_t need = 0, fresh = 0, lane_rounds = 0, overflow = 0;  // fresh bit k: at the bucket record
+  const bool rec8 = p.bucket8 != nullptr;
   auto start = [&](int k, uint32_t i) {
     row[k] = i;
     if (i < phys) {
       key[k] = s_key[i];
-      cur[k] = (uint32_t)murmurhash64((uint64_t)key[k]) & p.mask;
+      const uint64_t h = murmurhash64((uint64_t)key[k]);
+      cur[k] = (uint32_t)h & p.mask;
+      kfp[k] = bucket_fp(h);
       need |= 1u << k;
       fresh |= 1u << k;
     }
@@ -1234,7 +1237,7 @@ __global__ __launch_bounds__(kFlatThreads) void probe_chain_win(ProbeParams p) {
 #pragma unroll
   for (int k = 0; k < R; ++k) {
     key[k] = 0;
-    cur[k] = lim[k] = 0;
+    cur[k] = lim[k] = kfp[k] = 0;
     start(k, (uint32_t)k * kFlatThreads + tid);
   }
   while (__ballot(need != 0u) != 0ull) {
@@ -1243,6 +1246,7 @@ __global__ __launch_bounds__(kFlatThreads) void probe_chain_win(ProbeParams p) {
     for (int k = 0; k < R; ++k) {  // unconditional (an idle row reads bucket 0): no wait per load
       const bool nd = (need >> k) & 1u, fr = (fresh >> k) & 1u;
       const longlong2 *src = nd && !fr ? reinterpret_cast<const longlong2 *>(p.table + (cur[k] & ~1u))
+                             : rec8    ? reinterpret_cast<const longlong2 *>(p.bucket8 + (nd ? cur[k] & ~1u : 0u))
                                        : p.bucket + (nd ? cur[k] : 0u);
       v[k] = *src;
     }
@@ -1253,10 +1257,19 @@ __global__ __launch_bounds__(kFlatThreads) void probe_chain_win(ProbeParams p) {
       if ((need >> k) & 1u) {
         if ((fresh >> k) & 1u) {
           fresh &= ~(1u << k);
-          const uint32_t st = (uint32_t)v[k].x, len = (uint32_t)((uint64_t)v[k].x >> 32);
+          // 8-byte records come in aligned pairs: this bucket's is the half cur & 1
+          const uint64_t r = rec8 ? (uint64_t)((cur[k] & 1u) ? v[k].y : v[k].x) : (uint64_t)v[k].x;
+          const uint32_t st = (uint32_t)r, len = rec8 ? (uint32_t)(r >> 32) & 0xFFFFu : (uint32_t)(r >> 32);
           lane_rounds = len > lane_rounds ? len : lane_rounds;
           if (len == 0) {
             done |= 1u << k;  // empty bucket: not in the active set (chaining_ht.cpp:52-55)
+          } else if (rec8) {
+            // a key whose fingerprint differs is not the first chain key: round 0 needs no read;
+            // an equal fingerprint reads the first key with the rest of the chain
+            const bool skip = (uint32_t)(r >> 48) != kfp[k];
+            cur[k] = skip ? st + 1 : st;
+            lim[k] = st + len;
+            if (skip && len == 1) done |= 1u << k;
           } else {
             hits[k] = v[k].y == key[k] ? 1u : 0u;  // round 0 from the record's first key
             cur[k] = st + 1;
@@ -1765,8 +1778,13 @@ __device__ __forceinline__ void wait_vmcnt() {
 // inline asm so that the compiler, which cannot tell which ring slot a DMA writes, does not wait for
 // every DMA in flight (vmcnt(0)) before each LDS read of the ring: the caller waits itself
 // (wait_vmcnt), and no compiler-tracked vector-memory operation may be in flight across these.
+// M0 is saved and restored: the compiler treats M0 as reserved and does not honour a clobber of it.
 __device__ __forceinline__ void dma16(const void *g, uint32_t lds) {
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds) : "memory", "m0");
+  uint32_t saved;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(saved)
+               : "v"(g), "s"(lds)
+               : "memory");
 }
 constexpr uint32_t kRingSlot = 2 * 1024;  // one batch: 64 windows of 32 B, two DMA halves
 // probe_walk1's LDS: the chunk's keys and home slots / counts, and the wave's DMA ring, which the
@@ -2328,12 +2346,59 @@ __global__ __launch_bounds__(256) void gather_payload_quad(GatherParams g) {
   }
 }
 
+// gather_payload_quad with the row pieces brought in by LDS-DMA (dma16: lane (r0, q)'s 16 bytes of
+// row ps[u] land at its own 16 bytes of the wave's slot u) and read back from LDS before the column
+// stores.  Round 3: tools/reqpath measures random 32-64 B reads from HBM at ~100 G/s by LDS-DMA
+// against ~53 G/s as vector loads, with half the L2 requests.
+template <int U>
+__global__ __launch_bounds__(256) void gather_payload_dma(GatherParams g) {
+  __shared__ int64_t *s_cols[CCJ_MAX_PAYLOAD_COLS];
+  __shared__ __attribute__((aligned(16))) int64_t s_ring[4 * U * 2 * kWave];
+  if (threadIdx.x < CCJ_MAX_PAYLOAD_COLS) s_cols[threadIdx.x] = g.cols[threadIdx.x];
+  __syncthreads();
+  const uint64_t c = blockIdx.x;
+  const uint64_t ob = g.out_base ? g.out_base[c] : c * g.cap;
+  const uint32_t n = g.count[c];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t q = threadIdx.x & 3u, r0 = threadIdx.x >> 2;  // 64 rows per block step
+  int64_t *c0 = s_cols[2 * q], *c1 = s_cols[2 * q + 1];
+  int64_t *ring = s_ring + wave * U * 2 * kWave;
+  const uint32_t ring_lds = (uint32_t)__builtin_amdgcn_readfirstlane(
+      (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) int64_t *)ring);
+  for (uint32_t base = 0; base < n; base += 64 * U) {
+    uint32_t ps[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t j = base + u * 64 + r0;
+      ps[u] = g.pos[ob + (j < n ? j : 0u)];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      dma16(g.pay + (uint64_t)ps[u] * g.stride + 2 * q, ring_lds + (uint32_t)u * 1024u);
+    wait_vmcnt<0>();
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const longlong2 v = *reinterpret_cast<const longlong2 *>(ring + u * 2 * kWave + 2 * lane);
+      const uint32_t j = base + u * 64 + r0;
+      if (j < n) {
+        __builtin_nontemporal_store(v.x, c0 + ob + j);
+        __builtin_nontemporal_store(v.y, c1 + ob + j);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the ring is read before the next DMAs land
+  }
+}
+
 template <int NP>
 hipError_t launch_gather_np(const GatherParams &g, uint64_t n_chunks, hipStream_t s) {
   const bool vec = (g.stride % 2 == 0) && ((uintptr_t)g.pay % 16 == 0);
   // 8 columns: 2 / 4 / 8 rows in flight per lane group 26.9 ms each at C5, the walk's XCD order
   // 27.0, plain instead of non-temporal stores 27.8-28.9 (profiles/r1g_*)
-  if (NP == 8 && vec) hipLaunchKernelGGL((gather_payload_quad<4>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
+  if (NP == 8 && vec && ccj_tune_int("CCJ_GATHER_DMA", 1) == 1)
+    hipLaunchKernelGGL((gather_payload_dma<4>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
+  else if (NP == 8 && vec && ccj_tune_int("CCJ_GATHER_DMA", 1) == 2)
+    hipLaunchKernelGGL((gather_payload_dma<8>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
+  else if (NP == 8 && vec) hipLaunchKernelGGL((gather_payload_quad<4>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
   else if (vec) hipLaunchKernelGGL((gather_payload<NP, true>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
   else hipLaunchKernelGGL((gather_payload<NP, false>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
   return hipGetLastError();
@@ -2366,7 +2431,10 @@ hipError_t launch_gather_payload(const ProbeParams &p, const uint32_t *pos, hipS
 
 hipError_t launch_ordered_walk(const ProbeParams &p, hipStream_t s) {
   if (p.n_chunks == 0) return hipSuccess;
-  hipLaunchKernelGGL((probe_walk<3, true, 4, true>), dim3((unsigned)p.n_chunks), dim3(kFlatThreads), 0, s, p);
+  if (ccj_tune_int("CCJ_OWALK", 1) == 1)
+    hipLaunchKernelGGL((probe_walk1<1, true>), dim3((unsigned)p.n_chunks), dim3(kFlatThreads), 0, s, p);
+  else
+    hipLaunchKernelGGL((probe_walk<3, true, 4, true>), dim3((unsigned)p.n_chunks), dim3(kFlatThreads), 0, s, p);
   return hipGetLastError();
 }
 

@@ -302,6 +302,7 @@ extern "C" int ccj_pipeline_run(ccj_pipeline *pl, const int64_t *const *d_cols, 
     p.table = t->d_table;
     p.off = t->d_off;
     p.bucket = reinterpret_cast<const longlong2 *>(t->d_bucket);
+    p.bucket8 = nullptr;  // the chunk probe reads the 16-byte records (round 0's candidate inside)
     p.mask = (uint32_t)(t->info.size - 1);
     p.keys = in_cols[l];
     p.counts = in_counts;

@@ -31,6 +31,10 @@ for vd in sorted(glob.glob(os.path.join(base, "v*"))):
         if "TCP_TCC_READ_REQ_LATENCY_sum" in c and c.get("TCP_TCC_READ_REQ_sum"):
             d["read_latency_cyc"] = c["TCP_TCC_READ_REQ_LATENCY_sum"] / c["TCP_TCC_READ_REQ_sum"]
             d["reads_in_flight_per_cu"] = c["TCP_TCC_READ_REQ_LATENCY_sum"] / cyc / 256
+        if "SQ_THREAD_CYCLES_VALU" in c and "SQ_ACTIVE_INST_VALU" in c:
+            d["valu_lane_util"] = c["SQ_THREAD_CYCLES_VALU"] / (c["SQ_ACTIVE_INST_VALU"] * 4 * 64)
+        if "SQ_BUSY_CU_CYCLES" in c:
+            d["busy_cu_frac"] = c["SQ_BUSY_CU_CYCLES"] / cyc / 256
         if "SQ_ACTIVE_INST_VALU" in c:
             d["valu_active_per_simd"] = c["SQ_ACTIVE_INST_VALU"] * 4 / cyc / 1024
         if "TCC_HIT_sum" in c:
