@@ -94,11 +94,14 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1 << 28, help="probe keys in the multi-thread CPU sample")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-other", action="store_true", help="C2: do not time the other paths beside the headline")
-    ap.add_argument("--lib", default="product", choices=["product", "tuning"],
-                    help="tuning: libccj_tuning.so (make tuning; A/B sweeps with its env overrides)")
+    ap.add_argument("--lib", default="product",
+                    help="product | tuning (libccj_tuning.so: make tuning; A/B sweeps with its env overrides) | "
+                         "a path to another build of the library (same-box A/B of two source versions)")
     a = ap.parse_args()
     if a.lib == "tuning":
         ccj.LIB_PATH = os.path.join(PKG, "libccj_tuning.so")
+    elif a.lib != "product":
+        ccj.LIB_PATH = os.path.abspath(a.lib)
     return a
 
 

@@ -2346,59 +2346,13 @@ __global__ __launch_bounds__(256) void gather_payload_quad(GatherParams g) {
   }
 }
 
-// gather_payload_quad with the row pieces brought in by LDS-DMA (dma16: lane (r0, q)'s 16 bytes of
-// row ps[u] land at its own 16 bytes of the wave's slot u) and read back from LDS before the column
-// stores.  Round 3: tools/reqpath measures random 32-64 B reads from HBM at ~100 G/s by LDS-DMA
-// against ~53 G/s as vector loads, with half the L2 requests.
-template <int U>
-__global__ __launch_bounds__(256) void gather_payload_dma(GatherParams g) {
-  __shared__ int64_t *s_cols[CCJ_MAX_PAYLOAD_COLS];
-  __shared__ __attribute__((aligned(16))) int64_t s_ring[4 * U * 2 * kWave];
-  if (threadIdx.x < CCJ_MAX_PAYLOAD_COLS) s_cols[threadIdx.x] = g.cols[threadIdx.x];
-  __syncthreads();
-  const uint64_t c = blockIdx.x;
-  const uint64_t ob = g.out_base ? g.out_base[c] : c * g.cap;
-  const uint32_t n = g.count[c];
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  const uint32_t q = threadIdx.x & 3u, r0 = threadIdx.x >> 2;  // 64 rows per block step
-  int64_t *c0 = s_cols[2 * q], *c1 = s_cols[2 * q + 1];
-  int64_t *ring = s_ring + wave * U * 2 * kWave;
-  const uint32_t ring_lds = (uint32_t)__builtin_amdgcn_readfirstlane(
-      (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) int64_t *)ring);
-  for (uint32_t base = 0; base < n; base += 64 * U) {
-    uint32_t ps[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t j = base + u * 64 + r0;
-      ps[u] = g.pos[ob + (j < n ? j : 0u)];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      dma16(g.pay + (uint64_t)ps[u] * g.stride + 2 * q, ring_lds + (uint32_t)u * 1024u);
-    wait_vmcnt<0>();
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const longlong2 v = *reinterpret_cast<const longlong2 *>(ring + u * 2 * kWave + 2 * lane);
-      const uint32_t j = base + u * 64 + r0;
-      if (j < n) {
-        __builtin_nontemporal_store(v.x, c0 + ob + j);
-        __builtin_nontemporal_store(v.y, c1 + ob + j);
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the ring is read before the next DMAs land
-  }
-}
-
 template <int NP>
 hipError_t launch_gather_np(const GatherParams &g, uint64_t n_chunks, hipStream_t s) {
   const bool vec = (g.stride % 2 == 0) && ((uintptr_t)g.pay % 16 == 0);
   // 8 columns: 2 / 4 / 8 rows in flight per lane group 26.9 ms each at C5, the walk's XCD order
   // 27.0, plain instead of non-temporal stores 27.8-28.9 (profiles/r1g_*)
-  if (NP == 8 && vec && ccj_tune_int("CCJ_GATHER_DMA", 1) == 1)
-    hipLaunchKernelGGL((gather_payload_dma<4>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
-  else if (NP == 8 && vec && ccj_tune_int("CCJ_GATHER_DMA", 1) == 2)
-    hipLaunchKernelGGL((gather_payload_dma<8>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
-  else if (NP == 8 && vec) hipLaunchKernelGGL((gather_payload_quad<4>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
+  // (row pieces by LDS-DMA instead: 42.2-42.5 ms per C5 step against 42.2-42.3, round 3)
+  if (NP == 8 && vec) hipLaunchKernelGGL((gather_payload_quad<4>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
   else if (vec) hipLaunchKernelGGL((gather_payload<NP, true>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
   else hipLaunchKernelGGL((gather_payload<NP, false>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
   return hipGetLastError();
