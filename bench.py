@@ -198,7 +198,7 @@ def bench_c3(args, dev, stream):
     n_build, n_probe, chunk = args.n_build, args.n_probe, args.chunk
     t0 = time.perf_counter()
     part_mode = args.path == "partitioned"
-    part = pkeys = None
+    part = pkeys = ws_o = None
     with torch.cuda.stream(stream):
         table = ccj.Table.reference(ccj.CHAIN, n_build, 1, ccj.LAYOUT_DEVICE, stream=stream)
         keys = ccj.gen_c3_keys(n_probe, SEED, n_build, 1, stream=stream)
@@ -207,8 +207,10 @@ def bench_c3(args, dev, stream):
             out = table.alloc_outputs(part["positions"], chunk, rounds=False)
             out["max_rounds"] = 1
             pkeys = part["ws"][:part["positions"] * 8].view(torch.int64)  # the partitioned key column
-        else:
+        else:  # chunk / ordered: the reference's Next results (round-major per chunk), compacted as such
             out = table.alloc_outputs(n_probe, chunk, rounds=True)
+            if args.path == "ordered":
+                ws_o = table.alloc_ordered(n_probe, chunk)
     stream.synchronize()
     log(f"[setup c3] {table.size} buckets, max chain {table.max_rounds}: {time.perf_counter() - t0:.1f} s")
     comp = None
@@ -224,6 +226,8 @@ def bench_c3(args, dev, stream):
             with torch.cuda.stream(stream):  # partition order has no Next boundaries: one result per chunk
                 out["rounds"] = (out["count"] > 0).to(torch.int32)
                 out["round_counts"] = out["count"]
+        elif args.path == "ordered":  # L3 through the bucket-partitioned layout (status read after timing)
+            table.probe_ordered(keys, chunk, out=out, ws=ws_o, stream=stream, retry=False)
         else:
             table.probe(keys, chunk, out=out, stream=stream)
         if ev:
@@ -245,9 +249,10 @@ def bench_c3(args, dev, stream):
     wall = time.perf_counter() - t0
     probe_ms = sum(a.elapsed_time(b) for a, b, _ in evs) / args.steps
     comp_ms = sum(b.elapsed_time(c) for _, b, c in evs) / args.steps
-    if part_mode:
+    if part_mode or args.path == "ordered":
         if int(out["status"].item()) & ccj.FLAG_PART_OVERFLOW:
             raise SystemExit("bench c3: the split's overflow area overflowed")
+    if part_mode:
         matches, l2 = ccj.result_checksum(out, chunk, row_map=part["row_map"].to(torch.int64), stream=stream)
     else:
         matches, l2 = ccj.result_checksum(out, chunk, stream=stream)
@@ -313,6 +318,8 @@ def bench_c3(args, dev, stream):
                      "frac": achieved / HBM_PEAK_GBS, "traffic": c3_traffic,
                      "traffic_GBps": c3_traffic / (probe_ms * 1e-3) / 1e9 if c3_traffic else None,
                      "kernel": ("ccj_probe_partitioned (bucket-range split + probe_chain_win<3>)" if part_mode
+                                else "ccj_probe_ordered (bucket split with runs + chain_words<3> + unsplit_words + "
+                                     "emit_ordered<CHAIN>)" if args.path == "ordered"
                                 else "probe_chunks<CHAIN,2>"),
                      "kernel_ms": probe_ms, "alg_bytes_per_tuple": alg, "chain_keys_per_tuple": n_bar,
                      "m_bar": m_bar},

@@ -719,8 +719,8 @@ struct OrderedLayout {
 
 OrderedLayout ordered_layout(const ccj_table *t, uint64_t n_rows, uint32_t chunk) {
   OrderedLayout O;
-  if (!t || t->info.kind != CCJ_TABLE_LP || t->info.size < kOrderedMinSlots || n_rows == 0 || chunk == 0 ||
-      n_rows >= (1ull << 32))
+  if (!t || t->info.size < kOrderedMinSlots || n_rows == 0 || chunk == 0 || n_rows >= (1ull << 32) ||
+      (t->info.kind == CCJ_TABLE_CHAIN && !t->d_bucket))
     return O;
   O.L = part_layout(t, n_rows, chunk);
   // the split's run records and the unsplit address positions as u32: beyond 2^32 positions
@@ -798,7 +798,7 @@ int ccj_probe_ordered(const ccj_table *t, const ccj_probe_args *a, void *ws, siz
   // words' three HBM crossings: walk -> unsplit -> emit)
   const uint32_t w16 = t->info.max_dup <= 1 && ccj_tune_int("CCJ_W16", 1) ? 1u : 0u;
   q.w16 = w16;
-  HIP_TRY(ccj::launch_ordered_walk(q, s), "ordered walk");
+  HIP_TRY(ccj::launch_ordered_walk(t->info.kind, q, s), "ordered walk");
   // 3. the words back into row order, one split tile per workgroup
   HIP_TRY(ccj::launch_unsplit_words(runs, ovf_runs, reinterpret_cast<const uint16_t *>(row_map), w_pos, w_row,
                                     a->n_rows, L.parts, O.tile, a->status, s,
@@ -808,7 +808,7 @@ int ccj_probe_ordered(const ccj_table *t, const ccj_probe_args *a, void *ws, siz
   p.in_w = w_row;
   p.w16 = w16;
   p.xcd_swizzle = 0;
-  HIP_TRY(ccj::launch_ordered_emit(p, s), "ordered emit");
+  HIP_TRY(ccj::launch_ordered_emit(t->info.kind, p, s), "ordered emit");
   return CCJ_OK;
 }
 

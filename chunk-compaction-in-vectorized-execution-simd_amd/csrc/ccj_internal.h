@@ -121,14 +121,14 @@ constexpr uint32_t kEmitWave = 0xFFFFFFFFu;
 // Launchers (ccj_kernels.hip).  Return hipError_t of the launch.
 hipError_t launch_probe(int kind, const ProbeParams &p, hipStream_t s);
 hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s);
-// Ordered probe (ccj_probe_ordered, LP): walk of the slot-partitioned column leaving each row's
-// round word at its position (p.out_w); the words back into row order, one split tile per
-// workgroup; the reference-order emit of each chunk from its rows' words (p.in_w).
-hipError_t launch_ordered_walk(const ProbeParams &p, hipStream_t s);
+// Ordered probe (ccj_probe_ordered, LP or chaining): walk of the slot / bucket partitioned column
+// leaving each row's round word at its position (p.out_w); the words back into row order, one
+// split tile per workgroup; the reference-order emit of each chunk from its rows' words (p.in_w).
+hipError_t launch_ordered_walk(int kind, const ProbeParams &p, hipStream_t s);
 hipError_t launch_unsplit_words(const uint2 *runs, const uint32_t *ovf_runs, const uint16_t *row_loc,
                                 const void *w_pos, void *w_row, uint64_t n, uint32_t parts, uint32_t tile,
                                 uint32_t *status, hipStream_t s, bool w16);
-hipError_t launch_ordered_emit(const ProbeParams &p, hipStream_t s);
+hipError_t launch_ordered_emit(int kind, const ProbeParams &p, hipStream_t s);
 // C5 payload columns of a finished probe: out_cols[q][slot] = payload row of pos[slot], column q.
 hipError_t launch_gather_payload(const ProbeParams &p, const uint32_t *pos, hipStream_t s);
 hipError_t launch_gen_reference_keys(int64_t *out, uint64_t first, uint64_t n, uint64_t n_total, uint64_t cf,

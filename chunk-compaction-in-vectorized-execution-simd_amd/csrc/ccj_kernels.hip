@@ -1355,6 +1355,126 @@ __global__ __launch_bounds__(kFlatThreads) void probe_chain_win(ProbeParams p) {
   if (p.status && (overflow || total > p.cap)) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
 }
 
+// Ordered probe of a chaining table (ccj_probe_ordered), step 2: probe_chain_win's walk of the
+// bucket-partitioned column, leaving each row's Next-round word at its position instead of emitting
+// matches.  The reference walks a row's whole chain, one node per Next round
+// (chaining_ht.cpp:60-80, :109-124), so the row's rounds are its chain length L and bit r of mm says
+// chain node r equals the key (chaining_ht.cpp:88-99); an empty bucket's row has no rounds (:52-55).
+// Word: mm | L << 26, or kMmLong | L for chains longer than 26 (the emit re-walks that chunk round
+// by round); 16-bit words (p.w16) for distinct build keys.  The words are staged in LDS and
+// written out coalesced.
+template <int R>
+__global__ __launch_bounds__(kFlatThreads) void chain_words(ProbeParams p) {
+  __shared__ int64_t s_key[kMaxChunk];
+  __shared__ uint32_t s_w[kMaxChunk];
+  __shared__ uint32_t s_next;
+  const uint32_t tid = threadIdx.x;
+  uint64_t c = blockIdx.x;
+  if (p.xcd_swizzle) {
+    const uint64_t n8 = (p.swz_chunks ? p.swz_chunks : p.n_chunks) & ~7ull;
+    if (c < n8) c = (c & 7) * (n8 >> 3) + (c >> 3);
+  }
+  const uint64_t base = c * p.chunk;
+  const uint32_t phys = flat_phys(p, base);
+  stage_keys(s_key, p.keys + base, phys, tid);
+  if (tid == 0) s_next = kFlatThreads * R;
+  __syncthreads();
+  int64_t key[R];
+  uint32_t row[R], cur[R], lim[R], st0[R], kfp[R], mm[R];
+  uint32_t need = 0, fresh = 0;
+  const bool rec8 = p.bucket8 != nullptr;
+  auto start = [&](int k, uint32_t i) {
+    row[k] = i;
+    mm[k] = 0;
+    if (i < phys) {
+      key[k] = s_key[i];
+      const uint64_t h = murmurhash64((uint64_t)key[k]);
+      cur[k] = (uint32_t)h & p.mask;
+      kfp[k] = bucket_fp(h);
+      need |= 1u << k;
+      fresh |= 1u << k;
+    }
+  };
+  auto word = [&](int k) {
+    const uint32_t L = lim[k] - st0[k];
+    s_w[row[k]] = L <= kMmRounds ? (mm[k] & ((1u << kMmRounds) - 1u)) | L << kMmRounds : kMmLong | L;
+  };
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    key[k] = 0;
+    cur[k] = lim[k] = st0[k] = kfp[k] = 0;
+    start(k, (uint32_t)k * kFlatThreads + tid);
+  }
+  while (__ballot(need != 0u) != 0ull) {
+    longlong2 v[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {  // unconditional (an idle row reads bucket 0): no wait per load
+      const bool nd = (need >> k) & 1u, fr = (fresh >> k) & 1u;
+      const longlong2 *src = nd && !fr ? reinterpret_cast<const longlong2 *>(p.table + (cur[k] & ~1u))
+                             : rec8    ? reinterpret_cast<const longlong2 *>(p.bucket8 + (nd ? cur[k] & ~1u : 0u))
+                                       : p.bucket + (nd ? cur[k] : 0u);
+      v[k] = *src;
+    }
+    uint32_t done = 0;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      if ((need >> k) & 1u) {
+        if ((fresh >> k) & 1u) {
+          fresh &= ~(1u << k);
+          const uint64_t r = rec8 ? (uint64_t)((cur[k] & 1u) ? v[k].y : v[k].x) : (uint64_t)v[k].x;
+          const uint32_t st = (uint32_t)r, len = rec8 ? (uint32_t)(r >> 32) & 0xFFFFu : (uint32_t)(r >> 32);
+          st0[k] = st;
+          lim[k] = st + len;
+          if (len == 0) {
+            done |= 1u << k;  // empty bucket: no rounds
+          } else if (rec8) {
+            const bool skip = (uint32_t)(r >> 48) != kfp[k];  // not the first node: round 0 without a read
+            cur[k] = skip ? st + 1 : st;
+            if (skip && len == 1) done |= 1u << k;
+          } else {
+            mm[k] |= v[k].y == key[k] ? 1u : 0u;  // round 0 from the record's first key
+            cur[k] = st + 1;
+            if (len == 1) done |= 1u << k;
+          }
+        } else {
+          const uint32_t blk = cur[k] & ~1u;
+          const uint32_t r0 = blk - st0[k];  // chain node blk's round (node blk + 1: r0 + 1)
+          if (cur[k] == blk && v[k].x == key[k] && r0 < 32u) mm[k] |= 1u << r0;
+          if (blk + 1 < lim[k] && v[k].y == key[k] && r0 + 1 < 32u) mm[k] |= 1u << (r0 + 1);
+          cur[k] = blk + 2;
+          if (cur[k] >= lim[k]) done |= 1u << k;
+        }
+      }
+    }
+    const uint32_t nd = (uint32_t)__builtin_popcount(done);
+    uint32_t dpre = 0, dtot = 0;
+#pragma unroll
+    for (int b = 0; (1 << b) <= R; ++b) {
+      const uint64_t bm = __ballot((nd >> b) & 1u);
+      dpre += lane_prefix(bm) << b;
+      dtot += (uint32_t)__popcll(bm) << b;
+    }
+    if (dtot) {
+      uint32_t rb = 0;
+      if ((tid & (kWave - 1)) == 0) rb = atomicAdd(&s_next, dtot);
+      rb = (uint32_t)__builtin_amdgcn_readfirstlane((int)rb) + dpre;
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        if ((done >> k) & 1u) {
+          need &= ~(1u << k);
+          word(k);
+          start(k, rb++);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < phys; i += kFlatThreads) {  // the rows' words, coalesced at their positions
+    if (p.w16) __builtin_nontemporal_store(round_word16(s_w[i]), (uint16_t *)p.out_w + base + i);
+    else __builtin_nontemporal_store(s_w[i], p.out_w + base + i);
+  }
+}
+
 // probe_walk: the LP walk of slot-partitioned input, one wave per 512-row quarter of a chunk,
 // no per-step output bookkeeping.  Each wave stages its own rows' keys (and, with
 // HOME, their home slots) in LDS; its lanes walk rows through 32-byte windows from the row's next
@@ -1950,6 +2070,7 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk1(ProbeParams p) {
 // output is exactly ccj_probe's.  A chunk with a row of more than 26 rounds re-walks round by
 // round (rounds_generic).  LDS: s_off (4 KB) plus the staged output (s_osel 8 KB + s_opay 16 KB),
 // about 28 KB per workgroup: 5 workgroups per CU (round 2d: 8 before the output was staged).
+template <int KIND>
 __global__ __launch_bounds__(kBlock) void emit_ordered(ProbeParams p) {
   constexpr int kQ = kMaxChunk / kBlock;  // 8 rows per thread
   __shared__ uint32_t s_off[kMaxFastRounds * 32];
@@ -2034,7 +2155,7 @@ __global__ __launch_bounds__(kBlock) void emit_ordered(ProbeParams p) {
       uint32_t act_all = 0;
       for (uint32_t j = 0; j < nj; ++j)
         if (j * kWave + lane < count) act_all |= 1u << j;
-      rounds_generic<CCJ_TABLE_LP>(p, c, base, nj, act_all, p.keys + base, flags, total, rounds);
+      rounds_generic<KIND>(p, c, base, nj, act_all, p.keys + base, flags, total, rounds);
     }
   } else {
     // Count: matches per (round r, row group j = 4q + wave).
@@ -2383,9 +2504,12 @@ hipError_t launch_gather_payload(const ProbeParams &p, const uint32_t *pos, hipS
   }
 }
 
-hipError_t launch_ordered_walk(const ProbeParams &p, hipStream_t s) {
+hipError_t launch_ordered_walk(int kind, const ProbeParams &p, hipStream_t s) {
   if (p.n_chunks == 0) return hipSuccess;
-  if (ccj_tune_int("CCJ_OWALK", 1) == 1)
+  if (kind == CCJ_TABLE_CHAIN) {
+    if (!p.bucket) return hipErrorInvalidValue;  // every chaining table carries bucket records
+    hipLaunchKernelGGL((chain_words<3>), dim3((unsigned)p.n_chunks), dim3(kFlatThreads), 0, s, p);
+  } else if (ccj_tune_int("CCJ_OWALK", 1) == 1)
     hipLaunchKernelGGL((probe_walk1<1, true>), dim3((unsigned)p.n_chunks), dim3(kFlatThreads), 0, s, p);
   else
     hipLaunchKernelGGL((probe_walk<3, true, 4, true>), dim3((unsigned)p.n_chunks), dim3(kFlatThreads), 0, s, p);
@@ -2407,9 +2531,12 @@ hipError_t launch_unsplit_words(const uint2 *runs, const uint32_t *ovf_runs, con
   return hipGetLastError();
 }
 
-hipError_t launch_ordered_emit(const ProbeParams &p, hipStream_t s) {
+hipError_t launch_ordered_emit(int kind, const ProbeParams &p, hipStream_t s) {
   if (p.n_chunks == 0) return hipSuccess;
-  hipLaunchKernelGGL(emit_ordered, dim3((unsigned)p.n_chunks), dim3(kBlock), 0, s, p);
+  if (kind == CCJ_TABLE_CHAIN)
+    hipLaunchKernelGGL(emit_ordered<CCJ_TABLE_CHAIN>, dim3((unsigned)p.n_chunks), dim3(kBlock), 0, s, p);
+  else
+    hipLaunchKernelGGL(emit_ordered<CCJ_TABLE_LP>, dim3((unsigned)p.n_chunks), dim3(kBlock), 0, s, p);
   return hipGetLastError();
 }
 

@@ -151,13 +151,16 @@ typedef struct ccj_probe_args {
 int ccj_probe(const ccj_table *table, const ccj_probe_args *args, ccj_stream stream);
 
 /* Same outputs as ccj_probe — every chunk's per-Next stream in the reference's order (L3) — for
- * large LP tables (>= 2^22 slots) with sel == NULL, computed through the slot-partitioned layout:
- *   1. the one-pass slot split of the live rows (as ccj_probe_partitioned), which also records
- *      where every split tile's run of every partition went;
+ * large tables (LP: >= 2^22 slots; chaining: >= 2^22 buckets) with sel == NULL, computed through
+ * the slot / bucket partitioned layout:
+ *   1. the one-pass split of the live rows (as ccj_probe_partitioned), which also records where
+ *      every split tile's run of every partition went;
  *   2. a walk with the table window L2-resident that leaves each row's Next-round word (the
- *      rounds in which it matches + its round count) at its partitioned position;
+ *      rounds in which it matches + its round count: the run length, or the chain length) at its
+ *      partitioned position;
  *   3. the words back into row order, one split tile per workgroup;
- *   4. per chunk, the round-major / idx-ascending emit of linear_probing_ht.cpp:62-115 from them.
+ *   4. per chunk, the round-major / idx-ascending emit of linear_probing_ht.cpp:62-115 /
+ *      chaining_ht.cpp:60-124 from them.
  * Random slot reads become L2 hits instead of 128-byte HBM lines (C2: 1.24 lines per probe row on
  * ccj_probe).  Other tables, sel != NULL, out_pos or payload columns run ccj_probe itself and need
  * no workspace.  The partitioned route needs args->status: CCJ_FLAG_PART_OVERFLOW there (extreme

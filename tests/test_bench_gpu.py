@@ -42,10 +42,13 @@ def test_bench_c2_ordered_headline():
     assert line["path"] == "ordered" and line["parity"]["l1_ok"] and line["parity"]["l2_ok"]
 
 
-def test_bench_c3():
-    line = run_bench("--workload", "c3")
+@pytest.mark.parametrize("path", ["partitioned", "ordered", "chunk"])
+def test_bench_c3(path):
+    """C3 on every path; the ordered and chunk paths compact the reference's real Next results."""
+    line = run_bench("--workload", "c3", "--path", path)
     par = line["parity"]
     assert par["status_flags"] == 0 and par["l1_ok"] and par["l2_ok"] and par["compaction_keeps_all"]
+    assert line["path"] == path
 
 
 def test_bench_c5():

@@ -418,6 +418,42 @@ def test_ordered_probe_equals_chunk_probe(layout, n_build, cf, n_probe, rng, chu
     assert np.array_equal(got["payload"].reshape(-1, cap)[valid], want["payload"].reshape(-1, cap)[valid])
 
 
+@pytest.mark.parametrize("n_build,cf,n_probe,chunk,ragged,c3", [
+    (1 << 21, 1, 1 << 22, 2048, False, True),    # C3's stream: 10 % Zipf hits, 90 % misses
+    (1 << 21, 3, 3000000, 2048, True, True),     # duplicate keys (32-bit round words), ragged chunks
+    (1 << 21, 1, 999999, 1000, True, False),     # uniform hits, odd chunk width, ragged
+    (1 << 21, 1, 1 << 21, 256, False, False),    # the reference's default chunk
+    (1 << 21, 40, 1 << 20, 2048, False, False),  # chains longer than 26 nodes: re-walked chunks
+])
+def test_ordered_probe_chaining_equals_chunk_probe(n_build, cf, n_probe, chunk, ragged, c3):
+    """ccj_probe_ordered on a chaining table (bucket split -> round words from the chain walk ->
+    back to row order -> emit) gives exactly probe_chunks<CHAIN>'s outputs: per-chunk counts,
+    rounds, every Next's count and the ordered (sel, payload) stream (L3)."""
+    table = ccj.Table.reference(ccj.CHAIN, n_build, cf, ccj.LAYOUT_REFERENCE)
+    assert table.size >= 1 << 22
+    keys = (ccj.gen_c3_keys(n_probe, 29, n_build, cf) if c3 else
+            ccj.gen_uniform_keys(n_probe, 31, n_build * 2 // cf + 1))
+    counts = None
+    if ragged:
+        n_chunks = -(-n_probe // chunk)
+        g = np.random.default_rng(cf + 7)
+        c = g.integers(0, chunk + 1, size=n_chunks).astype(np.int32)
+        c[::5] = chunk
+        c[-1] = min(c[-1], n_probe - (n_chunks - 1) * chunk)
+        counts = to_dev(c)
+    want = host(table.probe(keys, chunk, counts=counts))
+    got = host(table.probe_ordered(keys, chunk, counts=counts))
+    assert got["status"][0] == 0 and want["status"][0] == 0 and not got.get("exact_retry")
+    assert want["count"].sum() > 0
+    assert np.array_equal(got["count"], want["count"])
+    assert np.array_equal(got["rounds"], want["rounds"])
+    assert np.array_equal(got["round_counts"], want["round_counts"])
+    cap = want["cap"]
+    valid = np.arange(cap)[None, :] < want["count"].astype(np.int64)[:, None]
+    assert np.array_equal(got["sel"].reshape(-1, cap)[valid], want["sel"].reshape(-1, cap)[valid])
+    assert np.array_equal(got["payload"].reshape(-1, cap)[valid], want["payload"].reshape(-1, cap)[valid])
+
+
 def test_ordered_probe_c2_table_reference_vector():
     """ccj_probe_ordered on the reference-order 2^26-key table against the reference's own vector
     (SURVEY §4 survey_lp_2048_64M_64M): matches, L2, the ordered L3 fold, the SURVEY checksum."""
