@@ -115,6 +115,28 @@ def cpu_model():
     return platform.processor()
 
 
+def physical_cores():
+    """Distinct (socket, core) pairs in /proc/cpuinfo (the host's physical cores), or None."""
+    try:
+        cores, phys = set(), None
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                phys = line.split(":", 1)[1].strip()
+            elif line.startswith("core id"):
+                cores.add((phys, line.split(":", 1)[1].strip()))
+        return len(cores) or None
+    except OSError:
+        return None
+
+
+def cpu_share():
+    """CPUs this process may use (the GPU box grants one GPU's share of the host: 16)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count()
+
+
 REF_DRIVER = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
 
 
@@ -167,6 +189,11 @@ def cpu_baseline(args):
     v1, n1, dt1, _ = res[1]
     port = {
         "value": v, "unit": "probe tuples/s", "cores": thr, "kind": "port",
+        "host": {"cpu_model": cpu_model(), "logical_cpus": os.cpu_count(), "physical_cores": physical_cores(),
+                 "cpus_granted": cpu_share(),
+                 "note": ("the GPU box grants one GPU's share of the host's CPUs (OMP_NUM_THREADS / MAX_JOBS = 16 "
+                          "there; at most that many worker processes or threads are allowed), so the port runs "
+                          "--cpu-threads (16) threads, not every physical core")},
         "sample": (f"first {n} of the same 2^30-key uniform probe stream (seed {SEED}) against the same "
                    f"{args.n_build}-key LP table built on the host, chunk {args.chunk}, {thr} threads "
                    f"(one per contiguous chunk range), {dt:.2f} s; 1 thread on {n1} keys: "
