@@ -46,10 +46,10 @@ METRIC = "probe tuples/sec + achieved HBM GB/s, 1B-row int64 join at 1/2/4/8 GPU
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
 SEED = 42
 PATH_KERNELS = {
-    "partitioned": "ccj_probe_partitioned, CCJ_PART_ROWS (slot_split_pipe writing keys + rows into the outputs, probe_walk<3>)",
+    "partitioned": "ccj_probe_partitioned, CCJ_PART_ROWS (slot_split_pipe writing keys + rows into the outputs, probe_walk1<1>: one lane per row, LDS-DMA table windows)",
     "rank": "ccj_probe_partitioned, CCJ_PART_ROWS | CCJ_PART_RANK (slot_split_pipe + probe_rank: the window's occupancy "
             "bitmap + rank in LDS, keys from the compact array; rank_finish) — opt-in, A/B",
-    "ordered": "ccj_probe_ordered (slot_split_pipe with runs + probe_walk<3,MM> + unsplit_words + emit_ordered, 16-bit round words)",
+    "ordered": "ccj_probe_ordered (slot_split_pipe with runs + probe_walk1<1,MM> + unsplit_words + emit_ordered, 16-bit round words)",
     "chunk": "ccj_probe (probe_chunks<LP,2>)",
 }
 
@@ -68,6 +68,9 @@ def parse():
     ap.add_argument("--group", type=int, default=None,
                     help="N > 1: received batches per local probe (each local probe sweeps the whole table); "
                          "default ccj_dist.GROUP")
+    ap.add_argument("--cu-split", default=None,
+                    help="N > 1: 'P,Q' = groups of 8 CUs (of 32) for the local probe's and the owner split's "
+                         "streams (the rest stay free for RCCL); '0,0' = unmasked; default ccj_dist.CU_SPLIT")
     ap.add_argument("--ops-module", default=None,
                     help=argparse.SUPPRESS)  # tests only: a module whose make_ops() replaces the HIP ops (CPU, gloo)
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"], help=argparse.SUPPRESS)
@@ -761,8 +764,9 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
     t0 = time.perf_counter()
     if ops is None:
         with torch.cuda.stream(stream):
-            sp = ccj_dist.ShardedProbe(n_build_total, 1, n_probe, chunk, world, rank, stream=stream,
-                                       batches=args.batches, group=group)
+            cu_split = tuple(int(x) for x in args.cu_split.split(",")) if args.cu_split else None
+            sp = ccj_dist.ShardedProbe(n_build_total, 1, n_probe, chunk, world, rank, batches=args.batches,
+                                       group=group, ops=ccj_dist.DeviceOps(cu_split=cu_split))
             keys = ccj.gen_uniform_keys(n_probe, SEED, n_build_total, first_row=rank * n_probe, stream=stream)
     else:
         sp = ccj_dist.ShardedProbe(n_build_total, 1, n_probe, chunk, world, rank, batches=args.batches, ops=ops,
@@ -772,16 +776,17 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
     o.synchronize()
     log(f"[rank {rank}] setup {time.perf_counter() - t0:.1f} s, local build {sp.n_build_local}, "
         f"{sp.batches} batches in groups of {sp.group}, segment capacity {sp.seg_cap}")
-    for _ in range(args.warmup):
-        sp.step(keys, rank * n_probe)
+    if args.warmup:
+        sp.run(keys, rank * n_probe, steps=args.warmup)
     o.synchronize()
     dist.barrier()
     o.synchronize()
     sp.reset_timing()
     exact_before = sp.exact_steps
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        sp.step(keys, rank * n_probe, timing=True)
+    # the K steps are issued back to back (ShardedProbe.run): step s + 1's partitions and exchanges
+    # overlap step s's last local probe, and the ranks agree on the status word once, at the end
+    sp.run(keys, rank * n_probe, steps=args.steps, timing=True)
     o.synchronize()
     dist.barrier()
     wall = time.perf_counter() - t0
@@ -833,6 +838,7 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
                                    f"{world * n_probe} probe int64, chunk=2048, RCCL all-to-all tuple shuffle",
                        "table": "linear_probing", "n_build_total": n_build_total, "n_probe_per_gpu": n_probe,
                        "chunk": chunk, "batches": sp.batches, "group": sp.group,
+                       "steps_pipelined": "the K steps issued back to back, one status agreement after them",
                        "parallelism": f"dp{world} (owner-partitioned)"},
             # per step, slowest rank; the three streams overlap, so these are busy times, not a sum
             "partition_ms": phase["partition_ms"], "exchange_ms": phase["exchange_ms"],

@@ -69,7 +69,8 @@ EXPORTS = ["ccj_last_error", "ccj_abi_version", "ccj_device_init", "ccj_table_bu
            "ccj_pipeline_run", "ccj_pipeline_free", "ccj_pipeline_checksum", "ccj_partition_by_owner_fixed",
            "ccj_segment_chunk_counts", "ccj_pipeline_set_thresholds", "ccj_gen_c3_keys",
            "ccj_partition_grouped_workspace_size", "ccj_partition_by_owner_grouped", "ccj_partition_grouped_sub_cap",
-           "ccj_probe_ordered_workspace_size", "ccj_probe_ordered", "ccj_probe_visits"]
+           "ccj_probe_ordered_workspace_size", "ccj_probe_ordered", "ccj_probe_visits",
+           "ccj_stream_create_cu_masked", "ccj_stream_destroy", "ccj_device_cus"]
 
 MAX_JOINS = 8
 COMPACT_NONE, COMPACT_FULL = 0, 1
@@ -141,6 +142,9 @@ def lib():
         L.ccj_pipeline_free.argtypes = [vp]
         L.ccj_pipeline_set_thresholds.argtypes = [vp, vp]
         L.ccj_pipeline_checksum.argtypes = [C.POINTER(PipelineResult), C.c_uint32, vp, vp]
+        L.ccj_stream_create_cu_masked.argtypes = [C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(vp)]
+        L.ccj_stream_destroy.argtypes = [vp]
+        L.ccj_device_cus.argtypes = [C.POINTER(C.c_uint32)]
         _lib = L
     return _lib
 
@@ -564,6 +568,36 @@ class GroupedOwnerPartitioner:
 def grouped_sub_cap(n: int, parts: int, chunk: int) -> int:
     """Sub-segment capacity for GroupedOwnerPartitioner over n uniformly hashed keys."""
     return int(lib().ccj_partition_grouped_sub_cap(n, parts, chunk))
+
+
+def device_cus() -> int:
+    n = C.c_uint32(0)
+    check(lib().ccj_device_cus(C.byref(n)), "ccj_device_cus")
+    return int(n.value)
+
+
+def cu_mask_groups(groups, n_cus: int | None = None, period: int = 32):
+    """CU mask (list of u32 words) of the CUs i with (i // 8) % period in `groups`: each group is 8
+    consecutive CU numbers (one per XCD where HIP deals CU numbers to the XCDs in turn, a
+    contiguous eighth of an XCD's CUs otherwise), so a set of groups spreads over all eight XCDs."""
+    n_cus = n_cus or device_cus()
+    words = [0] * ((n_cus + 31) // 32)
+    for i in range(n_cus):
+        if (i // 8) % period in groups:
+            words[i // 32] |= 1 << (i % 32)
+    return words
+
+
+def cu_masked_stream(mask_words):
+    """A torch stream confined to the CUs of `mask_words` (ccj_stream_create_cu_masked); the
+    library's persistent kernels launched on it size their grid to those CUs."""
+    import torch
+    arr = (C.c_uint32 * len(mask_words))(*mask_words)
+    h = C.c_void_p()
+    check(lib().ccj_stream_create_cu_masked(arr, len(mask_words), C.byref(h)), "ccj_stream_create_cu_masked")
+    st = torch.cuda.ExternalStream(h.value)
+    st._ccj_handle = h  # destroyed with ccj_stream_destroy by the owner, if ever (streams live per process)
+    return st
 
 
 def segment_chunk_counts(seg_counts, seg_cap: int, chunk: int, out, status, stream=None):

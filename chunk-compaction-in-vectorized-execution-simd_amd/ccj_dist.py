@@ -15,10 +15,11 @@ HIP streams (partition, comm, probe) with double-buffered send/receive slots:
 
 Overflow.  Three things can overflow under key skew, each raising a flag in the rank's status
 word: a send segment of the owner split, a receive segment's count, and the local probe's own
-one-pass slot split or output capacity (its args->status IS the same word).  At the end of a step
-the word is all-reduced with MAX, so every rank sees the same value and takes the same branch:
-either all return, or all redo the step with the exact-size protocol (exchange(): host-side split
-sizes, 16 B per tuple) — the ranks' collective sequences never diverge.
+one-pass slot split or output capacity (its args->status IS the same word).  At the end of a run
+(one or more steps issued back to back, ShardedProbe.run) the word is all-reduced with MAX, so
+every rank sees the same value and takes the same branch: either all return, or all redo the run's
+steps with the exact-size protocol (exchange(): host-side split sizes, 16 B per tuple) — the
+ranks' collective sequences never diverge.
 
 The step's control flow is written against an `ops` object: DeviceOps (below) runs the HIP kernels
 on torch.cuda streams; tests/test_dist_cpu.py drives the SAME ShardedProbe with gloo on CPU
@@ -92,16 +93,32 @@ def agree_status(status, group=None) -> int:
     return int(st.item())
 
 
+# CU split of the pipelined step, in groups of 8 CUs out of 32 (ccj.cu_mask_groups): the local
+# probe's stream, the owner split's stream; the groups in neither stay free for RCCL's kernels.
+# Without masks a local probe of ~3 * 10^5 workgroups holds every CU until it drains, and the owner
+# split (one 149 KB-LDS workgroup per CU) and RCCL's kernels wait for it: no overlap at all
+# (round-3 kernel trace of the one-rank rehearsal).  (0, 0): unmasked streams — the
+# default until a split measures faster (one-rank rehearsal: 31.4 ms unmasked, 48.7 at (24, 8)).
+CU_SPLIT = (0, 0)
+
+
 class DeviceOps:
     """The HIP kernels (libccj.so) and torch.cuda streams/events one rank's step runs on."""
 
-    def __init__(self):
+    def __init__(self, cu_split=None):
         import ccj
         self.ccj = ccj
         self.device = torch.device("cuda", torch.cuda.current_device())
+        self.cu_split = tuple(CU_SPLIT if cu_split is None else cu_split)
 
     # streams and events
-    def stream(self):
+    def stream(self, role=None):
+        """A stream for `role` ("probe", "partition"; None: any CUs)."""
+        probe_g, part_g = self.cu_split
+        if role and probe_g + part_g > 0:
+            groups = range(probe_g) if role == "probe" else range(probe_g, probe_g + part_g)
+            if role in ("probe", "partition") and len(groups):
+                return self.ccj.cu_masked_stream(self.ccj.cu_mask_groups(set(groups)))
         return torch.cuda.Stream(device=self.device)
 
     def event(self, timing=False):
@@ -195,9 +212,9 @@ class ShardedProbe:
         self.ops = ops or DeviceOps()
         o = self.ops
         self.world, self.rank, self.chunk, self.n_probe = world, rank, chunk, n_probe
-        self.stream = stream or o.stream()
+        self.stream = stream or o.stream("probe")
         self.comm = o.stream()
-        self.pstream = o.stream()  # partitions run beside the previous probe
+        self.pstream = o.stream("partition")  # partitions run beside the previous probe
         self.n_build_local = o.build_local(n_build_total, cf, world, rank, self.stream)
         # batched, fixed-capacity exchange buffers: two send slots; receive buffers of `group`
         # batches each, two of them, so one group is probed while the next one arrives
@@ -248,9 +265,14 @@ class ShardedProbe:
         lo = i * self.bn
         return lo, min(self.bn, self.n_probe - lo)
 
-    def _recv(self, i):
-        """Receive views of batch i: (group slot, keys, rows, counts)."""
-        gs, sub = (i // self.group) % 2, i % self.group
+    def _gslot(self, j):
+        """Receive group slot of run batch j (batch j % batches of step j // batches): the groups of a
+        run alternate between the two slots, across step boundaries too."""
+        return ((j // self.batches) * self.n_groups + (j % self.batches) // self.group) % 2
+
+    def _recv(self, j):
+        """Receive views of run batch j: (group slot, keys, rows, counts)."""
+        gs, sub = self._gslot(j), (j % self.batches) % self.group
         lo = sub * self.slots
         return (gs, self.rk[gs][lo:lo + self.slots], self.rr[gs][lo:lo + self.slots],
                 self.rc[gs][sub * self.nseg:(sub + 1) * self.nseg])
@@ -273,9 +295,9 @@ class ShardedProbe:
             events.append((a, b))
         return span()
 
-    def _partition(self, keys, i, timing=False):
-        s = i % 2
-        lo, n = self._batch(i)
+    def _partition(self, keys, j, timing=False):
+        s = j % 2
+        lo, n = self._batch(j % self.batches)
         if n not in self.fparts:
             self.fparts[n] = self.ops.fixed_partitioner(n, self.world, self.sub_cap)
         self.pstream.wait_event(self.ev_comm[s])  # the previous all-to-all from send slot s is done
@@ -283,11 +305,11 @@ class ShardedProbe:
             self.fparts[n](keys[lo:lo + n], lo, self.sk[s], self.sr[s], self.sc[s], self.status, self.pstream)
         self.ev_part[s].record(self.pstream)
 
-    def _exchange(self, i, timing=False):
-        s = i % 2
-        gs, rk, rr, rc = self._recv(i)
+    def _exchange(self, j, timing=False):
+        s = j % 2
+        gs, rk, rr, rc = self._recv(j)
         self.comm.wait_event(self.ev_part[s])
-        if i % self.group == 0:
+        if (j % self.batches) % self.group == 0:
             self.comm.wait_event(self.ev_probe[gs])  # the previous probe of receive group slot gs is done
         with self.ops.on(self.comm), self._timed(self.comm_events, self.comm, timing):
             exchange_fixed(self.sk[s], self.sr[s], self.sc[s], rk, rr, rc)
@@ -317,12 +339,13 @@ class ShardedProbe:
     def _group_range(self, g):
         return g * self.group, min((g + 1) * self.group, self.batches) - 1
 
-    def _probe(self, g, timing):
-        """Probe group g (batches g*group ... its last one, all exchanged in order on comm)."""
+    def _probe(self, j0, g, timing):
+        """Probe group g of the step whose first run batch is j0 (batches g*group ... its last one,
+        all exchanged in order on comm)."""
         o = self.ops
-        gs = g % 2
         first, last = self._group_range(g)
-        self.stream.wait_event(self.ev_comm[last % 2])
+        gs = self._gslot(j0 + first)
+        self.stream.wait_event(self.ev_comm[(j0 + last) % 2])
         per = self.slots // self.chunk
         for i in range(first, last + 1):
             sub = i % self.group
@@ -340,12 +363,13 @@ class ShardedProbe:
             self.probe_events.append((a, b))
         self.ev_probe[gs].record(self.stream)
 
-    def group_row_map(self, g):
-        gs = g % 2
+    def group_row_map(self, j0, g):
+        gs = self._gslot(j0 + self._group_range(g)[0])
         return self.ops.group_rows(self.parts[gs], self.rr[gs], self.n_probe, self.seg_cap, self.slots, self.stream)
 
     def received_keys(self, i):
-        """Batch i's received keys without the segment padding (work accounting)."""
+        """Batch i's received keys (of the last run's first step: call after a one-step run) without
+        the segment padding (work accounting)."""
         gs, rk, rr, rc = self._recv(i)
         self.ops.current().wait_event(self.ev_comm[i % 2])
         pos = torch.arange(self.slots, device=rk.device)
@@ -355,25 +379,35 @@ class ShardedProbe:
     def step(self, keys, row_base: int = 0, timing: bool = False, verify: bool = False):
         """One pass over this rank's keys.  verify=True returns (matches, l2) of this rank's probes
         (global rows: source rank * n_probe + local row)."""
+        return self.run(keys, row_base, 1, timing, verify)
+
+    def run(self, keys, row_base: int = 0, steps: int = 1, timing: bool = False, verify: bool = False):
+        """`steps` passes over this rank's keys, issued back to back: the batches of step s + 1 are
+        partitioned and exchanged while step s's last group is probed (no drain between steps), and
+        the status word is agreed on once, after the last step.  If any rank saw an overflow, every
+        rank redoes all `steps` passes with the exact-size protocol.  verify=True returns (matches,
+        l2) summed over the steps."""
         o = self.ops
-        assert keys.numel() == self.n_probe and row_base == self.rank * self.n_probe
+        assert keys.numel() == self.n_probe and row_base == self.rank * self.n_probe and steps >= 1
         cur = o.current()
         with o.on(cur):
             self.status.zero_()
         self.stream.wait_stream(cur)
         self.pstream.wait_stream(cur)
+        total = steps * self.batches  # run batches j: batch j % batches of step j // batches
         self._partition(keys, 0, timing)
         self._exchange(0, timing)
         m, l2 = 0, 0
-        for i in range(self.batches):
-            if i + 1 < self.batches:
-                self._partition(keys, i + 1, timing)
-                self._exchange(i + 1, timing)
+        for j in range(total):
+            if j + 1 < total:
+                self._partition(keys, j + 1, timing)
+                self._exchange(j + 1, timing)
+            i, j0 = j % self.batches, j - j % self.batches
             if i % self.group == self.group - 1 or i == self.batches - 1:  # group i // group complete
                 g = i // self.group
-                self._probe(g, timing)
+                self._probe(j0, g, timing)
                 if verify:
-                    bm, bl = o.checksum(self.outs[g % 2], self.chunk, self.group_row_map(g), self.stream)
+                    bm, bl = o.checksum(self.outs[self._gslot(j)], self.chunk, self.group_row_map(j0, g), self.stream)
                     m, l2 = m + bm, (l2 + bl) % (1 << 64)
         cur.wait_stream(self.stream)
         cur.wait_stream(self.pstream)
@@ -381,8 +415,13 @@ class ShardedProbe:
         # Every rank branches on the same value: the MAX of all ranks' status words.
         if agree_status(self.status):
             self.last_exact = True
-            self.exact_steps += 1
-            return self.step_exact(keys, row_base, verify)
+            self.exact_steps += steps
+            m, l2 = 0, 0
+            for _ in range(steps):
+                r = self.step_exact(keys, row_base, verify)
+                if verify:
+                    m, l2 = m + r[0], (l2 + r[1]) % (1 << 64)
+            return (m, l2) if verify else None
         self.last_exact = False
         return (m, l2) if verify else None
 
@@ -435,7 +474,7 @@ class HostOpsBase:
 
     device = torch.device("cpu")
 
-    def stream(self):
+    def stream(self, role=None):
         return HostStream()
 
     def event(self, timing=False):

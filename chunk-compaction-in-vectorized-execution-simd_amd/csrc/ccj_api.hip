@@ -13,6 +13,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "ccj_internal.h"
@@ -1023,3 +1024,58 @@ int ccj_result_checksum_mapped(const uint32_t *out_count, const uint32_t *out_se
 }
 
 }  // extern "C"
+
+// ---- CU-masked streams ---------------------------------------------------------------------
+namespace {
+std::mutex g_mask_mu;
+std::unordered_map<hipStream_t, uint32_t> g_mask_cus;  // streams made here -> their CU count
+
+uint32_t device_cus() {
+  int dev = 0, n = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+  return (uint32_t)(n > 0 ? n : 1);
+}
+}  // namespace
+
+uint32_t ccj::stream_cus(hipStream_t s) {
+  {
+    std::lock_guard<std::mutex> lk(g_mask_mu);
+    const auto it = g_mask_cus.find(s);
+    if (it != g_mask_cus.end()) return it->second;
+  }
+  static const uint32_t all = device_cus();
+  return all;
+}
+
+int ccj_stream_create_cu_masked(const uint32_t *cu_mask, uint32_t mask_words, ccj_stream *out) {
+  if (!cu_mask || !out || mask_words == 0) return fail(CCJ_ERR_INVALID, "ccj_stream_create_cu_masked: missing mask");
+  const uint32_t n = device_cus();
+  uint32_t cus = 0;
+  for (uint32_t i = 0; i < n && i / 32 < mask_words; ++i) cus += (cu_mask[i / 32] >> (i % 32)) & 1u;
+  if (cus == 0) return fail(CCJ_ERR_INVALID, "ccj_stream_create_cu_masked: the mask selects no CU");
+  hipStream_t s = nullptr;
+  HIP_TRY(hipExtStreamCreateWithCUMask(&s, mask_words, cu_mask), "hipExtStreamCreateWithCUMask");
+  {
+    std::lock_guard<std::mutex> lk(g_mask_mu);
+    g_mask_cus[s] = cus;
+  }
+  *out = (ccj_stream)s;
+  return CCJ_OK;
+}
+
+int ccj_stream_destroy(ccj_stream stream) {
+  if (!stream) return fail(CCJ_ERR_INVALID, "ccj_stream_destroy: NULL stream");
+  {
+    std::lock_guard<std::mutex> lk(g_mask_mu);
+    g_mask_cus.erase((hipStream_t)stream);
+  }
+  HIP_TRY(hipStreamDestroy((hipStream_t)stream), "hipStreamDestroy");
+  return CCJ_OK;
+}
+
+int ccj_device_cus(uint32_t *out) {
+  if (!out) return fail(CCJ_ERR_INVALID, "ccj_device_cus: NULL out");
+  *out = device_cus();
+  return CCJ_OK;
+}

@@ -125,6 +125,9 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s);
 // leaving each row's round word at its position (p.out_w); the words back into row order, one
 // split tile per workgroup; the reference-order emit of each chunk from its rows' words (p.in_w).
 hipError_t launch_ordered_walk(int kind, const ProbeParams &p, hipStream_t s);
+// CUs a persistent grid may use on stream s: the popcount of its CU mask for streams made by
+// ccj_stream_create_cu_masked, else the device's CU count.
+uint32_t stream_cus(hipStream_t s);
 hipError_t launch_unsplit_words(const uint2 *runs, const uint32_t *ovf_runs, const uint16_t *row_loc,
                                 const void *w_pos, void *w_row, uint64_t n, uint32_t parts, uint32_t tile,
                                 uint32_t *status, hipStream_t s, bool w16);

@@ -2366,12 +2366,14 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
       hipLaunchKernelGGL((probe_walk<3, true>), g, b, 0, s, p);
     else if (ccj_tune_int("CCJ_WALK_DMA", 2) == 1)
       hipLaunchKernelGGL((probe_walk<3, true, 4, false, 2, true>), g, b, 0, s, p);
-    else if (ccj_tune_int("CCJ_WALK_NB", 2) == 1)
-      hipLaunchKernelGGL((probe_walk1<1>), g, b, 0, s, p);
-    else if (ccj_tune_int("CCJ_WALK_NB", 2) == 3)
+    // probe_walk1: one batch of 64 rows in flight per wave (NB = 1) 12.07-12.09 ms per C2 step,
+    // NB = 2 / 3 / 4 12.23 / 12.40 / 14.27 (fewer workgroups per CU; profiles/r3_ab.md)
+    else if (ccj_tune_int("CCJ_WALK_NB", 1) == 2)
+      hipLaunchKernelGGL((probe_walk1<2>), g, b, 0, s, p);
+    else if (ccj_tune_int("CCJ_WALK_NB", 1) == 3)
       hipLaunchKernelGGL((probe_walk1<3>), g, b, 0, s, p);
     else
-      hipLaunchKernelGGL((probe_walk1<2>), g, b, 0, s, p);
+      hipLaunchKernelGGL((probe_walk1<1>), g, b, 0, s, p);
   }
   return hipGetLastError();
 }

@@ -598,7 +598,26 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
 #pragma unroll
     for (int it = 0; it < PER; ++it) {
       const uint32_t d = (uint32_t)(murmurhash64((uint64_t)kc[it]) >> shift) & mask;
-      dr[it] = d | ((live >> it) & 1u ? atomicAdd(&s_hist[d], 1u) : 0u) << 10;
+      if constexpr (MAXP <= 64) {
+        // few partitions (the owner split: one per rank): an LDS atomic per key would queue the
+        // wave's 64 lanes on at most `parts` addresses (one address at N = 1).  Instead one ballot
+        // per partition ranks the wave's keys, lane p adds partition p's wave count to s_hist[p]
+        // (distinct addresses), and each lane takes its partition's base from that lane.
+        const bool lv = (live >> it) & 1u;
+        uint32_t wcnt = 0;
+        uint64_t mine = 0;
+        for (uint32_t q = 0; q < parts; ++q) {
+          const uint64_t b = __ballot(lv && d == q);
+          if (lane == q) wcnt = (uint32_t)__popcll(b);
+          if (d == q) mine = b;
+        }
+        const uint32_t base = lane < parts && wcnt ? atomicAdd(&s_hist[lane], wcnt) : 0u;
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
+        const uint32_t rk = (uint32_t)__shfl((int)base, (int)d) + below;
+        dr[it] = d | (lv ? rk : 0u) << 10;
+      } else {
+        dr[it] = d | ((live >> it) & 1u ? atomicAdd(&s_hist[d], 1u) : 0u) << 10;
+      }
     }
     __syncthreads();
     const uint32_t h = tid < parts ? s_hist[tid] : 0u;
@@ -712,7 +731,11 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
   const uint32_t tile = slot_split_tile_keys(parts, runs != nullptr);
   if (shift == ~0u) shift = pl.window_bits;  // the slot split: partition = home slot >> window bits
   const uint64_t n_tiles = (n + tile - 1) / tile;
-  const unsigned grid = wgs ? (wgs + 7) / 8 * 8 : cus;  // wgs: leave CUs to kernels of other streams
+  // wgs: leave CUs to kernels of other streams; a CU-masked stream: one workgroup per CU it may use
+  // (a grid larger than that would run its last workgroups after the first ones: a persistent
+  // grid's whole work again)
+  const uint32_t scus = std::max<uint32_t>(8u, stream_cus(s) / 8 * 8);
+  const unsigned grid = std::min<unsigned>(wgs ? (wgs + 7) / 8 * 8 : cus, scus);
   // the pipelined form needs a sink for its inactive lanes' stores: 64 positions of the overflow
   // area (8 per XCD group), or the caller's kSplitSinkBytes
   if ((ovf_cap >= 128 || sink) && ccj_tune_int("CCJ_SPLIT_PIPE", 1)) {
@@ -730,7 +753,10 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
                          keys, n, shift, parts, n_tiles, cursors, cap, ovf_base, oc, out_keys, out_rows, status,     \
                          counts, chunk, runs, ovf_runs, row_base, sink_k, sink_r);                                   \
   } while (0)
-    if (parts > kSplitParts / 2) {
+    if (parts <= 64 && !runs && per == kSplitPer) {  // the owner split: ballot ranking (above)
+      if (counts) CCJ_PIPE_LAUNCH(true, 64, kSplitPer);
+      else CCJ_PIPE_LAUNCH(false, 64, kSplitPer);
+    } else if (parts > kSplitParts / 2) {
       if (counts) CCJ_PIPE_LAUNCH(true, kSplitParts, 10);
       else CCJ_PIPE_LAUNCH(false, kSplitParts, 10);
     } else if (per == 10) {

@@ -357,6 +357,17 @@ int ccj_partition_by_owner_grouped(const int64_t *d_keys, uint64_t n, uint32_t p
 int ccj_segment_chunk_counts(const uint64_t *d_seg_counts, uint32_t n_segs, uint64_t seg_cap, uint32_t chunk,
                              uint32_t *d_out_counts, uint32_t *d_status, ccj_stream stream);
 
+/* Streams confined to a subset of the CUs (the multi-GPU step: the local probe, the owner split
+ * and RCCL each keep CUs of their own, so that a kernel of 10^5 workgroups on one stream cannot
+ * hold every CU until it drains while the others' kernels wait).  cu_mask: mask_words 32-bit
+ * words, bit i = CU i in HIP's numbering (hipExtStreamCreateWithCUMask).  The persistent kernels
+ * (the one-pass splits) launched on such a stream size their grid to its CUs.  No reference
+ * counterpart: plumbing of the sharded path. */
+int ccj_stream_create_cu_masked(const uint32_t *cu_mask, uint32_t mask_words, ccj_stream *out);
+int ccj_stream_destroy(ccj_stream stream);
+/* The device's CU count (hipDeviceAttributeMultiprocessorCount). */
+int ccj_device_cus(uint32_t *out);
+
 /* ---- workload + measurement helpers (not on the reference's path) ------------------------- */
 /* Synthetic probe column: d_out[i] = SplitMix64(seed) output (first_row + i) mod range — the
  * stream of oracle/ccj_gen.h ccj_uniform_key, so any row can be regenerated on the host.

@@ -280,14 +280,18 @@ def _sharded_worker(rank, world, port, cfg, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    n_build, cf, n_probe, rng, seed, chunk, batches, group, skew_rank, local_ovf_rank, subs = cfg
+    n_build, cf, n_probe, rng, seed, chunk, batches, group, skew_rank, local_ovf_rank, subs = cfg[:11]
+    run_steps = cfg[11] if len(cfg) > 11 else 0  # > 0: one pipelined run of that many steps
     ops = HostOps(local_overflow=(rank == local_ovf_rank), subs=subs)
     sp = ccj_dist.ShardedProbe(n_build, cf, n_probe, chunk, world, rank, batches=batches, ops=ops, group=group)
     keys = O.uniform_keys(seed, rank * n_probe, (rank + 1) * n_probe, rng)
     if rank == skew_rank:  # one hot key: its owner's send segment overflows on this rank only
         keys[:] = keys[0]
     res = []
-    for _ in range(2):
+    if run_steps:
+        m, l2 = sp.run(torch.from_numpy(keys), rank * n_probe, steps=run_steps, verify=True)
+        res.append((m, l2, sp.last_exact))
+    for _ in range(0 if run_steps else 2):
         m, l2 = sp.step(torch.from_numpy(keys), rank * n_probe, verify=True)
         res.append((m, l2, sp.last_exact))
     tot = torch.tensor([m, l2 - (1 << 64) if l2 >= (1 << 63) else l2], dtype=torch.int64)
@@ -349,3 +353,19 @@ def test_sharded_overflow_on_one_rank_all_fall_back(world, skew_rank, local_ovf_
     for rank, m, l2, wm, wl2, exact, nb, ng, probes in got:
         assert (m, l2) == (wm, wl2)
         assert exact == [True, True]
+
+
+@pytest.mark.parametrize("world,batches,group,subs,steps,skew_rank", [(2, 3, 2, 1, 3, -1), (2, 4, 3, 8, 2, -1),
+                                                                       (4, 5, 2, 1, 2, -1), (2, 3, 2, 1, 2, 1)])
+def test_sharded_run_pipelined_steps_gloo(world, batches, group, subs, steps, skew_rank):
+    """ShardedProbe.run: `steps` passes issued back to back (the receive-group slots alternate across
+    step boundaries, odd group counts included; one status agreement at the end): L1 + L2 are
+    `steps` times one pass's exact answer, and an overflow on one rank makes every rank redo all
+    the run's steps exactly."""
+    cfg = (1 << 13, 2, 3 << 12, 3 << 12, 23, 256, batches, group, skew_rank, -1, subs, steps)
+    got = _run_sharded(world, cfg)
+    for rank, m, l2, wm, wl2, exact, nb, ng, probes in got:
+        assert (m, l2) == (steps * wm, steps * wl2 % (1 << 64))
+        assert exact == [skew_rank >= 0]
+        if skew_rank < 0:
+            assert probes == steps * ng
