@@ -25,6 +25,7 @@ FLAG_CAP_OVERFLOW, FLAG_ROUND_OVERFLOW, FLAG_BAD_INPUT, FLAG_PART_OVERFLOW = 1, 
 PART_EXACT = 1
 PART_ROWS = 2  # out_sel = the original row of every match (ccj.h CCJ_PART_ROWS)
 PART_RANK = 4  # the rank walk (LDS window index) instead of the slot-array walk (ccj.h CCJ_PART_RANK)
+PART_SHARE = 8  # the split leaves 1/4 of the CUs to other streams (ccj.h CCJ_PART_SHARE; multi-GPU step)
 
 _lib = None
 
@@ -319,7 +320,7 @@ class Table:
 
     def probe_partitioned(self, keys, chunk: int, out=None, part=None, stream=None, exact: bool = False,
                           retry: bool = True, counts=None, rows: bool = False, rank: bool = False,
-                          **alloc_kw):
+                          share: bool = False, **alloc_kw):
         """Slot-range-partitioned probe (ccj_probe_partitioned): L1/L2 results of probe(); out_sel
         indexes the partitioned layout and part["row_map"] maps a live position back to its row.
         The default one-pass split may overflow a segment under heavy key skew
@@ -345,7 +346,7 @@ class Table:
             raise CCJError("probe output buffers smaller than the partitioned layout needs")
         a = self._args(keys, chunk, None, counts, out)
         a.out_round_counts = None  # no Next boundaries in partition order
-        sw = PART_RANK if rank else 0
+        sw = (PART_RANK if rank else 0) | (PART_SHARE if share else 0)
         flags = (PART_EXACT if exact else 0) | (PART_ROWS if rows else 0) | sw
         row_map = None if rows else _ptr(part["row_map"])
         check(lib().ccj_probe_partitioned(self._h, C.byref(a), flags, row_map, _ptr(part["ws"]),

@@ -177,7 +177,9 @@ class DeviceOps:
         return part, out
 
     def probe_group(self, keys, counts, part, out, chunk, stream):
-        self.table.probe_partitioned(keys, chunk, counts=counts, out=out, part=part, stream=stream, retry=False)
+        # share: the local split leaves CUs to RCCL and the next owner splits (ccj.h CCJ_PART_SHARE)
+        self.table.probe_partitioned(keys, chunk, counts=counts, out=out, part=part, stream=stream, retry=False,
+                                     share=True)
 
     def group_rows(self, part, recv_rows, n_probe, seg_cap, slots, stream):
         """Global probe row of every position of a group's partitioned layout (gap positions hold

@@ -592,7 +592,8 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   if ((a->out_pos || a->n_payload_cols) && t->info.size < 16)
     return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: positions / payload columns need a table of >= 16 slots");
   if (a->n_rows >= (1ull << 32)) return fail(CCJ_ERR_LIMIT, "ccj_probe_partitioned: n_rows must be < 2^32");
-  if (flags & ~(CCJ_PART_EXACT | CCJ_PART_ROWS | CCJ_PART_RANK)) return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: unknown flags");
+  if (flags & ~(CCJ_PART_EXACT | CCJ_PART_ROWS | CCJ_PART_RANK | CCJ_PART_SHARE))
+    return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: unknown flags");
   if ((flags & CCJ_PART_RANK) && !t->d_ckeys && rank_index_applies(t))  // refused before any launch
     return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: CCJ_PART_RANK needs ccj_table_build_rank_index first");
   const bool rows = (flags & CCJ_PART_ROWS) != 0;
@@ -626,8 +627,11 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
     HIP_TRY(ccj::launch_iota_u32(out_row_map, a->n_rows, s), "iota");
   } else if (!exact) {
     uint32_t *cursors = (uint32_t *)rest;
+    // CCJ_PART_SHARE: 3/4 of the stream's CUs (a multiple of 8), the rest left to other streams
+    const uint32_t share = (flags & CCJ_PART_SHARE) ? std::max<uint32_t>(8u, ccj::stream_cus(s) * 3 / 4 / 8 * 8) : 0u;
     HIP_TRY(ccj::launch_slot_split_fixed(a->keys, a->n_rows, L.pl, L.seg_cap, L.ovf_base, L.ovf_cap, cursors, pkeys,
-                                         out_row_map, a->status, s, a->counts, a->chunk),
+                                         out_row_map, a->status, s, a->counts, a->chunk, nullptr, nullptr, 0, ~0u,
+                                         share),
             "slot split");
     p.seg_count = cursors;
     p.counts = nullptr;  // the input's chunk counts were applied by the split

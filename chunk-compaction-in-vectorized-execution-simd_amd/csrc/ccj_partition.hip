@@ -260,6 +260,10 @@ uint64_t partition_grouped_sub_cap(uint64_t n, uint32_t parts, uint32_t chunk) {
   return chunk ? (c + chunk - 1) / chunk * chunk : c;
 }
 
+static hipError_t launch_owner_split_small(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t shift,
+                                          uint64_t sub_cap, uint32_t *cur, int64_t *out_keys, uint32_t *out_rows,
+                                          uint32_t *status, uint32_t row_base, void *sink, hipStream_t s);
+
 hipError_t launch_partition_grouped(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t row_base,
                                     uint64_t sub_cap, int64_t *out_keys, uint32_t *out_rows, uint64_t *out_counts,
                                     uint32_t *status, void *ws, hipStream_t s) {
@@ -279,9 +283,14 @@ hipError_t launch_partition_grouped(const int64_t *keys, uint64_t n, uint32_t pa
     return (uint32_t)(n >= 16 ? n / 16 * 8 : 8);
   }();
   const uint32_t wgs = (uint32_t)ccj_tune_int("CCJ_OWNER_WGS", (int)half);
-  hipError_t e = launch_slot_split_fixed(keys, n, pl, sub_cap, 0, 0, cur, out_keys, out_rows, status, s, nullptr, 0,
-                                         nullptr, nullptr, row_base, shift, wgs,
-                                         (char *)ws + grouped_cursor_bytes(parts));
+  hipError_t e;
+  if (ccj_tune_int("CCJ_OWNER_SMALL", 1) && parts <= 64) {
+    e = launch_owner_split_small(keys, n, parts, shift, sub_cap, cur, out_keys, out_rows, status, row_base,
+                                 (char *)ws + grouped_cursor_bytes(parts), s);
+  } else {
+    e = launch_slot_split_fixed(keys, n, pl, sub_cap, 0, 0, cur, out_keys, out_rows, status, s, nullptr, 0,
+                                nullptr, nullptr, row_base, shift, wgs, (char *)ws + grouped_cursor_bytes(parts));
+  }
   if (e) return e;
   hipLaunchKernelGGL(grouped_counts, dim3((parts * 8 + 255) / 256), dim3(256), 0, s, cur, parts, out_counts);
   return hipGetLastError();
@@ -685,6 +694,34 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
 
 }  // namespace
 
+// The owner split in small workgroups (the multi-GPU step): slot_split_pipe with 256 threads and
+// 2048-key tiles (~26 KB of LDS) instead of one 1024-thread, 149 KB workgroup per CU.  The step
+// runs it beside the local probe: a workgroup that needs a whole CU's LDS waits until no walk
+// workgroup is left on some CU, i.e. until the walk's ~3·10^5 workgroups have drained (round-3
+// kernel trace of the one-rank rehearsal: no partition ran during any walk), while 26 KB
+// workgroups take the slots the walk's retiring workgroups free.  Persistent, 4 per CU of the
+// stream (a multiple of 8: one tile group per XCD).
+static hipError_t launch_owner_split_small(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t shift,
+                                          uint64_t sub_cap, uint32_t *cur, int64_t *out_keys, uint32_t *out_rows,
+                                          uint32_t *status, uint32_t row_base, void *sink, hipStream_t s) {
+  constexpr int kT = 256, kPer = 8;
+  constexpr uint32_t kTile = (uint32_t)kT * kPer;
+  hipError_t e = hipMemsetAsync(cur, 0, ((size_t)parts * 8 + 1) * 4, s);
+  if (e || n == 0) return e;
+  const uint64_t n_tiles = (n + kTile - 1) / kTile;
+  // per_cu = 0: one workgroup per tile (not persistent), so that workgroups dispatched late —
+  // behind another stream's kernel — do not each carry a fixed share of the tiles
+  const uint32_t per_cu = (uint32_t)ccj_tune_int("CCJ_OWNER_SMALL_PER_CU", 4);
+  uint64_t grid = per_cu ? (uint64_t)stream_cus(s) * per_cu / 8 * 8 : (n_tiles + 7) / 8 * 8;
+  grid = grid < 8 ? 8 : grid;
+  int64_t *sink_k = (int64_t *)sink;
+  uint32_t *sink_r = (uint32_t *)((char *)sink + kSplitSinkBytes / 16 * 8);
+  hipLaunchKernelGGL((slot_split_pipe<false, kT, 64, kPer, false>), dim3((unsigned)grid), dim3(kT), 0, s, keys, n, shift, parts,
+                     n_tiles, cur, sub_cap, (uint64_t)0, (uint64_t)0, out_keys, out_rows, status, nullptr, 0u, nullptr,
+                     nullptr, row_base, sink_k, sink_r);
+  return hipGetLastError();
+}
+
 uint64_t slot_seg_cap(uint64_t n, const SlotPlan &pl, uint32_t chunk) {
   const uint32_t parts = 1u << (pl.lo_bits + pl.hi_bits);
   const double m = (double)n / (8.0 * parts);
@@ -734,6 +771,7 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
   // wgs: leave CUs to kernels of other streams; a CU-masked stream: one workgroup per CU it may use
   // (a grid larger than that would run its last workgroups after the first ones: a persistent
   // grid's whole work again)
+  if (!wgs) wgs = (uint32_t)ccj_tune_int("CCJ_SPLIT_WGS", 0);  // (tuning build: a smaller persistent grid)
   const uint32_t scus = std::max<uint32_t>(8u, stream_cus(s) / 8 * 8);
   const unsigned grid = std::min<unsigned>(wgs ? (wgs + 7) / 8 * 8 : cus, scus);
   // the pipelined form needs a sink for its inactive lanes' stores: 64 positions of the overflow

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CCJ_ABI_VERSION 8  /* 8: CCJ_PART_RANK (LDS window index walk); 7: CCJ_PART_ROWS */
+#define CCJ_ABI_VERSION 9  /* 9: CCJ_PART_SHARE, CU-masked streams; 8: CCJ_PART_RANK; 7: CCJ_PART_ROWS */
 
 enum ccj_status {
   CCJ_OK = 0,
@@ -220,6 +220,11 @@ int ccj_probe_visits(const ccj_table *table, const int64_t *d_keys, const uint32
  * CU (the 80 KiB index) keeps half as many requests in flight: 9.9 ms against 7.4 for the slot
  * walk.  Not the default.  Needs ccj_table_build_rank_index (CCJ_ERR_INVALID without it). */
 #define CCJ_PART_RANK 4u
+/* flags & CCJ_PART_SHARE: the one-pass split runs on 3/4 of the CUs (of the stream's CUs), leaving
+ * the rest to kernels of other streams.  The split holds one 1024-thread, ~150 KB-LDS workgroup per
+ * CU, so without the flag nothing else — RCCL's kernels, the next batch's owner split — runs while
+ * it does.  The multi-GPU step passes it (one-rank rehearsal 32.4 -> 29.2 ms per step). */
+#define CCJ_PART_SHARE 8u
 uint64_t ccj_probe_partitioned_positions(const ccj_table *table, uint64_t n_rows, uint32_t chunk);
 size_t ccj_probe_partitioned_workspace_size(const ccj_table *table, uint64_t n_rows, uint32_t chunk);
 int ccj_probe_partitioned(const ccj_table *table, const ccj_probe_args *args, uint32_t flags,

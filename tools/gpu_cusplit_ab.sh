@@ -2,7 +2,7 @@
 # One-rank sharded rehearsal under several CU splits (ON THE GPU BOX): tools/gpu_cusplit_ab.sh "24,8" "0,0" ...
 cd "$GRAFT_REPO_ROOT" || exit 1
 for cs in "$@"; do
-  timeout -k 10 300 python3 bench.py --gpus 1 --sharded --steps 8 --warmup 2 --no-cpu --no-verify --cu-split "$cs" \
+  timeout -k 10 300 python3 bench.py $BENCH_EXTRA --gpus 1 --sharded --steps 8 --warmup 2 --no-cpu --no-verify --cu-split "$cs" \
       > gpurun_out/cusplit_${cs/,/_}.log 2>&1 || { echo "cu-split $cs failed"; tail -5 gpurun_out/cusplit_${cs/,/_}.log; exit 1; }
   python3 - "$cs" <<'PY'
 import json, sys
