@@ -118,6 +118,30 @@ def cpu_model():
     return platform.processor()
 
 
+def copy_ceiling(dev, stream, nbytes=4 << 30, iters=10):
+    """Measured HBM copy ceiling: GB/s of bytes read + written by ccj_copy_device
+    (16-byte non-temporal loads/stores) over a 4 GiB buffer, with torch's copy_ beside it."""
+    src = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    dst = torch.empty_like(src)
+    res = {"bytes_per_copy": nbytes, "iters": iters}
+    for name, fn in (("ccj_copy_device", lambda: ccj.copy_device(dst, src, stream=stream)),
+                     ("torch_copy", lambda: dst.copy_(src))):
+        st = stream if name == "ccj_copy_device" else torch.cuda.current_stream()
+        fn()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        a.record(st)
+        for _ in range(iters):
+            fn()
+        b.record(st)
+        torch.cuda.synchronize()
+        res[f"{name}_GBps"] = 2 * nbytes * iters / (a.elapsed_time(b) * 1e-3) / 1e9
+    del src, dst
+    torch.cuda.empty_cache()
+    res["GBps"] = max(res["ccj_copy_device_GBps"], res["torch_copy_GBps"])
+    return res
+
+
 def physical_cores():
     """Distinct (socket, core) pairs in /proc/cpuinfo (the host's physical cores), or None."""
     try:
@@ -706,6 +730,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and not c5:  # the reference has no payload gather
         cpu = cpu_baseline(args)
+    ceiling = None
+    if dev.type == "cuda" and n_probe >= (1 << 26):  # untimed, after the step's buffers are in place
+        ceiling = copy_ceiling(dev, stream)
 
     if rank == 0:
         line = {
@@ -727,7 +754,10 @@ def main():
                                      "gather_payload_quad)") if c5 and args.path == "partitioned" else
                                     "probe_chunks<LP,2> + gather_payload_quad" if c5 else PATH_KERNELS[args.path]),
                          "kernel_ms": kern_ms, "rocprof_kernels_ms": kernels_ms,
-                         "alg_bytes_per_tuple": alg_bytes_per_tuple, "s_bar": s_bar, "m_bar": m_bar},
+                         "alg_bytes_per_tuple": alg_bytes_per_tuple, "s_bar": s_bar, "m_bar": m_bar,
+                         # the same achieved rate against the copy rate measured on this box
+                         "frac_of_copy_ceiling": achieved / ceiling["GBps"] if ceiling else None},
+            "hbm_copy_ceiling": ceiling,
             "cpu_baseline": cpu,
             "parity": parity,
             "path": args.path,

@@ -71,7 +71,7 @@ EXPORTS = ["ccj_last_error", "ccj_abi_version", "ccj_device_init", "ccj_table_bu
            "ccj_segment_chunk_counts", "ccj_pipeline_set_thresholds", "ccj_gen_c3_keys",
            "ccj_partition_grouped_workspace_size", "ccj_partition_by_owner_grouped", "ccj_partition_grouped_sub_cap",
            "ccj_probe_ordered_workspace_size", "ccj_probe_ordered", "ccj_probe_visits",
-           "ccj_stream_create_cu_masked", "ccj_stream_destroy", "ccj_device_cus"]
+           "ccj_stream_create_cu_masked", "ccj_stream_destroy", "ccj_device_cus", "ccj_copy_device"]
 
 MAX_JOINS = 8
 COMPACT_NONE, COMPACT_FULL = 0, 1
@@ -146,6 +146,7 @@ def lib():
         L.ccj_stream_create_cu_masked.argtypes = [C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(vp)]
         L.ccj_stream_destroy.argtypes = [vp]
         L.ccj_device_cus.argtypes = [C.POINTER(C.c_uint32)]
+        L.ccj_copy_device.argtypes = [vp, vp, u64, vp]
         _lib = L
     return _lib
 
@@ -569,6 +570,14 @@ class GroupedOwnerPartitioner:
 def grouped_sub_cap(n: int, parts: int, chunk: int) -> int:
     """Sub-segment capacity for GroupedOwnerPartitioner over n uniformly hashed keys."""
     return int(lib().ccj_partition_grouped_sub_cap(n, parts, chunk))
+
+
+def copy_device(dst, src, stream=None):
+    """dst[:] = src (device tensors of equal byte size, a multiple of 16) by ccj_copy_device."""
+    nb = src.numel() * src.element_size()
+    assert dst.numel() * dst.element_size() == nb
+    check(lib().ccj_copy_device(_ptr(dst), _ptr(src), nb, _stream(stream)), "ccj_copy_device")
+    return dst
 
 
 def device_cus() -> int:

@@ -944,6 +944,13 @@ int ccj_gen_uniform_keys(int64_t *d_out, uint64_t n, uint64_t seed, uint64_t fir
   return CCJ_OK;
 }
 
+int ccj_copy_device(void *d_dst, const void *d_src, uint64_t bytes, ccj_stream stream) {
+  if (bytes % 16 || (bytes && (!d_dst || !d_src)) || ((uintptr_t)d_dst | (uintptr_t)d_src) % 16)
+    return fail(CCJ_ERR_INVALID, "ccj_copy_device: buffers must be 16-byte aligned, bytes a multiple of 16");
+  if (bytes) HIP_TRY(ccj::launch_copy16(d_src, d_dst, bytes / 16, (hipStream_t)stream), "copy");
+  return CCJ_OK;
+}
+
 int ccj_gen_c3_keys(int64_t *d_out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t n_build, uint64_t cf,
                     uint32_t hit_ppm, ccj_stream stream) {
   if ((!d_out && n) || cf == 0 || n_build == 0 || n_build >= (1ull << 62) || hit_ppm > 1000000)

@@ -138,6 +138,7 @@ hipError_t launch_gen_reference_keys(int64_t *out, uint64_t first, uint64_t n, u
                                      hipStream_t s);
 hipError_t launch_fill(int64_t *p, uint64_t n, int64_t v, hipStream_t s);
 hipError_t launch_iota_u32(uint32_t *p, uint64_t n, hipStream_t s);
+hipError_t launch_copy16(const void *src, void *dst, uint64_t n16, hipStream_t s);
 hipError_t launch_lp_insert(const int64_t *keys, uint64_t n, int64_t *slots, uint32_t *slot_row, uint32_t mask,
                             hipStream_t s);
 hipError_t launch_scatter_payload(const int64_t *src, uint32_t n_cols, const uint32_t *row, uint64_t positions,

@@ -2566,6 +2566,39 @@ hipError_t launch_iota_u32(uint32_t *p, uint64_t n, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Device-to-device copy for the measured HBM copy ceiling ("report a measured
+// STREAM-copy ceiling on the box"): 16-byte non-temporal loads, four in flight per thread, then
+// the four stores; a grid of 8 workgroups per CU strides over the buffer.
+__global__ __launch_bounds__(256) void copy16(const u32x4 *src, u32x4 *dst, uint64_t n16) {
+  const uint64_t stride = (uint64_t)gridDim.x * 1024;
+  for (uint64_t i = (uint64_t)blockIdx.x * 1024 + threadIdx.x; i < n16; i += stride) {
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint64_t j = i + (uint64_t)u * 256;
+      v[u] = __builtin_nontemporal_load(src + (j < n16 ? j : i));
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint64_t j = i + (uint64_t)u * 256;
+      if (j < n16) __builtin_nontemporal_store(v[u], dst + j);
+    }
+  }
+}
+
+hipError_t launch_copy16(const void *src, void *dst, uint64_t n16, hipStream_t s) {
+  static const unsigned cus = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return (unsigned)(n > 0 ? n : 1);
+  }();
+  const uint64_t need = (n16 + 1023) / 1024;
+  const unsigned grid = (unsigned)(need < 8ull * cus ? (need ? need : 1) : 8ull * cus);
+  hipLaunchKernelGGL(copy16, dim3(grid), dim3(256), 0, s, (const u32x4 *)src, (u32x4 *)dst, n16);
+  return hipGetLastError();
+}
+
 hipError_t launch_fill(int64_t *p, uint64_t n, int64_t v, hipStream_t s) {
   hipLaunchKernelGGL(fill_i64, dim3(grid_for(n, 256)), dim3(256), 0, s, p, n, v);
   return hipGetLastError();

@@ -374,6 +374,9 @@ int ccj_stream_destroy(ccj_stream stream);
 int ccj_device_cus(uint32_t *out);
 
 /* ---- workload + measurement helpers (not on the reference's path) ------------------------- */
+/* d_dst[0, bytes) = d_src[0, bytes): 16-byte non-temporal loads and stores (bench.py's measured
+ * HBM copy ceiling).  16-byte aligned buffers, bytes a multiple of 16. */
+int ccj_copy_device(void *d_dst, const void *d_src, uint64_t bytes, ccj_stream stream);
 /* Synthetic probe column: d_out[i] = SplitMix64(seed) output (first_row + i) mod range — the
  * stream of oracle/ccj_gen.h ccj_uniform_key, so any row can be regenerated on the host.
  * Replaces the reference's host-side source (main.cpp:41-55 + DataCollection::FetchChunk). */
