@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--ops-module", default=None,
                     help=argparse.SUPPRESS)  # tests only: a module whose make_ops() replaces the HIP ops (CPU, gloo)
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"], help=argparse.SUPPRESS)
+    # tests only: every rank on cuda:0 (with --backend gloo: the N > 1 HIP path rehearsed on a one-GPU
+    # box, the exchanges staged through the host by gloo instead of RCCL over xGMI)
+    ap.add_argument("--same-device", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--sharded", action="store_true",
                     help="run the N > 1 protocol (through the same self-launcher) even at N = 1 (rehearsal)")
     ap.add_argument("--pipe-lhs", type=int, default=20000000)
@@ -522,7 +525,10 @@ def main():
         return launch_ranks(args)  # before any GPU call in this process (--sharded: one rank too)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
+    if args.same_device and args.backend == "nccl" and world > 1:
+        log("--same-device needs --backend gloo (RCCL refuses two ranks on one GPU)")
+        return 2
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     if args.ops_module:  # tests: the N > 1 step on CPU tensors with gloo (no GPU)
@@ -541,8 +547,10 @@ def main():
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
                 os.environ.setdefault("MASTER_PORT", "29533")
                 dist.init_process_group(args.backend, rank=0, world_size=1, device_id=torch.device("cuda", local))
-            else:
+            elif args.backend == "nccl":
                 dist.init_process_group(args.backend, device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group(args.backend)
             dist.barrier()  # creates the communicator (and its banner) now
     dev = torch.device("cuda", local)
     stream = torch.cuda.Stream(device=dev)

@@ -655,6 +655,17 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   p.emit_pol = (uint32_t)ccj_tune_int("CCJ_EMIT_POL", 2);
 #ifdef CCJ_TUNING
   p.ablate = (uint32_t)ccj_tune_int("CCJ_ABLATE", 0);
+  // CCJ_PREFETCH = distance in eighths of a partition's chunks (probe_walk1's window prefetch),
+  // CCJ_PF_MULT = slices of lines per chunk
+  if (!exact && L.pl.lo_bits && t->info.kind == CCJ_TABLE_LP && L.pl.window_bits >= 4) {
+    const int pf8 = ccj_tune_int("CCJ_PREFETCH", 0);
+    if (pf8 > 0) {
+      const uint64_t K = 8 * (L.seg_cap / a->chunk);
+      const uint64_t wl = (1ull << L.pl.window_bits) / 16;
+      p.pf_dist = K * (uint64_t)pf8 / 8;
+      p.pf_lines = (uint32_t)std::min<uint64_t>(64, (wl + K - 1) / K * (uint64_t)ccj_tune_int("CCJ_PF_MULT", 1));
+    }
+  }
 #endif
   // The rank walk (CCJ_PART_RANK, ccj_rank.hip): the window index in LDS, candidate keys from the
   // compact array.  Distinct keys (a row matches at most once), the keys in out_payload (cap ==

@@ -114,6 +114,11 @@ struct ProbeParams {
   uint32_t w16;
   // probe_walk: first chunk of the launch (blockIdx.x + chunk0; the rank walk's overflow-area pass)
   uint64_t chunk0;
+  // probe_walk1, partitioned input: each workgroup first touches (LDS-DMA into its own scratch)
+  // the slice of table lines that the chunk pf_dist chunks later in its XCD's order will need, so a
+  // window's first reads hit L2 (0: off); pf_lines lines per chunk
+  uint64_t pf_dist;
+  uint32_t pf_lines;
 };
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 constexpr uint32_t kEmitWave = 0xFFFFFFFFu;

@@ -1907,6 +1907,26 @@ __device__ __forceinline__ void dma16(const void *g, uint32_t lds) {
                : "memory");
 }
 constexpr uint32_t kRingSlot = 2 * 1024;  // one batch: 64 windows of 32 B, two DMA halves
+// Window prefetch (p.pf_dist): chunk c (its XCD's order, partitioned layout) touches the table lines
+// of slice (c + pf_dist) mod K of partition (c + pf_dist) / K, K = chunks per partition, so that
+// the next window is in L2 before its first chunk starts.  One LDS-DMA of wave 0 into `lds` (1 KiB
+// of the chunk's home-slot array, written by the stage only after its loads — and with them this
+// older DMA — have landed).
+__device__ __forceinline__ void walk_prefetch(const ProbeParams &p, uint64_t c, uint32_t lane, uint32_t lds) {
+  const uint64_t cl = c - p.chunk0;
+  if (cl >= p.swz_chunks || p.seg_parts == 0) return;
+  const uint64_t K = 8 * (p.seg_cap / p.chunk);
+  const uint64_t t = cl + p.pf_dist;
+  const uint64_t d2 = t / K;
+  if (d2 >= p.seg_parts) return;
+  const uint64_t wl = ((uint64_t)p.mask + 1) / p.seg_parts / 16;  // 128-byte lines per window
+  const uint64_t first = d2 * wl + (t % K) * wl / K;
+  const uint64_t last = ((uint64_t)p.mask + 1) / 16 - 1;
+  uint64_t line = first + (lane < p.pf_lines ? lane : 0u);
+  line = line < last ? line : last;
+  const uint32_t m0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds);
+  dma16(p.table + line * 16, m0);
+}
 // probe_walk1's LDS: the chunk's keys and home slots / counts, and the wave's DMA ring, which the
 // emit's scratch (total, rounds, per-wave sums) overlaps once every wave's walk is over: 32 KiB at
 // NB = 1 (5 workgroups per CU), 40 KiB at NB = 2 (4 per CU)
@@ -1933,6 +1953,7 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk1(ProbeParams p) {
   const uint32_t phys = flat_phys(p, base);
   const uint32_t w0 = wave * kWaveRows;
   const uint32_t wend = phys > w0 ? (phys - w0 < kWaveRows ? phys : w0 + kWaveRows) : w0;  // wave's rows [w0, wend)
+  if (p.pf_dist && wave == 0) walk_prefetch(p, c, lane, (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)sm.hc);
   // (timing only, tuning build: 0x100 stages the keys of chunk c & 63 — L2-resident key lines)
   walk_stage<kWaveRows, true>(p, sm, CCJ_ABLATED(p.ablate, 0x100u) ? (c & 63u) * p.chunk : base, w0, wend, lane);
   char *ring = s_ring + wave * NB * kRingSlot;

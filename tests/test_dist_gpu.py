@@ -219,3 +219,31 @@ def test_bench_sharded_line():
     assert 0 < line["roofline"]["frac"] < 1
     assert line["local_probe_ms"] > 0 and line["partition_ms"] > 0 and line["exchange_ms"] >= 0
     assert line["xgmi_bytes_per_step"] == 0  # one rank: nothing crosses xGMI
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_multi_rank_on_one_gpu(world):
+    """The N > 1 HIP path as the driver's 8-GPU run takes it — bench.py --gpus N through its own
+    launcher, N rank processes, DeviceOps with N owners (owner split into N destinations, the local
+    table of 1/N of the build keys, received segments from N sources, the local partitioned probe) —
+    with every rank on cuda:0 and gloo moving the all-to-alls through the host (RCCL refuses two
+    ranks on one GPU; this box has one).  L1 + L2 of all ranks' probes exact, no fallback."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "2"
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", str(world), "--backend", "gloo", "--same-device",
+                        "--steps", "2", "--warmup", "1", "--no-cpu", "--n-build-per-gpu", str(1 << 19),
+                        "--n-probe", str(3 << 20), "--batches", "3", "--group", "2"],
+                       cwd=root, capture_output=True, text=True, timeout=600, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == world and line["value"] > 0
+    assert line["parity"]["l1_ok"] and line["parity"]["l2_ok"], line["parity"]
+    assert line["parity"]["exact_size_fallback_steps"] == 0
+    assert line["xgmi_bytes_per_step"] > 0 and line["local_probe_ms"] > 0
