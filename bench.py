@@ -100,6 +100,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1 << 28, help="probe keys in the multi-thread CPU sample")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-other", action="store_true", help="C2: do not time the other paths beside the headline")
+    ap.add_argument("--no-rows", action="store_true",
+                    help="partitioned path without CCJ_PART_ROWS (the walk writes every output; A/B)")
     ap.add_argument("--lib", default="product",
                     help="product | tuning (libccj_tuning.so: make tuning; A/B sweeps with its env overrides) | "
                          "a path to another build of the library (same-box A/B of two source versions)")
@@ -596,7 +598,8 @@ def main():
     # C2 (distinct build keys, one output slot per position): CCJ_PART_ROWS — out_sel receives each
     # match's original row, and the split writes every position's key and row straight into the
     # output columns (ccj.h), so the walk only compacts chunks with misses
-    rows_mode = not c5 and int(table.max_dup) <= 1
+    # C5 too (round 3): the walk then writes only each match's table position, at its output slot
+    rows_mode = int(table.max_dup) <= 1 and (not c5 or table.size <= 1 << 31) and not args.no_rows
 
     def step(path=args.path):
         if path == "partitioned":  # no host check inside the timed region: status is read after it
@@ -758,7 +761,10 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          # measured DRAM bytes (whole 128-B lines per random slot read) per second
                          "traffic_GBps": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
-                         "kernel": (("ccj_probe_partitioned (slot_split_pipe + probe_win<3> with positions + "
+                         "kernel": (("ccj_probe_partitioned, CCJ_PART_ROWS (slot_split_pipe writing keys + rows, "
+                                     "probe_walk1<1, POS> writing match positions, gather_payload_quad)") if c5 and
+                                    args.path == "partitioned" and rows_mode else
+                                    ("ccj_probe_partitioned (slot_split_pipe + probe_win<3> with positions + "
                                      "gather_payload_quad)") if c5 and args.path == "partitioned" else
                                     "probe_chunks<LP,2> + gather_payload_quad" if c5 else PATH_KERNELS[args.path]),
                          "kernel_ms": kern_ms, "rocprof_kernels_ms": kernels_ms,

@@ -597,10 +597,11 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   if ((flags & CCJ_PART_RANK) && !t->d_ckeys && rank_index_applies(t))  // refused before any launch
     return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: CCJ_PART_RANK needs ccj_table_build_rank_index first");
   const bool rows = (flags & CCJ_PART_ROWS) != 0;
-  if (rows && (!a->out_payload || p.cap != a->chunk || t->info.max_dup > 1 || a->out_pos || a->n_payload_cols ||
-               t->info.kind != CCJ_TABLE_LP || t->info.size < 16))
+  // (with positions / payload columns the walk packs matched | slot into 32 bits: <= 2^31 slots)
+  if (rows && (!a->out_payload || p.cap != a->chunk || t->info.max_dup > 1 || t->info.kind != CCJ_TABLE_LP ||
+               t->info.size < 16 || ((a->out_pos || a->n_payload_cols) && t->info.size > (1ull << 31))))
     return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: CCJ_PART_ROWS needs an LP table of >= 16 slots with distinct "
-                                 "keys, cap == chunk, out_payload, and no positions / payload columns");
+                                 "keys, cap == chunk, out_payload (with positions / payload columns: <= 2^31 slots)");
   if (a->n_rows == 0) return CCJ_OK;
   if ((!out_row_map && !rows) || !ws || ws_bytes < ccj_probe_partitioned_workspace_size(t, a->n_rows, a->chunk))
     return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: missing row map or workspace too small");

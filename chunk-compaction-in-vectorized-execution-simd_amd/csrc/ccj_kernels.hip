@@ -1941,13 +1941,87 @@ struct Walk1Shared {
     };
   };
 };
-template <int NB, bool MM = false>
+// probe_walk1<POS>'s emit (CCJ_PART_ROWS with positions, distinct keys, cap == chunk): the split
+// already wrote every position's original row (out_sel) and key (out_payload), and sm.hc holds
+// matched | slot per row.  A chunk whose rows all matched writes only its positions, in place; a
+// chunk with a miss (none at C5) writes its slots at their compacted output places directly and
+// compacts rows (sm.hc) and keys (sm.key) in LDS, written with 16-byte stores.
+template <uint32_t kWaveRows, int NW, typename SM>
+__device__ __forceinline__ void walk_emit_pos(const ProbeParams &p, SM &sm, uint64_t c,
+                                              uint32_t w0, uint32_t wend, uint32_t lane, uint32_t wave,
+                                              uint32_t *s_wtot, uint32_t phys) {
+  constexpr int kJ = (int)(kWaveRows / kWave);
+  uint32_t lsum = 0;
+  uint32_t h[kJ];
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) {
+    const uint32_t i = w0 + (uint32_t)j * kWave + lane;
+    h[j] = i < wend ? sm.hc[i] : 0u;
+    lsum += h[j] >> 31;
+  }
+  const uint32_t wtot = (uint32_t)__shfl((int)wave_incl_scan(lsum), kWave - 1);
+  if (lane == 0) s_wtot[wave] = wtot;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    base += (uint32_t)w < wave ? s_wtot[w] : 0u;
+    tot += s_wtot[w];
+  }
+  const uint64_t obase = c * p.cap;
+  if (tot == phys) {  // every row matched once: positions at the rows' own output slots
+    if (kJ == 8 && wend == w0 + kWaveRows && (p.cap & 3u) == 0u) {
+      const uint32_t i0 = w0 + 8 * lane;  // 8 consecutive rows per lane: two 16-byte stores
+      const u32x4 m = {0x7FFFFFFFu, 0x7FFFFFFFu, 0x7FFFFFFFu, 0x7FFFFFFFu};
+      const u32x4 v0 = *reinterpret_cast<const u32x4 *>(&sm.hc[i0]) & m;
+      const u32x4 v1 = *reinterpret_cast<const u32x4 *>(&sm.hc[i0 + 4]) & m;
+      __builtin_nontemporal_store(v0, reinterpret_cast<u32x4 *>(p.out_pos + obase + i0));
+      __builtin_nontemporal_store(v1, reinterpret_cast<u32x4 *>(p.out_pos + obase + i0 + 4));
+    } else {
+#pragma unroll
+      for (int j = 0; j < kJ; ++j) {
+        const uint32_t i = w0 + (uint32_t)j * kWave + lane;
+        if (i < wend) __builtin_nontemporal_store(h[j] & 0x7FFFFFFFu, p.out_pos + obase + i);
+      }
+    }
+    if (threadIdx.x == 0) sm.total = tot;
+    return;
+  }
+  int64_t k[kJ];
+  uint32_t t[kJ], rid[kJ];
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) {
+    const uint32_t i = w0 + (uint32_t)j * kWave + lane;
+    const bool hit = (h[j] >> 31) != 0u;
+    const uint64_t bm = __ballot(hit);
+    t[j] = base + lane_prefix(bm);
+    base += (uint32_t)__popcll(bm);
+    k[j] = sm.key[i & (kMaxChunk - 1)];
+    rid[j] = hit ? p.out_sel[obase + i] : 0u;  // the row the split stored there
+    if (hit) __builtin_nontemporal_store(h[j] & 0x7FFFFFFFu, p.out_pos + obase + t[j]);
+  }
+  __syncthreads();  // every key and row read before any entry moves down
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) {
+    if (h[j] >> 31) {
+      sm.key[t[j]] = k[j];
+      sm.hc[t[j]] = rid[j];
+    }
+  }
+  __syncthreads();
+  emit_wg_stores<2, kWave * NW>(p, sm, obase, tot, true);
+  if (threadIdx.x == 0) sm.total = tot;
+}
+template <int NB, bool MM = false, bool POS = false>
 __global__ __launch_bounds__(kWave * 4) void probe_walk1(ProbeParams p) {
   constexpr int NW = 4;
   constexpr uint32_t kWaveRows = kMaxChunk / NW;  // rows per wave
   __shared__ Walk1Shared<NB, NW> sm;
   char *const s_ring = sm.ring;
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  unsigned long long t0, t1, t2;
+  uint32_t steps = 0;
+  CCJ_STAMP(t0);
   const uint64_t c = walk_chunk_index(p);
   const uint64_t base = c * p.chunk;
   const uint32_t phys = flat_phys(p, base);
@@ -1956,6 +2030,7 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk1(ProbeParams p) {
   if (p.pf_dist && wave == 0) walk_prefetch(p, c, lane, (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)sm.hc);
   // (timing only, tuning build: 0x100 stages the keys of chunk c & 63 — L2-resident key lines)
   walk_stage<kWaveRows, true>(p, sm, CCJ_ABLATED(p.ablate, 0x100u) ? (c & 63u) * p.chunk : base, w0, wend, lane);
+  CCJ_STAMP(t1);
   char *ring = s_ring + wave * NB * kRingSlot;
   // the ring's LDS byte address, wave-uniform (M0 of the DMAs)
   const uint32_t ring_lds = (uint32_t)__builtin_amdgcn_readfirstlane(
@@ -1965,6 +2040,7 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk1(ProbeParams p) {
   // this lane's row in ring slot b: key, row, next unread slot, window start, rounds walked, matches
   int64_t key[NB];
   uint32_t row[NB], cur[NB], st[NB], r0[NB], cnt[NB];
+  uint32_t mpos[NB];  // POS: the row's matched slot (distinct keys: at most one)
   uint32_t live = 0, lane_rounds = 0;
   uint32_t next = w0;  // wave-uniform: the wave's next unwalked row
   auto take = [&](int b, bool want) {  // lanes with `want` take the wave's next rows, in lane order
@@ -1975,6 +2051,7 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk1(ProbeParams p) {
       row[b] = i;
       r0[b] = 0;
       cnt[b] = 0;
+      if (POS) mpos[b] = 0;
       if (i < wend) {
         key[b] = sm.key[i];
         cur[b] = sm.hc[i];
@@ -2012,12 +2089,14 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk1(ProbeParams p) {
       const uint32_t hits = (m >> off) & ((1u << f) - 1u);
       if (MM) cnt[b] |= r0[b] < kMmRounds ? hits << r0[b] : 0u;  // rounds >= 26 end as long rows
       else cnt[b] += (uint32_t)__builtin_popcount(hits);
+      if (POS && hits) mpos[b] = cur[b] + (uint32_t)__builtin_ctz(hits);
       if (ee) {
         const uint32_t r = r0[b] + f;  // occupied slots walked = the reference's rounds
         lane_rounds = r > lane_rounds ? r : lane_rounds;
         if (MM) cnt[b] = r <= kMmRounds ? (cnt[b] & ((1u << kMmRounds) - 1u)) | r << kMmRounds : kMmLong | r;
         if (CCJ_ABLATED(p.ablate, 0x200u)) cnt[b] = 1;  // (timing only: the emit path of the real data)
-        sm.hc[row[b]] = cnt[b];
+        // POS (tables of <= 2^31 slots): bit 31 = matched, the low bits its slot
+        sm.hc[row[b]] = POS ? (cnt[b] ? mpos[b] | 0x80000000u : 0u) : cnt[b];
         live &= ~(1u << b);
       } else {
         r0[b] += kWin - off;
@@ -2028,13 +2107,14 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk1(ProbeParams p) {
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     key[b] = 0;
-    row[b] = cur[b] = st[b] = r0[b] = cnt[b] = 0;
+    row[b] = cur[b] = st[b] = r0[b] = cnt[b] = mpos[b] = 0;
     take(b, true);
     issue(b);
   }
   for (bool more = true; more;) {
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
+      ++steps;
       wait_vmcnt<2 * (NB - 1)>();  // batch b (the oldest) has landed
       check(b);
       take(b, ((live >> b) & 1u) == 0u);
@@ -2046,6 +2126,7 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk1(ProbeParams p) {
     }
   }
   wait_vmcnt<0>();
+  CCJ_STAMP(t2);
   __syncthreads();  // every wave's ring is idle: the emit's scratch may overlap it
   if (tid == 0) {
     sm.total = 0;
@@ -2073,14 +2154,19 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk1(ProbeParams p) {
     }
     return;
   }
+  if (POS) {  // CCJ_PART_ROWS with match positions (C5): sel and payload are the split's
+    walk_emit_pos<kWaveRows, NW>(p, sm, c, w0, wend, lane, wave, sm.wtot, phys);
+    walk_finish(p, sm, c, lane, lane_rounds, 0u, t0, t1, t2, steps);
+    return;
+  }
   if (p.emit_pol != kEmitWave || p.rows_in_sel) {  // (rows_in_sel: only the workgroup emit maps rows)
     if (walk_emit_wg<kWaveRows, NW>(p, sm, c, w0, wend, lane, wave, sm.wtot, phys)) {
-      walk_finish(p, sm, c, lane, lane_rounds, 0u, 0ull, 0ull, 0ull, 0u);
+      walk_finish(p, sm, c, lane, lane_rounds, 0u, t0, t1, t2, steps);
       return;
     }
   }
   const uint32_t overflow = walk_emit<kWaveRows>(p, sm, c, w0, wend, lane);
-  walk_finish(p, sm, c, lane, lane_rounds, overflow, 0ull, 0ull, 0ull, 0u);
+  walk_finish(p, sm, c, lane, lane_rounds, overflow, t0, t1, t2, steps);
 }
 
 // Ordered probe, step 4 (emit_ordered): one chunk per 256-thread workgroup, the reference's
@@ -2375,7 +2461,11 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
   // lane per row with two 16-B loads (twice the L2 requests) 11.0-12.3 ms; a rolling load
   // pipeline (each slot re-issued as soon as it is consumed, vmcnt(R - 1) waits) 10.4-10.5 ms;
   // write-through (sc1) or plain output stores 10.2 ms vs non-temporal.
-  if (p.out_pos) {
+  if (p.out_pos && p.rows_in_sel) {
+    // C5 under CCJ_PART_ROWS (distinct keys, tables of <= 2^31 slots): the split wrote rows and keys,
+    // probe_walk1 leaves each row's matched slot at its output slot
+    hipLaunchKernelGGL((probe_walk1<1, false, true>), g, b, 0, s, p);
+  } else if (p.out_pos) {
     hipLaunchKernelGGL((probe_win<3>), g, b, 0, s, p);  // C5: match positions too
   } else {
     // 64-byte windows (4 lanes per row: 1.109 instead of 1.169 window reads per row in a host

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CCJ_ABI_VERSION 9  /* 9: CCJ_PART_SHARE, CU-masked streams; 8: CCJ_PART_RANK; 7: CCJ_PART_ROWS */
+#define CCJ_ABI_VERSION 10  /* 10: CCJ_PART_ROWS with positions / payload columns; 9: CCJ_PART_SHARE, CU-masked streams; 8: CCJ_PART_RANK; 7: CCJ_PART_ROWS */
 
 enum ccj_status {
   CCJ_OK = 0,
@@ -204,11 +204,13 @@ int ccj_probe_visits(const ccj_table *table, const int64_t *d_keys, const uint32
 #define CCJ_PART_EXACT 1u
 /* flags & CCJ_PART_ROWS: out_sel receives the ORIGINAL row of every match (u32, row of args->keys)
  * instead of its position inside the chunk, and out_row_map may be NULL.  LP tables of >= 16
- * slots with distinct keys (max_dup 1), cap == chunk, out_payload set, no out_pos / payload
- * columns.  The split then writes each position's key into out_payload and its row into out_sel
- * (position p IS output slot p of its chunk: an LP match's payload is the probe key), and the walk
- * only compacts the chunks where some row missed.  Without the flag, when cap == chunk the keys
- * still go to out_payload (the workspace's key region is then left untouched). */
+ * slots with distinct keys (max_dup 1), cap == chunk, out_payload set; with out_pos / payload
+ * columns (C5) the table may have at most 2^31 slots.  The split then writes each position's key
+ * into out_payload and its row into out_sel (position p IS output slot p of its chunk: an LP
+ * match's payload is the probe key), and the walk only compacts the chunks where some row missed
+ * (with positions / payload columns it writes each match's table position at its output slot,
+ * which the payload gather then reads).  Without the flag, when cap == chunk the keys still go to
+ * out_payload (the workspace's key region is then left untouched). */
 #define CCJ_PART_ROWS 2u
 /* flags & CCJ_PART_RANK: the RANK WALK instead of the slot-array walk (LP tables of distinct keys,
  * cap == chunk, chunk a multiple of 512, windows of <= 2^19 slots; otherwise the flag is ignored).

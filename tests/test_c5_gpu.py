@@ -113,3 +113,41 @@ def test_c5_partitioned(cf):
     assert len(np.unique(pairs)) == len(pairs)
     m, _ = O.count_uniform(21 + cf, 0, n_probe, n_build + n_build // 8, n_build, cf)
     assert len(brow) == m
+
+
+@pytest.mark.parametrize("chunk,n_probe,spread", [(2048, 1 << 20, 8), (2048, (1 << 20) + 777, 0), (1000, 1 << 20, 8),
+                                                  (1022, 300001, 8), (2048, 1 << 20, 1)])
+def test_c5_partitioned_rows(chunk, n_probe, spread):
+    """C5 under CCJ_PART_ROWS (distinct build keys, the bench's C5 route): the split writes every
+    position's row and key into the outputs, probe_walk1<POS> leaves each match's table position at
+    its output slot (all-matched chunks) or compacts the chunk (chunks with a miss), the gather reads
+    them.  spread: probe keys from [0, n_build + n_build / spread) (0: every probe hits; 1: half
+    miss).  sel is the original row; every gathered row belongs to the build tuple with the row's
+    key, the payload column holds the key, and the count is exact."""
+    n_build = 1 << 18
+    bkeys = ref_keys(n_build, 1)
+    pay = payload_rows(n_build)
+    table = ccj.Table.on_device(ccj.LP, torch.from_numpy(bkeys).cuda())
+    table.set_payload(torch.from_numpy(pay.reshape(-1)).cuda(), P)
+    assert int(table.max_dup) <= 1
+    rng = n_build + (n_build // spread if spread else 0)
+    keys = O.uniform_keys(77 + spread, 0, n_probe, rng)
+    out = table.probe_partitioned(torch.from_numpy(keys).cuda(), chunk, pos=True, payload_cols=P, rows=True)
+    torch.cuda.synchronize()
+    assert int(out["status"].item()) == 0
+    nc, cap = out["n_chunks"], out["cap"]
+    assert cap == chunk
+    cnt = out["count"].cpu().numpy()[:nc].astype(np.int64)
+    valid = (np.arange(cap)[None, :] < cnt[:, None]).reshape(-1)
+    prow = out["sel"].cpu().numpy()[:nc * cap].view(np.uint32)[valid].astype(np.int64)  # original rows
+    assert np.array_equal(out["payload"].cpu().numpy()[:nc * cap][valid], keys[prow])
+    col0 = out["payload_cols"][0].cpu().numpy()[:nc * cap][valid]
+    inv = {int(v): r for r, v in enumerate(pay[:, 0])}
+    brow = np.array([inv.get(int(v), -1) for v in col0], np.int64)
+    assert (brow >= 0).all()
+    assert np.array_equal(bkeys[brow], keys[prow])
+    for c in range(1, P):
+        assert np.array_equal(out["payload_cols"][c].cpu().numpy()[:nc * cap][valid], pay[brow, c])
+    assert len(np.unique(prow)) == len(prow)  # distinct keys: one match per probe row at most
+    m, _ = O.count_uniform(77 + spread, 0, n_probe, rng, n_build, 1)
+    assert len(prow) == m
