@@ -2012,9 +2012,8 @@ __device__ __forceinline__ void walk_emit_pos(const ProbeParams &p, SM &sm, uint
   emit_wg_stores<2, kWave * NW>(p, sm, obase, tot, true);
   if (threadIdx.x == 0) sm.total = tot;
 }
-template <int NB, bool MM = false, bool POS = false>
-__global__ __launch_bounds__(kWave * 4) void probe_walk1(ProbeParams p) {
-  constexpr int NW = 4;
+template <int NB, bool MM = false, bool POS = false, int NW = 4>
+__global__ __launch_bounds__(kWave * NW) void probe_walk1(ProbeParams p) {
   constexpr uint32_t kWaveRows = kMaxChunk / NW;  // rows per wave
   __shared__ Walk1Shared<NB, NW> sm;
   char *const s_ring = sm.ring;
@@ -2483,6 +2482,8 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
       hipLaunchKernelGGL((probe_walk1<2>), g, b, 0, s, p);
     else if (ccj_tune_int("CCJ_WALK_NB", 1) == 3)
       hipLaunchKernelGGL((probe_walk1<3>), g, b, 0, s, p);
+    else if (ccj_tune_int("CCJ_WALK_NW", 4) == 8)  // 8 waves x 256 rows: 40 KiB, 4 workgroups = 32 waves per CU
+      hipLaunchKernelGGL((probe_walk1<1, false, false, 8>), g, dim3(kWave * 8), 0, s, p);
     else
       hipLaunchKernelGGL((probe_walk1<1>), g, b, 0, s, p);
   }

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "ccj_internal.h"
+#include "ccj_tuning.h"
 
 namespace ccj {
 namespace {
@@ -190,6 +191,7 @@ struct ccj_pipeline {
     ccj::DevBuf cols[ccj::kCarry + 1];                      // this join's output rows (next input)
     ccj::DevBuf next_counts, seg_base, seg_obase;           // next join's chunks
     ccj::DevBuf compact_ws;
+    ccj::DevBuf ordered_ws;  // ccj_probe_ordered's workspace (large tables)
   };
   std::vector<const ccj_table *> tables;
   uint32_t joins = 0, chunk = 0;
@@ -319,7 +321,42 @@ extern "C" int ccj_pipeline_run(ccj_pipeline *pl, const int64_t *const *d_cols, 
     p.status = (uint32_t *)(tot + 3);
     p.chunk_base = in_base;
     p.out_base = in_obase;
-    PL_TRY(ccj::launch_probe(t->info.kind, p, s), "pipeline probe");
+    // Tables past L2 / the Infinity Cache (>= 2^22 slots or buckets) and inputs of whole chunks
+    // (the first join, or compacted chunks): ccj_probe_ordered — the same per-Next outputs as the
+    // chunk probe, through the slot / bucket partitioned layout, so the table reads are L2 hits
+    // instead of random HBM lines.  Its rare skew overflow re-runs the chunk probe.  Only where the
+    // input fills the split's fixed-capacity segments (positions <= 4/3 rows): a short input spread over
+    // many partitions walks mostly empty chunks (2^25 LHS rows per join, same box: 2^25-key tables
+    // 5.68 / 5.27 ms per pipeline step against 6.24 / 5.36 for chaining / LP, but 2^27-key tables
+    // 7.19 / 6.00 against 6.63 / 5.66 — positions 1.5 x rows there).
+    const size_t ows = in_base || in_obase ? 0 : ccj_probe_ordered_workspace_size(t, in_phys, B);
+    const bool dense = ows && ccj_probe_partitioned_positions(t, in_phys, B) * 3 <= in_phys * 4;
+    if (dense && ccj_tune_int("CCJ_PIPE_ORDERED", 1)) {
+      PL_TRY(L.ordered_ws.ensure(ows), "alloc");
+      ccj_probe_args a{};
+      a.keys = p.keys;
+      a.counts = in_counts;
+      a.n_rows = in_phys;
+      a.chunk = B;
+      a.max_rounds = R;
+      a.cap = cap;
+      a.out_count = p.out_count;
+      a.out_sel = p.out_sel;
+      a.out_payload = p.out_payload;
+      a.out_rounds = p.out_rounds;
+      a.out_round_counts = p.out_round_counts;
+      a.status = p.status;
+      if (int rc = ccj_probe_ordered(t, &a, L.ordered_ws.p, L.ordered_ws.bytes, stream)) return rc;
+      uint64_t st = 0;
+      PL_TRY(hipMemcpyAsync(&st, tot + 3, sizeof(st), hipMemcpyDeviceToHost, s), "copy status");
+      PL_TRY(hipStreamSynchronize(s), "sync");
+      if (st & CCJ_FLAG_PART_OVERFLOW) {
+        PL_TRY(hipMemsetAsync(tot + 3, 0, 8, s), "memset");
+        PL_TRY(ccj::launch_probe(t->info.kind, p, s), "pipeline probe");
+      }
+    } else {
+      PL_TRY(ccj::launch_probe(t->info.kind, p, s), "pipeline probe");
+    }
 
     // Output sizes: matches and non-empty Next results, per chunk and in total.
     PL_TRY(L.rows.ensure(in_chunks * 8), "alloc");

@@ -169,3 +169,32 @@ def test_gated_and_dynamic_compaction_match_reference(name, mode):
     assert (res["n_out"], res["l2"]) == (KA[name]["n_out"], KA[name]["l2"])
     if mode == "dynamic":
         assert p.stderr.count("TUNER join") == 3
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+@pytest.mark.parametrize("compact", [False, True])
+def test_pipeline_large_tables_ordered_route_l3(kind, compact):
+    """Tables past L2 / the Infinity Cache (>= 2^22 slots or buckets): ccj_pipeline_run probes the
+    first join and every compacted input through ccj_probe_ordered (split + L2-resident walk +
+    unsplit + reference-order emit) when the input fills the split's segments.  The whole result
+    table in order (L3) against the oracle pipeline, cf 2 (runs / chains of several keys), ragged
+    last chunk."""
+    import torch
+    import ccj
+    from oracle import oracle as O
+    dev = _dev()
+    joins, n, rhs, cf, B = 3, (1 << 22) + 777, (1 << 22) + 5, 2, 2048
+    cols = _inputs(joins, n, rhs, 29)
+    dt = [ccj.Table.reference(kind, rhs, cf, ccj.LAYOUT_REFERENCE) for _ in range(joins)]
+    # the partitioned route applies, and the input fills its segments (the pipeline's gate)
+    assert dt[0].alloc_ordered(n, B) is not None
+    assert ccj.lib().ccj_probe_partitioned_positions(dt[0]._h, n, B) * 3 <= n * 4
+    ot = [O.Table(kind, O.ref_build_keys(rhs, cf)) for _ in range(joins)]
+    want = oracle_pipeline(ot, cols, B, compact, cap_factor=cf)
+    pl = ccj.Pipeline(dt, B, compact)
+    pl.run([torch.from_numpy(c).to(dev) for c in cols])
+    got = pl.result_columns()
+    got = got[:joins] + [got[joins + 2 * l + 1] for l in range(joins)]
+    assert pl.res.n_out == len(want[0]) > 0
+    for g, w in zip(got, want):
+        np.testing.assert_array_equal(g, w)
