@@ -119,6 +119,7 @@ struct ProbeParams {
   // window's first reads hit L2 (0: off); pf_lines lines per chunk
   uint64_t pf_dist;
   uint32_t pf_lines;
+  uint32_t kp_dist;  // tuning build (CCJ_ABLATE 0x400): key-line touch distance in chunks
 };
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 constexpr uint32_t kEmitWave = 0xFFFFFFFFu;

@@ -2027,6 +2027,15 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk1(ProbeParams p) {
   const uint32_t w0 = wave * kWaveRows;
   const uint32_t wend = phys > w0 ? (phys - w0 < kWaveRows ? phys : w0 + kWaveRows) : w0;  // wave's rows [w0, wend)
   if (p.pf_dist && wave == 0) walk_prefetch(p, c, lane, (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)sm.hc);
+  if (CCJ_ABLATED(p.ablate, 0x400u)) {  // (tuning: touch the keys of the chunk kp_dist later on this XCD)
+    const uint64_t c2 = c + p.kp_dist;
+    const uint64_t per = p.n_chunks / 8;
+    if (per && c2 < p.n_chunks && c2 / per == c / per) {
+      const uint32_t m0 = (uint32_t)__builtin_amdgcn_readfirstlane(
+          (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)&sm.hc[w0]);
+      dma16(p.keys + c2 * p.chunk + w0 + (lane & 31u) * 16u, m0);
+    }
+  }
   // (timing only, tuning build: 0x100 stages the keys of chunk c & 63 — L2-resident key lines)
   walk_stage<kWaveRows, true>(p, sm, CCJ_ABLATED(p.ablate, 0x100u) ? (c & 63u) * p.chunk : base, w0, wend, lane);
   CCJ_STAMP(t1);

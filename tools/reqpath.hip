@@ -63,7 +63,7 @@ __global__ __launch_bounds__(256) void reqpath(const int64_t *table, uint32_t re
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
           st = lcg(st);
-          const uint32_t w = (st >> 8) & region_mask & ~(uint32_t)(LN / 2 - 1);
+          const uint32_t w = (st >> 8) & region_mask & ~(uint32_t)((LN >= 2 ? LN / 2 : 1) - 1);
           const int64_t *src = base + (uint64_t)w * 4 + 2 * sub;
           // inline asm: the builtin's address computation was hoisted out of the loop by the compiler
           // (every iteration re-read the same windows: round 3's first "2x" reading was that artifact)
@@ -334,6 +334,17 @@ int main() {
     run_policy<17>(table, sink);
     run_policy<18>(table, sink);
     run_policy<19>(table, sink);
+    return 0;
+  }
+  if (mode && !strcmp(mode, "lanes")) {  // LDS-DMA lanes per window: 16 / 32 / 64 / 128-byte windows
+    run<3, 0, true, 1>("lds16B", table, 19u, 6, it, sink);
+    run<3, 0, true, 2>("lds32B", table, 19u, 6, it, sink);
+    run<3, 0, true, 4>("lds64B", table, 19u, 6, it, sink);
+    run<3, 0, true, 8>("lds128B", table, 19u, 6, it, sink);
+    run<1, 0, true, 1>("lds16B_1", table, 19u, 6, it, sink);
+    run<1, 0, true, 2>("lds32B_1", table, 19u, 6, it, sink);
+    run<3, 0, false, 1>("vec16B", table, 19u, 6, it, sink);
+    run<3, 0, false, 2>("vec32B", table, 19u, 6, it, sink);
     return 0;
   }
   if (mode && !strcmp(mode, "sizes")) {  // request sizes from HBM (run under rocprofv3 --pmc)
