@@ -650,6 +650,9 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   }
   p.keys = pkeys;
   p.xcd_swizzle = 1;  // consecutive chunks (one partition's rows) go to one XCD: its L2 holds the window
+  // distinct build keys and no per-chunk rounds: the walk ends a row at its match (C2: 1.168 -> 1.013
+  // windows per row in a host simulation of the walk's windows)
+  p.first_match = t->info.max_dup <= 1 && !a->out_rounds && ccj_tune_int("CCJ_FIRST_MATCH", 1) ? 1u : 0u;
   // probe_walk's emit: the chunk's matches staged in LDS, 16-byte non-temporal stores (C2 walk
   // 14.04-14.07 ms per step against 14.19-14.20 with per-wave 4/8-byte stores; write-through sc1
   // 16-byte stores 14.6, plain 15.2; CCJ_EMIT_POL = -1 is the per-wave form)

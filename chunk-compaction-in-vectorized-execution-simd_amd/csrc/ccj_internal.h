@@ -120,6 +120,9 @@ struct ProbeParams {
   uint64_t pf_dist;
   uint32_t pf_lines;
   uint32_t kp_dist;  // tuning build (CCJ_ABLATE 0x400): key-line touch distance in chunks
+  // probe_walk1: the table's keys are distinct (max_dup 1) and no rounds are asked for, so a row
+  // stops at its match instead of walking to the end of its run (same matches and multiplicities)
+  uint32_t first_match;
 };
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 constexpr uint32_t kEmitWave = 0xFFFFFFFFu;

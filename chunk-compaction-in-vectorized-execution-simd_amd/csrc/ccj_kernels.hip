@@ -2098,8 +2098,10 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk1(ProbeParams p) {
       if (MM) cnt[b] |= r0[b] < kMmRounds ? hits << r0[b] : 0u;  // rounds >= 26 end as long rows
       else cnt[b] += (uint32_t)__builtin_popcount(hits);
       if (POS && hits) mpos[b] = cur[b] + (uint32_t)__builtin_ctz(hits);
-      if (ee) {
-        const uint32_t r = r0[b] + f;  // occupied slots walked = the reference's rounds
+      // p.first_match (distinct build keys, no rounds asked for): a row's only possible match
+      // ends its walk — the rest of its run cannot hold its key again
+      if (ee || (!MM && p.first_match && hits)) {
+        const uint32_t r = r0[b] + f;  // occupied slots walked = the reference's rounds (run end)
         lane_rounds = r > lane_rounds ? r : lane_rounds;
         if (MM) cnt[b] = r <= kMmRounds ? (cnt[b] & ((1u << kMmRounds) - 1u)) | r << kMmRounds : kMmLong | r;
         if (CCJ_ABLATED(p.ablate, 0x200u)) cnt[b] = 1;  // (timing only: the emit path of the real data)
