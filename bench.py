@@ -46,7 +46,7 @@ METRIC = "probe tuples/sec + achieved HBM GB/s, 1B-row int64 join at 1/2/4/8 GPU
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
 SEED = 42
 PATH_KERNELS = {
-    "partitioned": "ccj_probe_partitioned, CCJ_PART_ROWS (slot_split_pipe writing keys + rows into the outputs, probe_walk1<1>: one lane per row, LDS-DMA table windows)",
+    "partitioned": "ccj_probe_partitioned, CCJ_PART_ROWS (slot_split_pipe writing keys + rows into the outputs, probe_walk2: one lane per row, LDS-DMA table windows, a row ends at its match (distinct keys))",
     "rank": "ccj_probe_partitioned, CCJ_PART_ROWS | CCJ_PART_RANK (slot_split_pipe + probe_rank: the window's occupancy "
             "bitmap + rank in LDS, keys from the compact array; rank_finish) — opt-in, A/B",
     "ordered": "ccj_probe_ordered (slot_split_pipe with runs + probe_walk1<1,MM> + unsplit_words + emit_ordered, 16-bit round words)",
@@ -762,7 +762,7 @@ def main():
                          # measured DRAM bytes (whole 128-B lines per random slot read) per second
                          "traffic_GBps": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
                          "kernel": (("ccj_probe_partitioned, CCJ_PART_ROWS (slot_split_pipe writing keys + rows, "
-                                     "probe_walk1<1, POS> writing match positions, gather_payload_quad)") if c5 and
+                                     "probe_walk2<POS> writing match positions, gather_payload_quad)") if c5 and
                                     args.path == "partitioned" and rows_mode else
                                     ("ccj_probe_partitioned (slot_split_pipe + probe_win<3> with positions + "
                                      "gather_payload_quad)") if c5 and args.path == "partitioned" else

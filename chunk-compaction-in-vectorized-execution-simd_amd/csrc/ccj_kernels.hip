@@ -2179,6 +2179,168 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk1(ProbeParams p) {
   walk_finish(p, sm, c, lane, lane_rounds, overflow, t0, t1, t2, steps);
 }
 
+// probe_walk2<POS>: probe_walk1 for tables of distinct keys with no rounds asked for
+// (p.first_match), where a row's walk ends at its match and 98.7 % of C2's rows end in their first
+// 32-byte window.  Phase A gives every row its first window with a fixed assignment — lane L of
+// wave w walks row w0 + 64 j + L in step j — so the row's key and home slot stay in the registers
+// the stage loaded and hashed them into: no refill ballot, no LDS reads of the row before its
+// DMA, about half of probe_walk1's instructions per batch.  A row whose run continues past that
+// window (no match yet, no empty slot) leaves its next slot in sm.hc and a bit in its lane's mask;
+// phase B walks those rows lane by lane (a lane takes its next continuing row as soon as one
+// finishes).  Same outputs as probe_walk1 (counts 0 / 1, or matched | slot for POS) in sm.hc,
+// then the same emits.
+template <bool POS>
+__global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
+  constexpr int NW = 4;
+  constexpr uint32_t kWaveRows = kMaxChunk / NW;      // rows per wave
+  constexpr int kJ = (int)(kWaveRows / kWave);         // row groups (phase-A steps) per wave
+  __shared__ Walk1Shared<1, NW> sm;
+  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  unsigned long long t0, t1, t2;
+  uint32_t steps = 0;
+  CCJ_STAMP(t0);
+  const uint64_t c = walk_chunk_index(p);
+  const uint64_t base = c * p.chunk;
+  const uint32_t phys = flat_phys(p, base);
+  const uint32_t w0 = wave * kWaveRows;
+  const uint32_t wend = phys > w0 ? (phys - w0 < kWaveRows ? phys : w0 + kWaveRows) : w0;  // wave's rows [w0, wend)
+  // stage: keys (all loads in flight first) and home slots stay in registers; the keys also go to
+  // LDS for phase B and the emit's compaction
+  int64_t k[kJ];
+  uint32_t h[kJ];
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) {
+    const uint32_t i = w0 + (uint32_t)j * kWave + lane;
+    k[j] = i < wend ? __builtin_nontemporal_load(p.keys + base + i) : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) {
+    sm.key[w0 + (uint32_t)j * kWave + lane] = k[j];
+    h[j] = (uint32_t)murmurhash64((uint64_t)k[j]) & p.mask;
+  }
+  CCJ_STAMP(t1);
+  char *ring = sm.ring + wave * kRingSlot;
+  const uint32_t ring_lds = (uint32_t)__builtin_amdgcn_readfirstlane(
+      (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)ring);
+  const char *win = ring + (lane & 1u) * 1024 + (lane >> 1) * 32;  // this lane's window, once landed
+  const uint32_t last_start = p.mask - (kWin - 1);  // table size - window (size >= 16)
+  const uint32_t half = (lane & 1u) * 2u;
+  // the window [s, s + kWin) that holds slot `cur` (never past the table's end or its 128-byte line)
+  auto start = [&](uint32_t cur) {
+    uint32_t s = cur < last_start ? cur : last_start;
+    const uint32_t lim = (s & ~15u) + (16u - kWin);
+    return s < lim ? s : lim;
+  };
+  // Every lane issues (an idle one loads slot 0's line), and with all lanes active: the DPP moves
+  // read the pair's other lane, so a lane switched off here would hand its partner a stale address.
+  // The callers keep these in uniform control flow (phase B's loop exits on a ballot, like
+  // probe_walk1's; a `while (__ballot(...))` form was structurised into a nested loop whose lanes
+  // left one by one — the DMAs then ran with lanes off and read wild addresses).
+  auto issue = [&](uint32_t a) {
+    uint32_t a0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, 0xA0, 0xF, 0xF, false);  // quad_perm 0,0,2,2
+    uint32_t a1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, 0xF5, 0xF, 0xF, false);  // quad_perm 1,1,3,3
+    a0 = a0 < last_start ? a0 : last_start;  // (a guard: whatever a DPP returns, the DMA stays in the table)
+    a1 = a1 < last_start ? a1 : last_start;
+    dma16(p.table + a0 + half, ring_lds);
+    dma16(p.table + a1 + half, ring_lds + 1024u);
+  };
+  // the landed window against key kk from slot cur (window start s): hits (bits from cur) and
+  // whether the run ends inside the window
+  auto look = [&](int64_t kk, uint32_t cur, uint32_t s, uint32_t &hits) {
+    const longlong2 x0 = *reinterpret_cast<const longlong2 *>(win);
+    const longlong2 x1 = *reinterpret_cast<const longlong2 *>(win + 16);
+    const uint32_t e = (x0.x == -1 ? 1u : 0u) | (x0.y == -1 ? 2u : 0u) | (x1.x == -1 ? 4u : 0u) | (x1.y == -1 ? 8u : 0u);
+    const uint32_t m = (x0.x == kk ? 1u : 0u) | (x0.y == kk ? 2u : 0u) | (x1.x == kk ? 4u : 0u) | (x1.y == kk ? 8u : 0u);
+    const uint32_t off = cur - s;
+    const uint32_t ee = e >> off;
+    const uint32_t f = (uint32_t)__builtin_ctz(ee | ((1u << kWin) >> off));  // run end (or window end) past cur
+    hits = (m >> off) & ((1u << f) - 1u);
+    return ee != 0u || hits != 0u;
+  };
+  auto result = [&](uint32_t cur, uint32_t hits) {
+    return POS ? (hits ? (cur + (uint32_t)__builtin_ctz(hits)) | 0x80000000u : 0u) : (hits ? 1u : 0u);
+  };
+  // phase A: every row's first window
+  uint32_t cont = 0;
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) {
+    ++steps;
+    const uint32_t i = w0 + (uint32_t)j * kWave + lane;
+    const bool valid = i < wend;
+    const uint32_t s = start(h[j]);
+    issue(valid ? s : 0u);
+    wait_vmcnt<0>();
+    if (valid) {
+      uint32_t hits;
+      if (look(k[j], h[j], s, hits)) {
+        sm.hc[i] = result(h[j], hits);
+      } else {
+        sm.hc[i] = (s + kWin) & p.mask;  // the next unread slot
+        cont |= 1u << j;
+      }
+    }
+  }
+  // phase B: the rows whose run went on, each lane its own, one window per step
+  if (__ballot(cont != 0u)) {
+    bool have = false;
+    uint32_t bi = 0, bcur = 0, bst = 0;
+    int64_t bkey = 0;
+    auto take = [&]() {
+      if (!have && cont) {
+        const uint32_t j = (uint32_t)__builtin_ctz(cont);
+        cont &= cont - 1u;
+        bi = w0 + j * kWave + lane;
+        bkey = sm.key[bi];
+        bcur = sm.hc[bi];
+        have = true;
+      }
+    };
+    take();
+    bst = start(bcur);
+    issue(have ? bst : 0u);
+    for (bool more = true; more;) {
+      ++steps;
+      wait_vmcnt<0>();
+      if (have) {
+        uint32_t hits;
+        if (look(bkey, bcur, bst, hits)) {
+          sm.hc[bi] = result(bcur, hits);
+          have = false;
+        } else {
+          bcur = (bst + kWin) & p.mask;
+        }
+      }
+      take();
+      if (__ballot(have) == 0ull) {  // every lane's rows done
+        more = false;
+        break;
+      }
+      bst = start(bcur);
+      issue(have ? bst : 0u);
+    }
+  }
+  CCJ_STAMP(t2);
+  __syncthreads();  // every wave's ring is idle: the emit's scratch may overlap it
+  if (tid == 0) {
+    sm.total = 0;
+    sm.rounds = 0;
+  }
+  __syncthreads();
+  if (POS) {
+    walk_emit_pos<kWaveRows, NW>(p, sm, c, w0, wend, lane, wave, sm.wtot, phys);
+    walk_finish(p, sm, c, lane, 0u, 0u, t0, t1, t2, steps);
+    return;
+  }
+  if (p.emit_pol != kEmitWave || p.rows_in_sel) {
+    if (walk_emit_wg<kWaveRows, NW>(p, sm, c, w0, wend, lane, wave, sm.wtot, phys)) {
+      walk_finish(p, sm, c, lane, 0u, 0u, t0, t1, t2, steps);
+      return;
+    }
+  }
+  const uint32_t overflow = walk_emit<kWaveRows>(p, sm, c, w0, wend, lane);
+  walk_finish(p, sm, c, lane, 0u, overflow, t0, t1, t2, steps);
+}
+
 // Ordered probe, step 4 (emit_ordered): one chunk per 256-thread workgroup, the reference's
 // per-Next stream from its rows' round words (p.in_w: mm | rounds << 26, or kMmLong | rounds).
 // Thread (wave, lane) owns rows q*256 + tid (q < 8), i.e. row group j = 4q + wave, lane `lane`:
@@ -2471,10 +2633,12 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
   // lane per row with two 16-B loads (twice the L2 requests) 11.0-12.3 ms; a rolling load
   // pipeline (each slot re-issued as soon as it is consumed, vmcnt(R - 1) waits) 10.4-10.5 ms;
   // write-through (sc1) or plain output stores 10.2 ms vs non-temporal.
+  const bool walk2 = p.first_match && ccj_tune_int("CCJ_WALK2", 1);
   if (p.out_pos && p.rows_in_sel) {
     // C5 under CCJ_PART_ROWS (distinct keys, tables of <= 2^31 slots): the split wrote rows and keys,
-    // probe_walk1 leaves each row's matched slot at its output slot
-    hipLaunchKernelGGL((probe_walk1<1, false, true>), g, b, 0, s, p);
+    // the walk leaves each row's matched slot at its output slot
+    if (walk2) hipLaunchKernelGGL((probe_walk2<true>), g, b, 0, s, p);
+    else hipLaunchKernelGGL((probe_walk1<1, false, true>), g, b, 0, s, p);
   } else if (p.out_pos) {
     hipLaunchKernelGGL((probe_win<3>), g, b, 0, s, p);  // C5: match positions too
   } else {
@@ -2493,6 +2657,8 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
       hipLaunchKernelGGL((probe_walk1<2>), g, b, 0, s, p);
     else if (ccj_tune_int("CCJ_WALK_NB", 1) == 3)
       hipLaunchKernelGGL((probe_walk1<3>), g, b, 0, s, p);
+    else if (walk2)  // distinct keys, no rounds: fixed first windows, then the rows that go on
+      hipLaunchKernelGGL((probe_walk2<false>), g, b, 0, s, p);
     else if (ccj_tune_int("CCJ_WALK_NW", 4) == 8)  // 8 waves x 256 rows: 40 KiB, 4 workgroups = 32 waves per CU
       hipLaunchKernelGGL((probe_walk1<1, false, false, 8>), g, dim3(kWave * 8), 0, s, p);
     else
