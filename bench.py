@@ -568,6 +568,8 @@ def main():
     t0 = time.perf_counter()
     c5 = args.workload == "c5"
     P = 8 if c5 else 0
+    # the rank walk is in libccj_tuning.so only: timed beside the headline with --lib tuning
+    rank_ab = args.path == "partitioned" and not c5 and not args.no_other and args.lib == "tuning"
     with torch.cuda.stream(stream):
         table = ccj.Table.reference(ccj.LP, n_build, 1, layout, stream=stream)
         if c5:  # C5 payload of build tuple t (key k): p_c = k*(c+1)+c, row-major [n_build, 8]
@@ -585,7 +587,7 @@ def main():
             out_o = table.alloc_outputs(n_probe, chunk, rounds=True)
             ws_o = table.alloc_ordered(n_probe, chunk)
         if args.path == "partitioned" or every:
-            if not c5 and not args.no_other:  # the rank walk is timed beside the headline (A/B)
+            if rank_ab:  # the rank walk (tuning build only) is timed beside the headline (A/B)
                 table.build_rank_index(stream=stream)
             part = table.alloc_partitioned(n_probe, chunk)
             # C5: the match positions the payload gather reads are a caller-owned buffer, so no
@@ -656,7 +658,7 @@ def main():
         matches, l2 = ccj.result_checksum(res0, chunk, row_base=rank * n_probe, stream=stream)
     # the other paths, timed the same way (reported beside the headline)
     others = [] if c5 or args.no_other else [q for q in ("ordered", "chunk", "partitioned") if q != args.path]
-    if args.path == "partitioned" and not c5 and not args.no_other:
+    if rank_ab:
         others.append("rank")  # A/B: the rank walk on the same split, same run
     other_runs = {}
     for other in others:

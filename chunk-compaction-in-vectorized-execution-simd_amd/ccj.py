@@ -17,14 +17,16 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libccj.so")
+# the product library; CCJ_LIB_PATH names another build (tests/test_rank_gpu.py runs the rank walk's
+# checks against libccj_tuning.so, the only build that contains it)
+LIB_PATH = os.environ.get("CCJ_LIB_PATH") or os.path.join(HERE, "libccj.so")
 
 LP, CHAIN = 0, 1
 LAYOUT_REFERENCE, LAYOUT_DEVICE = 0, 1
 FLAG_CAP_OVERFLOW, FLAG_ROUND_OVERFLOW, FLAG_BAD_INPUT, FLAG_PART_OVERFLOW = 1, 2, 4, 8
 PART_EXACT = 1
 PART_ROWS = 2  # out_sel = the original row of every match (ccj.h CCJ_PART_ROWS)
-PART_RANK = 4  # the rank walk (LDS window index) instead of the slot-array walk (ccj.h CCJ_PART_RANK)
+PART_RANK = 4  # the rank walk (LDS window index; libccj_tuning.so only) instead of the slot-array walk
 PART_SHARE = 8  # the split leaves 1/4 of the CUs to other streams (ccj.h CCJ_PART_SHARE; multi-GPU step)
 
 _lib = None
@@ -272,7 +274,8 @@ class Table:
         self.n_payload_cols = n_cols
 
     def build_rank_index(self, stream=None):
-        """The rank walk's window index (ccj_table_build_rank_index; CCJ_PART_RANK needs it)."""
+        """The rank walk's window index (ccj_table_build_rank_index; CCJ_PART_RANK needs it).  Only
+        libccj_tuning.so contains the rank walk: libccj.so refuses with CCJ_ERR_INVALID."""
         check(lib().ccj_table_build_rank_index(self._h, _stream(stream)), "ccj_table_build_rank_index")
 
     def probe_cost(self, keys, stream=None):

@@ -117,6 +117,7 @@ int upload(void **dst, const void *src, size_t bytes, const char *what) {
   return CCJ_OK;
 }
 
+#ifdef CCJ_RANK_WALK
 // The rank walk's window index (ccj_rank.hip), built on the device from the finished slot array for
 // tables the partitioned probe splits into windows the LDS can hold (<= 2^19 slots).  Build-time
 // work like the table itself (main.cpp:62-68 times neither).  Without it the slot-array walk runs.
@@ -153,6 +154,13 @@ int build_rank_index(ccj_table *t, hipStream_t s) {
   t->rank_wbits = pl.window_bits;
   return CCJ_OK;
 }
+#else
+// The rank walk (ccj_rank.hip, DESIGN §3.3: measured slower than the slot-array walk) is built into
+// libccj_tuning.so only; the product library refuses its index and flag.
+int build_rank_index(ccj_table *, hipStream_t) {
+  return fail(CCJ_ERR_INVALID, "ccj_table_build_rank_index: the rank walk is built into libccj_tuning.so only");
+}
+#endif
 
 int build_lp_host(const int64_t *keys, uint64_t n, ccj_table **out) {
   const uint64_t size = lp_num_slots(n);
@@ -574,7 +582,11 @@ size_t ccj_probe_partitioned_workspace_size(const ccj_table *t, uint64_t n_rows,
   const size_t fixed = align256(((uint64_t)L.parts * 8 + 1) * 4);
   const size_t exact = ccj::slot_partition_workspace(n_rows, L.pl);
   // + the rank walk's per-block hit masks, hit counts and partition counters
+#ifdef CCJ_RANK_WALK
   const size_t rank = t->d_ckeys && L.pl.lo_bits ? ccj::rank_workspace(L.positions, L.parts) : 0;
+#else
+  const size_t rank = 0;
+#endif
   return align256(L.positions * 8) + align256(fixed > exact ? fixed : exact) + rank;
 }
 
@@ -594,8 +606,13 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   if (a->n_rows >= (1ull << 32)) return fail(CCJ_ERR_LIMIT, "ccj_probe_partitioned: n_rows must be < 2^32");
   if (flags & ~(CCJ_PART_EXACT | CCJ_PART_ROWS | CCJ_PART_RANK | CCJ_PART_SHARE))
     return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: unknown flags");
+#ifdef CCJ_RANK_WALK
   if ((flags & CCJ_PART_RANK) && !t->d_ckeys && rank_index_applies(t))  // refused before any launch
     return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: CCJ_PART_RANK needs ccj_table_build_rank_index first");
+#else
+  if (flags & CCJ_PART_RANK)
+    return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: CCJ_PART_RANK: the rank walk is built into libccj_tuning.so only");
+#endif
   const bool rows = (flags & CCJ_PART_ROWS) != 0;
   // (with positions / payload columns the walk packs matched | slot into 32 bits: <= 2^31 slots)
   if (rows && (!a->out_payload || p.cap != a->chunk || t->info.max_dup > 1 || t->info.kind != CCJ_TABLE_LP ||
@@ -672,6 +689,7 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
     }
   }
 #endif
+#ifdef CCJ_RANK_WALK
   // The rank walk (CCJ_PART_RANK, ccj_rank.hip): the window index in LDS, candidate keys from the
   // compact array.  Distinct keys (a row matches at most once), the keys in out_payload (cap ==
   // chunk), blocks of 512 rows inside chunks, the index built for this window size.
@@ -686,6 +704,7 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
     HIP_TRY(ccj::launch_probe_rank(p, ix, rws, s), "rank walk launch");
     return CCJ_OK;
   }
+#endif
   if (p.n_pay == 0) {
 #ifdef CCJ_TUNING
     // CCJ_STATS: per-phase cycle sums of the walk's waves, printed per launch (tuning only)

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CCJ_ABI_VERSION 10  /* 10: CCJ_PART_ROWS with positions / payload columns; 9: CCJ_PART_SHARE, CU-masked streams; 8: CCJ_PART_RANK; 7: CCJ_PART_ROWS */
+#define CCJ_ABI_VERSION 11  /* 11: the rank walk in the tuning build only; 10: CCJ_PART_ROWS with positions / payload columns; 9: CCJ_PART_SHARE, CU-masked streams; 8: CCJ_PART_RANK; 7: CCJ_PART_ROWS */
 
 enum ccj_status {
   CCJ_OK = 0,
@@ -107,7 +107,8 @@ int ccj_table_free(ccj_table *table);
  * and the occupied slots' keys in slot order, built on the device from the finished LP table
  * (size/8 + size/32 + n_keys*8 bytes: 560 MiB at C2).  A no-op for tables the rank walk does not
  * serve (chaining, one window, windows > 2^19 slots).  Build-time work, like the table.  Call it
- * before sizing the partitioned workspace (ccj_probe_partitioned_workspace_size grows with it). */
+ * before sizing the partitioned workspace (ccj_probe_partitioned_workspace_size grows with it).
+ * The rank walk is built into libccj_tuning.so only; libccj.so returns CCJ_ERR_INVALID. */
 int ccj_table_build_rank_index(ccj_table *table, ccj_stream stream);
 
 /* ---- probe -------------------------------------------------------------------------------- */
@@ -212,7 +213,9 @@ int ccj_probe_visits(const ccj_table *table, const int64_t *d_keys, const uint32
  * which the payload gather then reads).  Without the flag, when cap == chunk the keys still go to
  * out_payload (the workspace's key region is then left untouched). */
 #define CCJ_PART_ROWS 2u
-/* flags & CCJ_PART_RANK: the RANK WALK instead of the slot-array walk (LP tables of distinct keys,
+/* flags & CCJ_PART_RANK (libccj_tuning.so only — libccj.so, the product, refuses the flag and
+ * ccj_table_build_rank_index with CCJ_ERR_INVALID: the rank walk measured slower):
+ * the RANK WALK instead of the slot-array walk (LP tables of distinct keys,
  * cap == chunk, chunk a multiple of 512, windows of <= 2^19 slots; otherwise the flag is ignored).
  * Each partition's window index (occupancy bitmap + occupied-slot rank per 128 slots, built with
  * the table) is held in LDS, so a row's run [home, first empty) costs no memory read and its

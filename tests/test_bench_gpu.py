@@ -1,6 +1,6 @@
 """bench.py end to end at small sizes, one process per workload: the JSON line of the driver's
-contract for every workload and path (C2 partitioned with the rank-walk A/B and the reference-order
-paths beside it, C2 ordered, C3 with compaction, C5 with payload columns, the main.cpp pipeline),
+contract for every workload and path (C2 partitioned with the reference-order paths beside it, and
+the tuning build's rank-walk A/B, C2 ordered, C3 with compaction, C5 with payload columns, the main.cpp pipeline),
 with the bench's own full-size-style parity checks green.  Catches a broken bench path before the
 driver's round-end run does."""
 import json
@@ -28,6 +28,18 @@ def run_bench(*extra):
 
 def test_bench_c2_with_other_paths():
     line = run_bench()
+    par = line["parity"]
+    assert par["status_flags"] == 0 and par["l1_ok"] and par["l2_ok"]
+    paths = {o["path"]: o for o in line["other_paths"]}
+    assert set(paths) == {"ordered", "chunk"}
+    for o in paths.values():
+        assert o["check"]["status_flags"] == 0 and o["check"]["l1_ok"] and o["check"]["l2_ok"]
+    assert paths["ordered"]["check"]["equals_chunk_path_l3"]
+
+
+def test_bench_c2_tuning_build_with_rank_ab():
+    """--lib tuning: the same line, with the rank walk (tuning build only) timed beside the headline."""
+    line = run_bench("--lib", "tuning")
     par = line["parity"]
     assert par["status_flags"] == 0 and par["l1_ok"] and par["l2_ok"]
     paths = {o["path"]: o for o in line["other_paths"]}
