@@ -477,3 +477,77 @@ def test_ordered_probe_skew_retries_chunk_path():
     got = host(table.probe_ordered(keys, 2048))
     assert got["status"][0] == 0 and got.get("exact_retry")
     assert np.array_equal(got["count"], want["count"]) and np.array_equal(got["sel"], want["sel"])
+
+
+def _np_murmur(x):
+    """hash_functions.h:8-16 on a uint64 array (wrapping multiplies)."""
+    x = x.astype(np.uint64)
+    c = np.uint64(0xd6e8feb86659fd93)
+    with np.errstate(over="ignore"):
+        x ^= x >> np.uint64(32)
+        x *= c
+        x ^= x >> np.uint64(32)
+        x *= c
+        x ^= x >> np.uint64(32)
+    return x
+
+
+@pytest.mark.parametrize("mode", ["rows", "positions", "plain", "payload"])
+def test_partitioned_walk_long_runs_across_windows(mode):
+    """probe_walk2 (distinct keys: a row ends at its match, phase B for rows whose run goes on) on
+    runs hundreds of keys long that cross a 2^19-slot window's end and wrap around the table's:
+    a host-built table of 2^18 keys in 2^20 slots with 400-key clusters hashed just below each
+    window's end.  Probes: every build key, repeats, misses (which walk whole clusters) and the
+    cluster keys again.  L1 + L2 exact in rows mode, with positions (every position holds its key),
+    in plain mode (row map) and with payload columns (CCJ_PART_ROWS + walk2<POS> + gather)."""
+    g = np.random.default_rng(11)
+    size = 1 << 20
+    cand = np.unique(g.integers(1, 1 << 40, size=1 << 24, dtype=np.int64))
+    g.shuffle(cand)
+    home = (_np_murmur(cand.astype(np.uint64)) & np.uint64(size - 1)).astype(np.int64)
+    edge0 = cand[(home >= (1 << 19) - 96) & (home < (1 << 19))][:400]
+    edge1 = cand[(home >= size - 96)][:400]
+    assert len(edge0) == 400 and len(edge1) == 400
+    rest = np.setdiff1d(cand[:600000], np.concatenate([edge0, edge1]))
+    n_build = 1 << 18
+    build = np.concatenate([edge0, edge1, rest[:n_build - 800]])
+    g.shuffle(build)
+    table = ccj.Table.from_host(ccj.LP, build)
+    assert table.size == size and int(table.max_dup) == 1
+    pk = np.concatenate([build, build[:1000], rest[n_build:n_build + 50000], edge0, edge1, edge1])
+    g.shuffle(pk)
+    keys = torch.from_numpy(pk).cuda()
+    hit = np.isin(pk, build)
+    r = np.nonzero(hit)[0].astype(np.uint64)
+    want = (len(r), O.l2_sum(r, pk[hit]))
+    if mode == "payload":
+        pay = (build.astype(np.int64)[:, None] * 3 + np.arange(8, dtype=np.int64)[None, :]).reshape(-1)
+        table.set_payload(torch.from_numpy(pay).cuda(), 8)
+        out = table.probe_partitioned(keys, 2048, rows=True, pos=True, payload_cols=8)
+    else:
+        out = table.probe_partitioned(keys, 2048, rows=mode != "plain", pos=mode == "positions")
+    torch.cuda.synchronize()
+    assert int(out["status"].item()) == 0
+    if mode == "plain":
+        assert ccj.result_checksum(out, 2048, row_map=out["row_map"].to(torch.int64)) == want
+    else:
+        assert ccj.result_checksum(out, 0) == want
+    if mode in ("positions", "payload"):
+        nc, cap = out["n_chunks"], out["cap"]
+        cnt = out["count"][:nc].to(torch.int64).cpu().numpy()
+        valid = (np.arange(cap)[None, :] < cnt[:, None]).reshape(-1)
+        pos = out["pos"].cpu().numpy()[:nc * cap].view(np.uint32)[valid]
+        key = out["payload"].cpu().numpy()[:nc * cap][valid]
+        slots = np.full(size, -1, np.int64)
+        # the table's slot array, host-built in the reference's order
+        for k in build:
+            s = int(_np_murmur(np.array([k], np.uint64))[0] & np.uint64(size - 1))
+            while slots[s] != -1:
+                s = (s + 1) & (size - 1)
+            slots[s] = k
+        assert np.array_equal(slots[pos], key)  # every recorded position holds its row's key
+        if mode == "payload":
+            for c in (0, 7):
+                col = out["payload_cols"][c].cpu().numpy()[:nc * cap][valid]
+                assert np.array_equal(col, key * 3 + c)
+    table.free()
