@@ -5,13 +5,17 @@ Per step, on every rank, the 2^30 local probe keys go through in B batches, pipe
 HIP streams (partition, comm, probe) with double-buffered send/receive slots:
   1. owner partition of batch i (ccj_partition_by_owner_fixed, HIP): destination d's keys and u32
      row ids in fixed-capacity segment d, true counts beside them;
-  2. all-to-all of counts, keys, rows with equal splits (three all_to_all_single calls on the comm
-     stream: the tuple shuffle over xGMI, the only data-path collective; no host round trip);
+  2. all-to-all of counts and keys with equal splits (all_to_all_single calls on the comm stream:
+     the tuple shuffle over xGMI, the only data-path collective; no host round trip);
   3. local probe of the received segments, GROUP batches at a time (ccj_segment_chunk_counts +
      ccj_probe_partitioned: the live rows split by home-slot window, then walked with the window
      L2-resident) while the comm stream moves the next group's batches;
   4. (verification only) all-reduce of match counts and of the order-insensitive L2 checksum.
-12 bytes cross xGMI per tuple (the source rank is implied by the receive segment).
+8 bytes cross xGMI per tuple in a timed step: the source rank is implied by the receive segment and
+the source row by the position in it — the sender's owner split keeps every position's row in its
+send slot's row buffer, so a match (receive position, payload) names its probe tuple without the
+row travelling.  verify=True also moves the rows (a third all-to-all): the checksum needs global
+rows on the receiver.
 
 Overflow.  Three things can overflow under key skew, each raising a flag in the rank's status
 word: a send segment of the owner split, a receive segment's count, and the local probe's own
@@ -63,12 +67,14 @@ def batch_count(n_probe: int, world: int, chunk: int, at_least: int = 1, subs: i
     return b
 
 
-def exchange_fixed(send_keys, send_rows, send_counts, recv_keys, recv_rows, recv_counts, group=None):
-    """All-to-all of fixed-capacity segments: equal splits, so no sizes travel through the host."""
+def exchange_fixed(send_keys, send_rows, send_counts, recv_keys, recv_rows, recv_counts, group=None, rows=True):
+    """All-to-all of fixed-capacity segments: equal splits, so no sizes travel through the host.
+    rows=False: counts and keys only (a timed step: the rows stay with their sender)."""
     assert send_keys.numel() * send_keys.element_size() <= MAX_A2A_BYTES
     dist.all_to_all_single(recv_counts, send_counts, group=group)
     dist.all_to_all_single(recv_keys, send_keys, group=group)
-    dist.all_to_all_single(recv_rows, send_rows, group=group)
+    if rows:
+        dist.all_to_all_single(recv_rows, send_rows, group=group)
 
 
 def exchange(send_keys, send_rows, send_counts, group=None):
@@ -307,14 +313,14 @@ class ShardedProbe:
             self.fparts[n](keys[lo:lo + n], lo, self.sk[s], self.sr[s], self.sc[s], self.status, self.pstream)
         self.ev_part[s].record(self.pstream)
 
-    def _exchange(self, j, timing=False):
+    def _exchange(self, j, timing=False, rows=True):
         s = j % 2
         gs, rk, rr, rc = self._recv(j)
         self.comm.wait_event(self.ev_part[s])
         if (j % self.batches) % self.group == 0:
             self.comm.wait_event(self.ev_probe[gs])  # the previous probe of receive group slot gs is done
         with self.ops.on(self.comm), self._timed(self.comm_events, self.comm, timing):
-            exchange_fixed(self.sk[s], self.sr[s], self.sc[s], rk, rr, rc)
+            exchange_fixed(self.sk[s], self.sr[s], self.sc[s], rk, rr, rc, rows=rows)
         self.ev_comm[s].record(self.comm)
 
     def reset_timing(self):
@@ -330,13 +336,14 @@ class ShardedProbe:
                 "local_probe_ms": tot(self.probe_events)}
 
     def xgmi_bytes_per_step(self) -> dict:
-        """Bytes this rank sends to the other ranks per step: the fixed-capacity segments move whole
-        (equal splits: keys 8 B + u32 rows per slot, one count per sub-segment), and the expected
-        live part of them for uniform keys (12 B per tuple that changes GPU)."""
+        """Bytes this rank sends to the other ranks per timed step: the fixed-capacity segments move
+        whole (equal splits: keys 8 B per slot, one count per sub-segment; the rows stay with their
+        sender), and the expected live part of them for uniform keys (8 B per tuple that changes
+        GPU)."""
         peers = self.world - 1
-        per_batch = peers * (self.seg_cap * 12 + self.subs * 8)
+        per_batch = peers * (self.seg_cap * 8 + self.subs * 8)
         return {"sent_to_peers": self.batches * per_batch,
-                "useful_to_peers": self.n_probe * peers / self.world * 12}
+                "useful_to_peers": self.n_probe * peers / self.world * 8}
 
     def _group_range(self, g):
         return g * self.group, min((g + 1) * self.group, self.batches) - 1
@@ -398,12 +405,12 @@ class ShardedProbe:
         self.pstream.wait_stream(cur)
         total = steps * self.batches  # run batches j: batch j % batches of step j // batches
         self._partition(keys, 0, timing)
-        self._exchange(0, timing)
+        self._exchange(0, timing, rows=verify)
         m, l2 = 0, 0
         for j in range(total):
             if j + 1 < total:
                 self._partition(keys, j + 1, timing)
-                self._exchange(j + 1, timing)
+                self._exchange(j + 1, timing, rows=verify)
             i, j0 = j % self.batches, j - j % self.batches
             if i % self.group == self.group - 1 or i == self.batches - 1:  # group i // group complete
                 g = i // self.group

@@ -294,6 +294,18 @@ def _sharded_worker(rank, world, port, cfg, q):
     for _ in range(0 if run_steps else 2):
         m, l2 = sp.step(torch.from_numpy(keys), rank * n_probe, verify=True)
         res.append((m, l2, sp.last_exact))
+    probes_verified = ops.probes
+    if not run_steps and not sp.last_exact:
+        # a timed (verify=False) step moves counts and keys only: the received rows stay as they were
+        # (poisoned here) and every local probe's result is the verify step's
+        used = [o for o in sp.outs if "count" in o]  # (one group per step: one receive-group slot in use)
+        before = [dict(count=o["count"].copy(), payload=o["payload"].copy()) for o in used]
+        for rr in sp.rr:
+            rr.fill_(-7)
+        sp.step(torch.from_numpy(keys), rank * n_probe, verify=False)
+        assert all(bool((rr == -7).all()) for rr in sp.rr), "rows crossed in a timed step"
+        for b, o in zip(before, used):
+            assert np.array_equal(b["count"], o["count"]) and np.array_equal(b["payload"], o["payload"])
     tot = torch.tensor([m, l2 - (1 << 64) if l2 >= (1 << 63) else l2], dtype=torch.int64)
     dist.all_reduce(tot)
     # the exact answer for this rank's stream (full build side, global rows)
@@ -301,7 +313,7 @@ def _sharded_worker(rank, world, port, cfg, q):
     wt = torch.tensor([want[0], want[1] - (1 << 64) if want[1] >= (1 << 63) else want[1]], dtype=torch.int64)
     dist.all_reduce(wt)
     q.put((rank, int(tot[0]), int(tot[1]) % (1 << 64), int(wt[0]), int(wt[1]) % (1 << 64),
-           [r[2] for r in res], sp.batches, sp.n_groups, ops.probes))
+           [r[2] for r in res], sp.batches, sp.n_groups, probes_verified))
     dist.destroy_process_group()
 
 
