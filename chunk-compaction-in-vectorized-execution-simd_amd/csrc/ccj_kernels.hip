@@ -2189,12 +2189,12 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk1(ProbeParams p) {
 // phase B walks those rows lane by lane (a lane takes its next continuing row as soon as one
 // finishes).  Same outputs as probe_walk1 (counts 0 / 1, or matched | slot for POS) in sm.hc,
 // then the same emits.
-template <bool POS>
+template <bool POS, int NB = 1>
 __global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
   constexpr int NW = 4;
   constexpr uint32_t kWaveRows = kMaxChunk / NW;      // rows per wave
   constexpr int kJ = (int)(kWaveRows / kWave);         // row groups (phase-A steps) per wave
-  __shared__ Walk1Shared<1, NW> sm;
+  __shared__ Walk1Shared<NB, NW> sm;
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   unsigned long long t0, t1, t2;
   uint32_t steps = 0;
@@ -2219,7 +2219,7 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
     h[j] = (uint32_t)murmurhash64((uint64_t)k[j]) & p.mask;
   }
   CCJ_STAMP(t1);
-  char *ring = sm.ring + wave * kRingSlot;
+  char *ring = sm.ring + wave * NB * kRingSlot;
   const uint32_t ring_lds = (uint32_t)__builtin_amdgcn_readfirstlane(
       (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)ring);
   const char *win = ring + (lane & 1u) * 1024 + (lane >> 1) * 32;  // this lane's window, once landed
@@ -2236,19 +2236,19 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
   // The callers keep these in uniform control flow (phase B's loop exits on a ballot, like
   // probe_walk1's; a `while (__ballot(...))` form was structurised into a nested loop whose lanes
   // left one by one — the DMAs then ran with lanes off and read wild addresses).
-  auto issue = [&](uint32_t a) {
+  auto issue = [&](uint32_t a, uint32_t slot) {
     uint32_t a0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, 0xA0, 0xF, 0xF, false);  // quad_perm 0,0,2,2
     uint32_t a1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, 0xF5, 0xF, 0xF, false);  // quad_perm 1,1,3,3
     a0 = a0 < last_start ? a0 : last_start;  // (a guard: whatever a DPP returns, the DMA stays in the table)
     a1 = a1 < last_start ? a1 : last_start;
-    dma16(p.table + a0 + half, ring_lds);
-    dma16(p.table + a1 + half, ring_lds + 1024u);
+    dma16(p.table + a0 + half, ring_lds + slot * kRingSlot);
+    dma16(p.table + a1 + half, ring_lds + slot * kRingSlot + 1024u);
   };
   // the landed window against key kk from slot cur (window start s): hits (bits from cur) and
   // whether the run ends inside the window
-  auto look = [&](int64_t kk, uint32_t cur, uint32_t s, uint32_t &hits) {
-    const longlong2 x0 = *reinterpret_cast<const longlong2 *>(win);
-    const longlong2 x1 = *reinterpret_cast<const longlong2 *>(win + 16);
+  auto look = [&](int64_t kk, uint32_t cur, uint32_t s, uint32_t &hits, uint32_t slot) {
+    const longlong2 x0 = *reinterpret_cast<const longlong2 *>(win + slot * kRingSlot);
+    const longlong2 x1 = *reinterpret_cast<const longlong2 *>(win + slot * kRingSlot + 16);
     const uint32_t e = (x0.x == -1 ? 1u : 0u) | (x0.y == -1 ? 2u : 0u) | (x1.x == -1 ? 4u : 0u) | (x1.y == -1 ? 8u : 0u);
     const uint32_t m = (x0.x == kk ? 1u : 0u) | (x0.y == kk ? 2u : 0u) | (x1.x == kk ? 4u : 0u) | (x1.y == kk ? 8u : 0u);
     const uint32_t off = cur - s;
@@ -2260,19 +2260,33 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
   auto result = [&](uint32_t cur, uint32_t hits) {
     return POS ? (hits ? (cur + (uint32_t)__builtin_ctz(hits)) | 0x80000000u : 0u) : (hits ? 1u : 0u);
   };
-  // phase A: every row's first window
+  // phase A: every row's first window (NB = 2: step j + 1's windows are fetched while step j's
+  // are checked)
   uint32_t cont = 0;
+  uint32_t sa[kJ];
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) sa[j] = start(h[j]);
+  if (NB > 1) issue(w0 < wend ? sa[0] : 0u, 0u);
 #pragma unroll
   for (int j = 0; j < kJ; ++j) {
     ++steps;
     const uint32_t i = w0 + (uint32_t)j * kWave + lane;
     const bool valid = i < wend;
-    const uint32_t s = start(h[j]);
-    issue(valid ? s : 0u);
-    wait_vmcnt<0>();
+    const uint32_t s = sa[j];
+    if (NB > 1) {
+      if (j + 1 < kJ) {
+        issue(i + kWave < wend ? sa[j + 1] : 0u, (uint32_t)(j + 1) & 1u);
+        wait_vmcnt<2>();  // step j's two DMAs have landed (step j + 1's are in flight)
+      } else {
+        wait_vmcnt<0>();
+      }
+    } else {
+      issue(valid ? s : 0u, 0u);
+      wait_vmcnt<0>();
+    }
     if (valid) {
       uint32_t hits;
-      if (look(k[j], h[j], s, hits)) {
+      if (look(k[j], h[j], s, hits, NB > 1 ? (uint32_t)j & 1u : 0u)) {
         sm.hc[i] = result(h[j], hits);
       } else {
         sm.hc[i] = (s + kWin) & p.mask;  // the next unread slot
@@ -2297,13 +2311,13 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
     };
     take();
     bst = start(bcur);
-    issue(have ? bst : 0u);
+    issue(have ? bst : 0u, 0u);
     for (bool more = true; more;) {
       ++steps;
       wait_vmcnt<0>();
       if (have) {
         uint32_t hits;
-        if (look(bkey, bcur, bst, hits)) {
+        if (look(bkey, bcur, bst, hits, 0u)) {
           sm.hc[bi] = result(bcur, hits);
           have = false;
         } else {
@@ -2316,7 +2330,7 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
         break;
       }
       bst = start(bcur);
-      issue(have ? bst : 0u);
+      issue(have ? bst : 0u, 0u);
     }
   }
   CCJ_STAMP(t2);
@@ -2657,8 +2671,13 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
       hipLaunchKernelGGL((probe_walk1<2>), g, b, 0, s, p);
     else if (ccj_tune_int("CCJ_WALK_NB", 1) == 3)
       hipLaunchKernelGGL((probe_walk1<3>), g, b, 0, s, p);
-    else if (walk2)  // distinct keys, no rounds: fixed first windows, then the rows that go on
-      hipLaunchKernelGGL((probe_walk2<false>), g, b, 0, s, p);
+    // distinct keys, no rounds: fixed first windows (step j + 1's fetched while step j's are
+    // checked: 40 KiB, 4 workgroups per CU), then the rows that go on.  Same box, C2 step:
+    // 11.34 / 11.36 ms against 11.47 / 11.39 with one window batch in flight (5 workgroups per CU)
+    else if (walk2 && ccj_tune_int("CCJ_WALK2_NB", 2) == 1)
+      hipLaunchKernelGGL((probe_walk2<false, 1>), g, b, 0, s, p);
+    else if (walk2)
+      hipLaunchKernelGGL((probe_walk2<false, 2>), g, b, 0, s, p);
     else if (ccj_tune_int("CCJ_WALK_NW", 4) == 8)  // 8 waves x 256 rows: 40 KiB, 4 workgroups = 32 waves per CU
       hipLaunchKernelGGL((probe_walk1<1, false, false, 8>), g, dim3(kWave * 8), 0, s, p);
     else
