@@ -551,3 +551,30 @@ def test_partitioned_walk_long_runs_across_windows(mode):
                 col = out["payload_cols"][c].cpu().numpy()[:nc * cap][valid]
                 assert np.array_equal(col, key * 3 + c)
     table.free()
+
+
+@pytest.mark.parametrize("chunk", [1, 7, 64, 100, 511, 512, 1000, 1024, 1536, 2047])
+def test_partitioned_distinct_keys_every_chunk_width(chunk):
+    """probe_walk2 (distinct keys) with chunks that leave waves partly or wholly empty (a wave owns
+    512 rows of a chunk): rows mode, plain mode with the row map, and positions, each with misses
+    (1/5 of the probes) and a ragged last chunk.  Exact L1 + L2; rows mode: every (row, payload)
+    pair is the row's own key."""
+    n_build, n_probe, rng = 1 << 18, 300007, (1 << 18) + (1 << 16)
+    table = ccj.Table.reference(ccj.LP, n_build, 1, ccj.LAYOUT_DEVICE)
+    assert int(table.max_dup) == 1
+    keys = ccj.gen_uniform_keys(n_probe, 71, rng)
+    want = O.count_uniform(71, 0, n_probe, rng, n_build, 1)
+    out = table.probe_partitioned(keys, chunk, rows=True)
+    torch.cuda.synchronize()
+    assert int(out["status"].item()) == 0
+    assert ccj.result_checksum(out, 0) == want
+    cnt = out["count"][:out["n_chunks"]].cpu().numpy().view(np.uint32).astype(np.int64)
+    cap = out["cap"]
+    idx = (np.arange(len(cnt))[:, None] * cap + np.arange(cap)[None, :])[np.arange(cap)[None, :] < cnt[:, None]]
+    sel = out["sel"].cpu().numpy().view(np.uint32)[idx].astype(np.int64)
+    assert np.array_equal(out["payload"].cpu().numpy()[idx], keys.cpu().numpy()[sel])
+    out = table.probe_partitioned(keys, chunk, pos=True)
+    torch.cuda.synchronize()
+    assert int(out["status"].item()) == 0
+    assert ccj.result_checksum(out, chunk, row_map=out["row_map"].to(torch.int64)) == want
+    table.free()
