@@ -280,12 +280,13 @@ int build_chain_host(const int64_t *keys, uint64_t n, ccj_table **out) {
     }
     t->d_bucket = (int64_t *)d;
   }
-  if (longest < 0xFFFFu) {  // 8-byte records {start | len << 32 | fp(first key) << 48}
+  if (longest < 0xFFu) {  // 8-byte records {start | len << 32 | fp(node 0) << 40 | fp(node 1) << 52}
     std::vector<uint64_t> rec(size);
     for (uint64_t b = 0; b < size; ++b) {
       const uint64_t lo = off[b], len = off[b + 1] - off[b];
-      const uint64_t fp = len ? ccj::bucket_fp(ccj::murmurhash64((uint64_t)chain[lo])) : 0u;
-      rec[b] = lo | len << 32 | fp << 48;
+      const uint64_t fp0 = len ? ccj::bucket_fp(ccj::murmurhash64((uint64_t)chain[lo])) : 0u;
+      const uint64_t fp1 = len > 1 ? ccj::bucket_fp(ccj::murmurhash64((uint64_t)chain[lo + 1])) : 0u;
+      rec[b] = lo | len << 32 | fp0 << 40 | fp1 << 52;
     }
     rc = upload(&d, rec.data(), rec.size() * sizeof(uint64_t), "chain bucket records (8 B)");
     if (rc) {

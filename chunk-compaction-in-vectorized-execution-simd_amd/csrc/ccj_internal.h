@@ -13,8 +13,9 @@ struct ccj_table {
   int64_t *d_table = nullptr;   // LP slots / chain keys
   uint32_t *d_off = nullptr;    // chain CSR offsets (size + 1)
   int64_t *d_bucket = nullptr;  // chain: per bucket {start | len << 32, first chain key} (16 B)
-  // chain: per bucket {start | len << 32 | fp << 48} (8 B): fp = the first key's fingerprint
-  // (bucket_fp), len < 2^16 (absent when a chain is longer: the 16-byte records serve alone)
+  // chain: per bucket {start | len << 32 | fp0 << 40 | fp1 << 52} (8 B): the 12-bit fingerprints
+  // (bucket_fp) of the first two chain keys, len < 2^8 (absent when a chain is longer: the 16-byte
+  // records serve alone)
   uint64_t *d_bucket8 = nullptr;
   uint32_t *d_row = nullptr;    // table position -> build tuple index (LP: kNoRow for empty slots)
   uint64_t positions = 0;       // allocated positions (LP slots / chain keys, padded)
@@ -42,8 +43,18 @@ __host__ __device__ __forceinline__ uint64_t murmurhash64(uint64_t x) {
   return x;
 }
 
-// Fingerprint of a chain key for the 8-byte bucket records: hash bits far above any bucket index.
-__host__ __device__ __forceinline__ uint32_t bucket_fp(uint64_t h) { return (uint32_t)(h >> 48); }
+// Fingerprint of a chain key for the 8-byte bucket records: 12 hash bits far above any bucket index.
+__host__ __device__ __forceinline__ uint32_t bucket_fp(uint64_t h) { return (uint32_t)(h >> 52); }
+// 8-byte bucket record {start | len << 32 | fp(node 0) << 40 | fp(node 1) << 52} (len < 256): the
+// first chain node that can hold a key of fingerprint kfp — nodes 0 and 1 are skipped when their
+// fingerprints differ — or start + len when none can (the key is not in the chain).
+__host__ __device__ __forceinline__ uint32_t rec8_first(uint64_t r, uint32_t kfp) {
+  const uint32_t st = (uint32_t)r, len = (uint32_t)(r >> 32) & 0xFFu;
+  const bool m0 = ((uint32_t)(r >> 40) & 0xFFFu) == kfp;
+  const bool m1 = len >= 2u && ((uint32_t)(r >> 52) & 0xFFFu) == kfp;
+  const uint32_t c = m0 ? st : m1 ? st + 1u : st + 2u;
+  return c < st + len ? c : st + len;
+}
 
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
@@ -56,9 +67,10 @@ struct ProbeParams {
   // chain only, optional: bucket records {start | len << 32, first key} — one 16-byte load gives
   // the chain's range and its round-0 candidate (most chains at load 1/2 have one key)
   const longlong2 *bucket;
-  // chain only, optional: 8-byte bucket records {start | len << 32 | fp << 48} (the partitioned
-  // walk): a key whose fingerprint differs from fp is not the chain's first key, so most misses end
-  // at the record, and a partition's records take half the L2
+  // chain only, optional: 8-byte bucket records {start | len << 32 | fp0 << 40 | fp1 << 52} (the
+  // partitioned walks): a key whose fingerprint differs from fp0 / fp1 is not the chain's first /
+  // second key, so misses on chains of up to two keys end at the record, and a partition's records
+  // take half the L2
   const uint64_t *bucket8;
   uint32_t mask;  // size - 1 (size <= 2^32)
   const int64_t *keys;

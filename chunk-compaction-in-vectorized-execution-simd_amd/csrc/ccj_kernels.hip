@@ -1259,17 +1259,16 @@ __global__ __launch_bounds__(kFlatThreads) void probe_chain_win(ProbeParams p) {
           fresh &= ~(1u << k);
           // 8-byte records come in aligned pairs: this bucket's is the half cur & 1
           const uint64_t r = rec8 ? (uint64_t)((cur[k] & 1u) ? v[k].y : v[k].x) : (uint64_t)v[k].x;
-          const uint32_t st = (uint32_t)r, len = rec8 ? (uint32_t)(r >> 32) & 0xFFFFu : (uint32_t)(r >> 32);
+          const uint32_t st = (uint32_t)r, len = rec8 ? (uint32_t)(r >> 32) & 0xFFu : (uint32_t)(r >> 32);
           lane_rounds = len > lane_rounds ? len : lane_rounds;
           if (len == 0) {
             done |= 1u << k;  // empty bucket: not in the active set (chaining_ht.cpp:52-55)
           } else if (rec8) {
-            // a key whose fingerprint differs is not the first chain key: round 0 needs no read;
-            // an equal fingerprint reads the first key with the rest of the chain
-            const bool skip = (uint32_t)(r >> 48) != kfp[k];
-            cur[k] = skip ? st + 1 : st;
+            // the first two chain keys are skipped without a read when their fingerprints differ;
+            // the rest of the chain is read from the first node that can match
+            cur[k] = rec8_first(r, kfp[k]);
             lim[k] = st + len;
-            if (skip && len == 1) done |= 1u << k;
+            if (cur[k] >= lim[k]) done |= 1u << k;
           } else {
             hits[k] = v[k].y == key[k] ? 1u : 0u;  // round 0 from the record's first key
             cur[k] = st + 1;
@@ -1422,15 +1421,14 @@ __global__ __launch_bounds__(kFlatThreads) void chain_words(ProbeParams p) {
         if ((fresh >> k) & 1u) {
           fresh &= ~(1u << k);
           const uint64_t r = rec8 ? (uint64_t)((cur[k] & 1u) ? v[k].y : v[k].x) : (uint64_t)v[k].x;
-          const uint32_t st = (uint32_t)r, len = rec8 ? (uint32_t)(r >> 32) & 0xFFFFu : (uint32_t)(r >> 32);
+          const uint32_t st = (uint32_t)r, len = rec8 ? (uint32_t)(r >> 32) & 0xFFu : (uint32_t)(r >> 32);
           st0[k] = st;
           lim[k] = st + len;
           if (len == 0) {
             done |= 1u << k;  // empty bucket: no rounds
-          } else if (rec8) {
-            const bool skip = (uint32_t)(r >> 48) != kfp[k];  // not the first node: round 0 without a read
-            cur[k] = skip ? st + 1 : st;
-            if (skip && len == 1) done |= 1u << k;
+          } else if (rec8) {  // nodes 0 / 1 whose fingerprints differ: their rounds without a read
+            cur[k] = rec8_first(r, kfp[k]);
+            if (cur[k] >= lim[k]) done |= 1u << k;
           } else {
             mm[k] |= v[k].y == key[k] ? 1u : 0u;  // round 0 from the record's first key
             cur[k] = st + 1;
