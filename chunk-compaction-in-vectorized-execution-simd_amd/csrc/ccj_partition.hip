@@ -733,8 +733,9 @@ uint64_t slot_seg_cap(uint64_t n, const SlotPlan &pl, uint32_t chunk) {
 // keys per thread per tile: 11 (11264-key tiles, 149 KB of LDS with <= 512 partitions); 1024
 // partitions leave room for 10 (the tuning build sweeps 10 / 11 below that)
 static int split_per(uint32_t parts) {
-  const int per = ccj_tune_int("CCJ_SPLIT_PER", kSplitPer);
-  return parts > kSplitParts / 2 && per > 10 ? 10 : per;
+  // (only 10 and 11 are instantiated below: any other value must not size the tiles)
+  const int per = ccj_tune_int("CCJ_SPLIT_PER", kSplitPer) == 10 ? 10 : kSplitPer;
+  return parts > kSplitParts / 2 ? 10 : per;
 }
 
 // With run records (the ordered probe) the pipelined split holds 10 keys per thread: at 11 its
