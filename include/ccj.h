@@ -201,7 +201,9 @@ int ccj_probe_visits(const ccj_table *table, const int64_t *d_keys, const uint32
  * live position.  Same matches, payloads and per-row multiplicities as ccj_probe (L1 + L2);
  * within a chunk the order is unspecified, so out_round_counts is not produced (must be NULL).
  * out_pos (table position of every match) and payload columns (C5: gathered after the walk) are
- * produced as by ccj_probe, for tables of >= 16 slots. */
+ * produced as by ccj_probe, for tables of >= 16 slots.  For a table of distinct keys (max_dup 1)
+ * without out_rounds the walk ends a row at its match (the rest of its run cannot hold the key);
+ * with out_rounds every row is walked to the end of its run, as the reference's Next calls do. */
 #define CCJ_PART_EXACT 1u
 /* flags & CCJ_PART_ROWS: out_sel receives the ORIGINAL row of every match (u32, row of args->keys)
  * instead of its position inside the chunk, and out_row_map may be NULL.  LP tables of >= 16
