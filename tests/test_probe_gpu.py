@@ -578,3 +578,39 @@ def test_partitioned_distinct_keys_every_chunk_width(chunk):
     assert int(out["status"].item()) == 0
     assert ccj.result_checksum(out, chunk, row_map=out["row_map"].to(torch.int64)) == want
     table.free()
+
+
+def test_partitioned_distinct_keys_rounds_walk_whole_runs():
+    """With out_rounds asked for, the partitioned walk of a distinct-key table still walks every row
+    to the end of its run (no early end at the match): each chunk's rounds equal the longest run,
+    from the row's home slot to the first empty one, over the chunk's rows (the reference's Next
+    calls for the chunk).  Every probe hits, so a chunk's count is its number of live rows."""
+    n_build, n_probe = 1 << 18, 1 << 20
+    table = ccj.Table.reference(ccj.LP, n_build, 1, ccj.LAYOUT_DEVICE)
+    assert int(table.max_dup) == 1
+    keys = ccj.gen_uniform_keys(n_probe, 91, n_build)
+    out = table.probe_partitioned(keys, 2048, rounds=True)
+    torch.cuda.synchronize()
+    assert int(out["status"].item()) == 0
+    slots = table_slots(table)[:table.size]
+    occ = slots != -1
+    # run length from every slot: occupied slots from it up to the first empty one (with wrap)
+    size = len(slots)
+    runlen = np.zeros(size, np.int64)
+    first_empty = int(np.nonzero(~occ)[0][0])
+    run = 0
+    for s in range(first_empty - 1 + size, first_empty - 1, -1):  # backwards, starting at an empty slot
+        i = s % size
+        run = run + 1 if occ[i] else 0
+        runlen[i] = run
+    k = keys.cpu().numpy()
+    home = (_np_murmur(k.astype(np.uint64)) & np.uint64(size - 1)).astype(np.int64)
+    nc = out["n_chunks"]
+    cnt = out["count"][:nc].cpu().numpy().view(np.uint32).astype(np.int64)
+    rounds = out["rounds"][:nc].cpu().numpy().view(np.uint32).astype(np.int64)
+    rm = out["row_map"].cpu().numpy().view(np.uint32).astype(np.int64)
+    assert cnt.sum() == n_probe
+    for c in np.nonzero(cnt)[0]:
+        rows = rm[c * 2048:c * 2048 + cnt[c]]
+        assert rounds[c] == runlen[home[rows]].max(), c
+    table.free()
