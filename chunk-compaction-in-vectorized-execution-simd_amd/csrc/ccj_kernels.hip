@@ -2649,7 +2649,8 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
   if (p.out_pos && p.rows_in_sel) {
     // C5 under CCJ_PART_ROWS (distinct keys, tables of <= 2^31 slots): the split wrote rows and keys,
     // the walk leaves each row's matched slot at its output slot
-    if (walk2) hipLaunchKernelGGL((probe_walk2<true>), g, b, 0, s, p);
+    if (walk2 && ccj_tune_int("CCJ_WALK2_POS_NB", 1) == 2) hipLaunchKernelGGL((probe_walk2<true, 2>), g, b, 0, s, p);
+    else if (walk2) hipLaunchKernelGGL((probe_walk2<true>), g, b, 0, s, p);
     else hipLaunchKernelGGL((probe_walk1<1, false, true>), g, b, 0, s, p);
   } else if (p.out_pos) {
     hipLaunchKernelGGL((probe_win<3>), g, b, 0, s, p);  // C5: match positions too
