@@ -681,6 +681,7 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   // CCJ_PF_MULT = slices of lines per chunk
   if (!exact && L.pl.lo_bits && t->info.kind == CCJ_TABLE_LP && L.pl.window_bits >= 4) {
     p.kp_dist = (uint32_t)ccj_tune_int("CCJ_KEYPF", 64);
+    p.key_aux = (uint32_t)ccj_tune_int("CCJ_KEY_AUX", 0);
     const int pf8 = ccj_tune_int("CCJ_PREFETCH", 0);
     if (pf8 > 0) {
       const uint64_t K = 8 * (L.seg_cap / a->chunk);

@@ -135,6 +135,7 @@ struct ProbeParams {
   // probe_walk1: the table's keys are distinct (max_dup 1) and no rounds are asked for, so a row
   // stops at its match instead of walking to the end of its run (same matches and multiplicities)
   uint32_t first_match;
+  uint32_t key_aux;  // tuning build (CCJ_KEY_AUX): probe_walk2's key loads as buffer loads, policy key_aux - 1
 };
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 constexpr uint32_t kEmitWave = 0xFFFFFFFFu;

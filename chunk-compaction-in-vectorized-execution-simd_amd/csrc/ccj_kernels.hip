@@ -2187,6 +2187,22 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk1(ProbeParams p) {
 // phase B walks those rows lane by lane (a lane takes its next continuing row as soon as one
 // finishes).  Same outputs as probe_walk1 (counts 0 / 1, or matched | slot for POS) in sm.hc,
 // then the same emits.
+// The stage's key loads as buffer loads of cache policy AUX (tuning build: CCJ_KEY_AUX A/B of how
+// the streamed key lines share the L2 with the table window).
+template <int AUX, int KJ>
+__device__ __forceinline__ void stage_keys_aux(const int64_t *keys, uint32_t phys, uint32_t w0, uint32_t wend,
+                                               uint32_t lane, int64_t (&k)[KJ]) {
+  // the descriptor spans the chunk's live rows only: a load past them returns 0 (no access)
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<int64_t *>(keys), (short)0, (int)(phys * 8), 0x00020000);
+#pragma unroll
+  for (int j = 0; j < KJ; ++j) {
+    const uint32_t i = w0 + (uint32_t)j * kWave + lane;
+    k[j] = (int64_t)__builtin_amdgcn_raw_buffer_load_b64(rs, (int)(i * 8), 0, AUX);
+  }
+#pragma unroll
+  for (int j = 0; j < KJ; ++j)
+    if (w0 + (uint32_t)j * kWave + lane >= wend) k[j] = 0;
+}
 template <bool POS, int NB = 1>
 __global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
   constexpr int NW = 4;
@@ -2206,10 +2222,23 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
   // LDS for phase B and the emit's compaction
   int64_t k[kJ];
   uint32_t h[kJ];
+  if (p.key_aux == 0u) {
 #pragma unroll
-  for (int j = 0; j < kJ; ++j) {
-    const uint32_t i = w0 + (uint32_t)j * kWave + lane;
-    k[j] = i < wend ? __builtin_nontemporal_load(p.keys + base + i) : 0;
+    for (int j = 0; j < kJ; ++j) {
+      const uint32_t i = w0 + (uint32_t)j * kWave + lane;
+      k[j] = i < wend ? __builtin_nontemporal_load(p.keys + base + i) : 0;
+    }
+  } else {  // (tuning build only: p.key_aux = 1 + the buffer loads' cache-policy bits)
+    switch (p.key_aux - 1u) {
+      case 1: stage_keys_aux<1>(p.keys + base, phys, w0, wend, lane, k); break;
+      case 2: stage_keys_aux<2>(p.keys + base, phys, w0, wend, lane, k); break;
+      case 3: stage_keys_aux<3>(p.keys + base, phys, w0, wend, lane, k); break;
+      case 16: stage_keys_aux<16>(p.keys + base, phys, w0, wend, lane, k); break;
+      case 17: stage_keys_aux<17>(p.keys + base, phys, w0, wend, lane, k); break;
+      case 18: stage_keys_aux<18>(p.keys + base, phys, w0, wend, lane, k); break;
+      case 19: stage_keys_aux<19>(p.keys + base, phys, w0, wend, lane, k); break;
+      default: stage_keys_aux<0>(p.keys + base, phys, w0, wend, lane, k); break;
+    }
   }
 #pragma unroll
   for (int j = 0; j < kJ; ++j) {
