@@ -183,9 +183,13 @@ class DeviceOps:
         return part, out
 
     def probe_group(self, keys, counts, part, out, chunk, stream):
-        # share: the local split leaves CUs to RCCL and the next owner splits (ccj.h CCJ_PART_SHARE)
+        # share: the local split leaves CUs to RCCL and the next owner splits (ccj.h CCJ_PART_SHARE);
+        # rows (CCJ_PART_ROWS, distinct build keys): the split writes every position's receive slot
+        # and key into the outputs, so the walk writes only the chunks with a miss
+        rows = int(self.table.max_dup) <= 1 and out["cap"] == chunk
+        part["rows_mode"] = rows
         self.table.probe_partitioned(keys, chunk, counts=counts, out=out, part=part, stream=stream, retry=False,
-                                     share=True)
+                                     share=True, rows=rows)
 
     def group_rows(self, part, recv_rows, n_probe, seg_cap, slots, stream):
         """Global probe row of every position of a group's partitioned layout (gap positions hold
@@ -194,11 +198,14 @@ class DeviceOps:
         with torch.cuda.stream(stream):
             q = torch.arange(n, device=recv_rows.device) % slots
             recv = (q // seg_cap) * n_probe + recv_rows.to(torch.int64)
+            if part.get("rows_mode"):  # out_sel holds receive slots: the map is by slot
+                return recv
             rm = part["row_map"].to(torch.int64).clamp_(0, n - 1)
             return recv[rm]
 
     def checksum(self, out, chunk, row_map, stream):
-        return self.ccj.result_checksum(out, chunk, row_map=row_map, stream=stream)
+        # rows mode: sel is the receive slot itself, so the map is read at sel (chunk 0)
+        return self.ccj.result_checksum(out, 0 if out.get("rows_in_sel") else chunk, row_map=row_map, stream=stream)
 
     # exact-size protocol
     def owner_partitioner(self, n, world):
