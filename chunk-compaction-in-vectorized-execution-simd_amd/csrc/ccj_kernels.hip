@@ -2075,8 +2075,10 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk1(ProbeParams p) {
       a = s;
     }
     if (CCJ_ABLATED(p.ablate, 0x200u)) a &= 0x1FFFu;  // (timing only: windows from the first 64 KiB)
-    const uint32_t a0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, 0xA0, 0xF, 0xF, false);  // quad_perm 0,0,2,2
-    const uint32_t a1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, 0xF5, 0xF, 0xF, false);  // quad_perm 1,1,3,3
+    uint32_t a0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, 0xA0, 0xF, 0xF, false);  // quad_perm 0,0,2,2
+    uint32_t a1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, 0xF5, 0xF, 0xF, false);  // quad_perm 1,1,3,3
+    a0 = a0 < last_start ? a0 : last_start;  // (a guard, as in probe_walk2: the DMA stays in the table)
+    a1 = a1 < last_start ? a1 : last_start;
     const uint32_t slot = ring_lds + (uint32_t)b * kRingSlot;
     dma16(p.table + a0 + half, slot);
     dma16(p.table + a1 + half, slot + 1024u);
