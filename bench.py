@@ -251,6 +251,33 @@ def cpu_baseline(args):
     }
 
 
+PHASE_KERNELS = {  # which kernels sit between the phase boundaries of each path (ccj.h ccj_set_phase_events)
+    "partitioned": ("slot_split_pipe (hash, home partition, keys + rows to their positions)",
+                    "probe_walk2 (match + advance, fused; compacts the chunks with misses)",
+                    "— (the split wrote the payload: it IS the probe key at its position)"),
+    "ordered": ("slot_split_pipe with run records", "probe_walk1<1,MM> / chain_words (round words)",
+                "unsplit_words + emit_ordered (the reference's per-Next order)"),
+    "chunk": ("probe_chunks (fused: hash, match, gather, advance in one kernel)", "—", "—"),
+    "rank": ("slot_split_pipe", "probe_rank + rank_finish", "—"),
+}
+
+
+def phase_report(pev, path, c5=False):
+    """Mean per-step phase times in the reference's 4-phase schema (CycleProfiler, profiler.h:262-290:
+    "Hash & Find Bucket", "Match Tuples", "Gather Tuples", "Advance Pointers") from the HIP events the
+    library recorded at its kernel boundaries.  The walks fuse Match and Advance (one kernel), so they
+    are reported as one phase."""
+    t = [p.ms() for p in pev]
+    mean = [sum(x[i] for x in t) / len(t) for i in range(3)]
+    k = PHASE_KERNELS.get(path, ("?", "?", "?"))
+    gather_k = "gather_payload_quad (8 payload columns)" if c5 else k[2]
+    return {"schema": "reference CycleProfiler phases (profiler.h:262-290)",
+            "hash_find_bucket_ms": mean[0], "match_tuples_and_advance_pointers_ms": mean[1],
+            "gather_tuples_ms": mean[2],
+            "kernels": {"hash_find_bucket": k[0], "match_tuples_and_advance_pointers": k[1],
+                        "gather_tuples": gather_k}}
+
+
 def bench_c3(args, dev, stream):
     """C3: chaining probe + NaiveCompactor under Zipf-skewed keys with ~10 % matches."""
     import subprocess
@@ -274,10 +301,12 @@ def bench_c3(args, dev, stream):
     log(f"[setup c3] {table.size} buckets, max chain {table.max_rounds}: {time.perf_counter() - t0:.1f} s")
     comp = None
 
-    def step(ev=None):
+    def step(ev=None, pe=None):
         nonlocal comp
         if ev:
             ev[0].record(stream)
+        if pe:
+            pe.arm()
         if part_mode:
             # one-pass split: the Zipf-hot keys' runs that overflow their segments go to the shared
             # overflow area; status is checked after the timed region (no host sync inside it)
@@ -291,6 +320,8 @@ def bench_c3(args, dev, stream):
             table.probe(keys, chunk, out=out, stream=stream)
         if ev:
             ev[1].record(stream)
+        if pe:
+            ccj.PhaseEvents.disarm()
         comp = ccj.compact(out, chunk, cols=[pkeys if part_mode else keys], rows=True, stream=stream)
         if ev:
             ev[2].record(stream)
@@ -300,14 +331,21 @@ def bench_c3(args, dev, stream):
     stream.synchronize()
     torch.cuda.synchronize()
     evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
+    pev = [ccj.PhaseEvents() for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(evs[i])
+        step(evs[i], pev[i])
     stream.synchronize()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     probe_ms = sum(a.elapsed_time(b) for a, b, _ in evs) / args.steps
     comp_ms = sum(b.elapsed_time(c) for _, b, c in evs) / args.steps
+    phases = phase_report(pev, args.path)
+    phases["compaction_ms"] = comp_ms
+    phases["kernels"]["compaction"] = "ccj_compact (NaiveCompactor closed form: scans + copy_rows_flat)"
+    if part_mode:
+        phases["kernels"]["match_tuples_and_advance_pointers"] = "probe_chain_win<3> (bucket records, 2-key windows)"
+        phases["kernels"]["gather_tuples"] = "— (the walk writes each match's payload)"
     if part_mode or args.path == "ordered":
         if int(out["status"].item()) & ccj.FLAG_PART_OVERFLOW:
             raise SystemExit("bench c3: the split's overflow area overflowed")
@@ -331,7 +369,7 @@ def bench_c3(args, dev, stream):
         from oracle import oracle as O
         comp_l2 = O.l2_sum(c_rows.cpu().numpy().astype(np.uint64), c_pay.cpu().numpy())
     del c_rows, c_pay, c_key, idx, valid
-    examined, _ = table.probe_cost(keys, stream=stream)
+    examined, _, walked, windows = table.probe_cost_walk(keys, stream=stream)
     parity = {"status_flags": int(out["status"].item()) | int(comp["status"].item()), "matches": matches,
               "l2": hex(l2), "compacted_rows": n_comp, "compacted_l2": None if comp_l2 is None else hex(comp_l2),
               "compaction_keeps_all": n_comp == matches and key_ok and comp_l2 in (None, l2)}
@@ -366,6 +404,12 @@ def bench_c3(args, dev, stream):
         except (OSError, ValueError):
             pass
     achieved = alg * n_probe / (probe_ms * 1e-3) / 1e9
+    # the chain keys a walk that stops at the first match examines (distinct build keys: the
+    # partitioned walk); the bucket record counts as the offsets' 8 B
+    fm = part_mode and int(table.max_dup) <= 1
+    n_walk = (walked if fm else examined) / n_probe
+    alg_walked = 8 + 8 + 8 * n_walk + 12 * m_bar
+    achieved_walked = alg_walked * n_probe / (probe_ms * 1e-3) / 1e9
     line = {
         "metric": METRIC, "value": n_probe / (wall / args.steps), "unit": "probe tuples/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall * 1e3 / args.steps,
@@ -381,7 +425,11 @@ def bench_c3(args, dev, stream):
                                      "emit_ordered<CHAIN>)" if args.path == "ordered"
                                 else "probe_chunks<CHAIN,2>"),
                      "kernel_ms": probe_ms, "alg_bytes_per_tuple": alg, "chain_keys_per_tuple": n_bar,
-                     "m_bar": m_bar},
+                     "m_bar": m_bar, "frac_walked": achieved_walked / HBM_PEAK_GBS,
+                     "alg_bytes_walked_per_tuple": alg_walked, "chain_keys_walked_per_tuple": n_walk,
+                     "walk": "first match" if fm else "whole chain",
+                     "chain_windows_per_tuple": windows / n_probe},
+        "phases": phases,
         "compaction_ms": comp_ms, "path": args.path,
         "cpu_baseline": cpu,
         "parity": parity,
@@ -621,9 +669,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    pev = [ccj.PhaseEvents() for _ in range(args.steps)]  # the reference's 4-phase schema, per step
     t0 = time.perf_counter()
     for i in range(args.steps):
         evs[i][0].record(stream)
+        pev[i].arm()
         step()
         evs[i][1].record(stream)
     stream.synchronize()
@@ -631,6 +681,8 @@ def main():
     if dist:
         dist.barrier()
     wall = time.perf_counter() - t0
+    ccj.PhaseEvents.disarm()
+    phases = phase_report(pev, args.path, c5)
     if dist:
         t = torch.tensor([wall], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -699,7 +751,7 @@ def main():
         l3_same = same
         if "ordered" in other_runs:
             other_runs["ordered"][1]["equals_chunk_path_l3"] = same
-    examined, cost_matches = table.probe_cost(keys, stream=stream)
+    examined, cost_matches, walked, windows = table.probe_cost_walk(keys, stream=stream)
     parity = {"status_flags": status, "matches": matches, "l2": hex(l2)}
     if args.path == "ordered" and l3_same is not None:
         parity["equals_chunk_path_l3"] = l3_same
@@ -727,6 +779,14 @@ def main():
     alg_bytes_per_tuple = 8 + 8 * s_bar + m_bar * (12 + 16 * P)  # +16 B per payload column
     alg_bytes = alg_bytes_per_tuple * n_probe
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    # what the headline path's walk actually examines: with distinct build keys a row ends at its
+    # first match (ccj.h ccj_probe_partitioned), so its slot words are s_walk, not the reference's
+    # s_bar; the 32-byte windows it reads are the transaction-level view of the same walk
+    first_match = args.path == "partitioned" and int(table.max_dup) <= 1
+    s_walk = (walked if first_match else examined) / n_probe
+    walked_bytes_per_tuple = 8 + 8 * s_walk + m_bar * (12 + 16 * P)
+    window_bytes_per_tuple = 8 + 32 * windows / n_probe + m_bar * (12 + 16 * P)
+    achieved_walked = walked_bytes_per_tuple * n_probe / (kern_ms * 1e-3) / 1e9
     traffic = None
     kernels_ms = None
     # DRAM bytes per step of THIS path's kernels, from tools/profile.sh + tools/prof_summary.py
@@ -771,8 +831,17 @@ def main():
                                     "probe_chunks<LP,2> + gather_payload_quad" if c5 else PATH_KERNELS[args.path]),
                          "kernel_ms": kern_ms, "rocprof_kernels_ms": kernels_ms,
                          "alg_bytes_per_tuple": alg_bytes_per_tuple, "s_bar": s_bar, "m_bar": m_bar,
+                         # the same step on the bytes its walk reads: slot words through the first
+                         # match (distinct keys), not through the run's end
+                         "frac_walked": achieved_walked / HBM_PEAK_GBS, "achieved_walked": achieved_walked,
+                         "alg_bytes_walked_per_tuple": walked_bytes_per_tuple, "s_walk": s_walk,
+                         "walk": "first match" if first_match else "whole run",
+                         "window_bytes_per_tuple": window_bytes_per_tuple,
+                         "windows_per_tuple": windows / n_probe,
                          # the same achieved rate against the copy rate measured on this box
-                         "frac_of_copy_ceiling": achieved / ceiling["GBps"] if ceiling else None},
+                         "frac_of_copy_ceiling": achieved / ceiling["GBps"] if ceiling else None,
+                         "frac_walked_of_copy_ceiling": achieved_walked / ceiling["GBps"] if ceiling else None},
+            "phases": phases,
             "hbm_copy_ceiling": ceiling,
             "cpu_baseline": cpu,
             "parity": parity,
@@ -850,6 +919,25 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
     # timed steps redone with the exact-size protocol (every rank takes the same branch: the status
     # word is all-reduced before it, so this count is the same on all ranks)
     exact_fallback = sp.exact_steps - exact_before
+    # the timed steps moved keys only: the groups whose results are still held get their probe rows
+    # from the senders' kept per-batch row buffers (untimed all-to-all), checked against the exact
+    # answer over those batches of every rank (a key-only step must stay traceable)
+    resolved = None
+    if not exact_fallback:
+        rm_, rl_, covered = sp.resolve_kept_groups()
+        t = torch.tensor([rm_, rl_ - (1 << 64) if rl_ >= (1 << 63) else rl_], dtype=torch.int64, device=tdev)
+        dist.all_reduce(t)
+        resolved = {"batches": covered, "matches": int(t[0].item()), "l2": hex(int(t[1].item()) % (1 << 64))}
+        if not args.no_verify and rank == 0:
+            from oracle import oracle as O
+            wm_, wl_ = 0, 0
+            for src in range(world):
+                for i in covered:
+                    lo, n = sp._batch(i)
+                    a, b = O.count_uniform(SEED, src * n_probe + lo, src * n_probe + lo + n, n_build_total,
+                                           n_build_total, 1, threads=args.cpu_threads)
+                    wm_, wl_ = wm_ + a, (wl_ + b) % (1 << 64)
+            resolved.update(l1_ok=wm_ == resolved["matches"], l2_ok=hex(wl_) == resolved["l2"])
     # verification (untimed): global L1 / L2 against the exact membership answer
     m, l2 = sp.step(keys, rank * n_probe, verify=True)
     examined, received = 0, 0
@@ -863,7 +951,8 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
     m_all, l2_all = int(tot[0].item()), int(tot[1].item()) % (1 << 64)
     s_bar = int(tot[2].item()) / max(int(tot[3].item()), 1)
     xgmi = sp.xgmi_bytes_per_step()
-    parity = {"matches": m_all, "l2": hex(l2_all), "exact_size_fallback_steps": exact_fallback}
+    parity = {"matches": m_all, "l2": hex(l2_all), "exact_size_fallback_steps": exact_fallback,
+              "timed_step_rows_resolved": resolved}
     if not args.no_verify and rank == 0:
         from oracle import oracle as O
         want_m, want_l2 = O.count_uniform(SEED, 0, world * n_probe, n_build_total, n_build_total, 1,
@@ -889,6 +978,9 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
             # per step, slowest rank; the three streams overlap, so these are busy times, not a sum
             "partition_ms": phase["partition_ms"], "exchange_ms": phase["exchange_ms"],
             "local_probe_ms": probe_ms,
+            "exchange": ("key-only all-to-all in timed steps (8 B per tuple + segment counts); each sender keeps its "
+                         "rows per batch, so the held groups' matches are resolved to global rows after timing "
+                         "(parity.timed_step_rows_resolved)"),
             "xgmi_bytes_per_step": xgmi["sent_to_peers"], "xgmi_useful_bytes_per_step": xgmi["useful_to_peers"],
             "xgmi_GBps_per_rank": xgmi["sent_to_peers"] / (wall / args.steps) / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

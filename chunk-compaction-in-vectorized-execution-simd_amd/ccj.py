@@ -42,6 +42,12 @@ class TableInfo(C.Structure):
                 ("d_table", C.c_void_p), ("d_bucket_off", C.c_void_p)]
 
 
+class TableArrays(C.Structure):
+    _fields_ = [("d_table", C.c_void_p), ("positions", C.c_uint64), ("d_row", C.c_void_p),
+                ("d_bucket_off", C.c_void_p), ("d_bucket16", C.c_void_p), ("d_bucket8", C.c_void_p),
+                ("n_bucket8", C.c_uint64)]
+
+
 class ProbeArgs(C.Structure):
     _fields_ = [("keys", C.c_void_p), ("sel", C.c_void_p), ("counts", C.c_void_p), ("n_rows", C.c_uint64),
                 ("chunk", C.c_uint32), ("max_rounds", C.c_uint32), ("cap", C.c_uint64),
@@ -73,7 +79,8 @@ EXPORTS = ["ccj_last_error", "ccj_abi_version", "ccj_device_init", "ccj_table_bu
            "ccj_segment_chunk_counts", "ccj_pipeline_set_thresholds", "ccj_gen_c3_keys",
            "ccj_partition_grouped_workspace_size", "ccj_partition_by_owner_grouped", "ccj_partition_grouped_sub_cap",
            "ccj_probe_ordered_workspace_size", "ccj_probe_ordered", "ccj_probe_visits",
-           "ccj_stream_create_cu_masked", "ccj_stream_destroy", "ccj_device_cus", "ccj_copy_device"]
+           "ccj_stream_create_cu_masked", "ccj_stream_destroy", "ccj_device_cus", "ccj_copy_device",
+           "ccj_table_get_arrays", "ccj_probe_cost_walk", "ccj_set_phase_events"]
 
 MAX_JOINS = 8
 COMPACT_NONE, COMPACT_FULL = 0, 1
@@ -106,6 +113,7 @@ def lib():
         L.ccj_table_build_from_host.argtypes = [i32, vp, u64, C.POINTER(vp)]
         L.ccj_table_build_on_device.argtypes = [i32, vp, u64, vp, C.POINTER(vp)]
         L.ccj_table_get_info.argtypes = [vp, C.POINTER(TableInfo)]
+        L.ccj_table_get_arrays.argtypes = [vp, C.POINTER(TableArrays)]
         L.ccj_table_free.argtypes = [vp]
         L.ccj_table_set_payload.argtypes = [vp, vp, C.c_uint32, vp]
         L.ccj_table_build_rank_index.argtypes = [vp, vp]
@@ -122,6 +130,8 @@ def lib():
         L.ccj_gen_reference_keys.argtypes = [vp, u64, u64, u64, u64, vp]
         L.ccj_gen_c3_keys.argtypes = [vp, u64, u64, u64, u64, u64, C.c_uint32, vp]
         L.ccj_probe_cost.argtypes = [vp, vp, u64, vp, vp]
+        L.ccj_probe_cost_walk.argtypes = [vp, vp, u64, vp, vp]
+        L.ccj_set_phase_events.argtypes = [C.POINTER(vp), C.c_uint32]
         L.ccj_probe_visits.argtypes = [vp, vp, vp, C.c_uint32, C.c_uint32, vp, vp, vp]
         L.ccj_compact_workspace_size.restype = C.c_size_t
         L.ccj_compact_workspace_size.argtypes = [u64, u64, C.c_uint32, C.c_uint32, C.c_uint32]
@@ -172,6 +182,46 @@ def _stream(stream):
 
 def _ptr(t):
     return None if t is None else C.c_void_p(t.data_ptr())
+
+
+class PhaseEvents:
+    """One probe call's phase boundaries in the reference's 4-phase schema (CycleProfiler,
+    profiler.h:262-290), timed by HIP events the library records at its kernel boundaries
+    (ccj_set_phase_events): [0] start, [1] hash & find bucket done, [2] match + advance done,
+    [3] gather done.  arm() before the call (this thread's next probe calls record them), ms()
+    after the stream has finished: (hash_find, match_advance, gather) in ms."""
+
+    def __init__(self):
+        h = _hip()
+        self.ev = [C.c_void_p() for _ in range(4)]
+        for e in self.ev:
+            if h.hipEventCreate(C.byref(e)) != 0:
+                raise CCJError("hipEventCreate failed")
+
+    def arm(self):
+        arr = (C.c_void_p * 4)(*[e.value for e in self.ev])
+        check(lib().ccj_set_phase_events(arr, 4), "ccj_set_phase_events")
+
+    @staticmethod
+    def disarm():
+        check(lib().ccj_set_phase_events(None, 0), "ccj_set_phase_events")
+
+    def ms(self):
+        h = _hip()
+        out = []
+        for a, b in zip(self.ev[:-1], self.ev[1:]):
+            t = C.c_float(0.0)
+            if h.hipEventElapsedTime(C.byref(t), a, b) != 0:
+                raise CCJError("hipEventElapsedTime failed (phase events not recorded?)")
+            out.append(float(t.value))
+        return tuple(out)
+
+    def __del__(self):
+        try:
+            for e in self.ev:
+                _hip().hipEventDestroy(e)
+        except Exception:
+            pass
 
 
 def device_init(device: int = 0):
@@ -268,6 +318,26 @@ class Table:
         except Exception:
             pass
 
+    def arrays(self):
+        """The table's device arrays copied to the host (numpy; ccj_table_get_arrays): table
+        (slots / chain keys), row, and for chaining off, bucket16 (int64 pairs), bucket8 (or None)."""
+        import numpy as np
+        import torch
+        a = TableArrays()
+        check(lib().ccj_table_get_arrays(self._h, C.byref(a)), "ccj_table_get_arrays")
+        torch.cuda.synchronize()
+
+        def get(ptr, n, dt):
+            n_i64 = (n * np.dtype(dt).itemsize + 7) // 8
+            return _d2h_i64(ptr, n_i64).view(np.uint8)[:n * np.dtype(dt).itemsize].view(dt)
+
+        out = dict(table=get(a.d_table, a.positions, np.int64), row=get(a.d_row, a.positions, np.uint32))
+        if self.kind == CHAIN:
+            out["off"] = get(a.d_bucket_off, self.size + 1, np.uint32)
+            out["bucket16"] = get(a.d_bucket16, 2 * self.size, np.int64)
+            out["bucket8"] = get(a.d_bucket8, a.n_bucket8, np.uint64) if a.d_bucket8 else None
+        return out
+
     def set_payload(self, d_payload, n_cols: int, stream=None):
         """Attach build payload columns: d_payload row-major int64 [n_keys, n_cols] in build order."""
         check(lib().ccj_table_set_payload(self._h, _ptr(d_payload), n_cols, _stream(stream)), "ccj_table_set_payload")
@@ -286,6 +356,16 @@ class Table:
         torch.cuda.synchronize()
         a = acc.cpu().tolist()
         return a[0], a[1]
+
+    def probe_cost_walk(self, keys, stream=None):
+        """(words examined, matches, words a first-match walk examines, its aligned 32-byte windows)
+        over a key column (ccj_probe_cost_walk) — roofline accounting of the first-match walk."""
+        import torch
+        acc = torch.zeros(4, dtype=torch.int64, device=keys.device)
+        check(lib().ccj_probe_cost_walk(self._h, _ptr(keys), keys.numel(), _ptr(acc), _stream(stream)),
+              "ccj_probe_cost_walk")
+        torch.cuda.synchronize()
+        return tuple(int(x) for x in acc.cpu().tolist())
 
     def alloc_outputs(self, n_rows: int, chunk: int, cap: int | None = None, rounds: bool = True,
                       payload: bool = True, device=None, pos: bool = False, payload_cols: int = 0):
@@ -622,17 +702,26 @@ def segment_chunk_counts(seg_counts, seg_cap: int, chunk: int, out, status, stre
 _HIP = None
 
 
+def _hip():
+    """The HIP runtime (the one libccj.so and torch use) for raw copies and phase events."""
+    global _HIP
+    if _HIP is None:
+        lib()
+        _HIP = C.CDLL("libamdhip64.so")
+        _HIP.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        _HIP.hipEventCreate.argtypes = [C.POINTER(C.c_void_p)]
+        _HIP.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
+        _HIP.hipEventDestroy.argtypes = [C.c_void_p]
+    return _HIP
+
+
 def _d2h_i64(ptr, n):
     """Copy n int64 from a raw device pointer the library owns (hipMemcpy; caller synchronised)."""
     import numpy as np
-    global _HIP
     out = np.empty(n, np.int64)
     if n == 0:
         return out
-    if _HIP is None:
-        _HIP = C.CDLL("libamdhip64.so")
-        _HIP.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-    rc = _HIP.hipMemcpy(out.ctypes.data_as(C.c_void_p), C.c_void_p(ptr), n * 8, 2)  # hipMemcpyDeviceToHost
+    rc = _hip().hipMemcpy(out.ctypes.data_as(C.c_void_p), C.c_void_p(ptr), n * 8, 2)  # hipMemcpyDeviceToHost
     if rc != 0:
         raise CCJError(f"hipMemcpy failed ({rc})")
     return out

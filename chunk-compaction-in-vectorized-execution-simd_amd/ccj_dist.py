@@ -12,10 +12,12 @@ HIP streams (partition, comm, probe) with double-buffered send/receive slots:
      L2-resident) while the comm stream moves the next group's batches;
   4. (verification only) all-reduce of match counts and of the order-insensitive L2 checksum.
 8 bytes cross xGMI per tuple in a timed step: the source rank is implied by the receive segment and
-the source row by the position in it — the sender's owner split keeps every position's row in its
-send slot's row buffer, so a match (receive position, payload) names its probe tuple without the
-row travelling.  verify=True also moves the rows (a third all-to-all): the checksum needs global
-rows on the receiver.
+the source row by the position in it — the sender's owner split keeps every position's row in a row
+buffer of that BATCH (one per batch of the step, kept until the batch is partitioned again in the
+next step, i.e. longer than the receiver keeps the batch's probe results: two receive groups), so a
+match (receive position, payload) names its probe tuple without the row travelling.  The rows can be
+fetched afterwards (resolve_kept_groups: an untimed all-to-all of the kept row buffers); verify=True
+moves them inside the step (a third all-to-all): its checksum needs global rows on the receiver.
 
 Overflow.  Three things can overflow under key skew, each raising a flag in the rank's status
 word: a send segment of the owner split, a receive segment's count, and the local probe's own
@@ -265,7 +267,10 @@ class ShardedProbe:
         gslots = self.group * slots
         self.fparts = {}
         mk = lambda dt, n: [o.zeros(n, dt) for _ in range(2)]  # noqa: E731
-        self.sk, self.sr, self.sc = mk(torch.int64, slots), mk(torch.int32, slots), mk(torch.int64, self.nseg)
+        self.sk, self.sc = mk(torch.int64, slots), mk(torch.int64, self.nseg)
+        # send rows: one buffer per batch (not per send slot), so a timed step's matches stay traceable
+        # to their probe rows after the step (4 B per slot: 4.3 GB per rank at C4)
+        self.srb = [o.zeros(slots, torch.int32) for _ in range(self.batches)]
         self.rk, self.rr = mk(torch.int64, gslots), mk(torch.int32, gslots)
         self.rc = mk(torch.int64, self.group * self.nseg)
         self.cc = mk(torch.int32, gslots // self.chunk)
@@ -317,7 +322,8 @@ class ShardedProbe:
             self.fparts[n] = self.ops.fixed_partitioner(n, self.world, self.sub_cap)
         self.pstream.wait_event(self.ev_comm[s])  # the previous all-to-all from send slot s is done
         with self._timed(self.part_events, self.pstream, timing):
-            self.fparts[n](keys[lo:lo + n], lo, self.sk[s], self.sr[s], self.sc[s], self.status, self.pstream)
+            self.fparts[n](keys[lo:lo + n], lo, self.sk[s], self.srb[j % self.batches], self.sc[s], self.status,
+                           self.pstream)
         self.ev_part[s].record(self.pstream)
 
     def _exchange(self, j, timing=False, rows=True):
@@ -327,7 +333,7 @@ class ShardedProbe:
         if (j % self.batches) % self.group == 0:
             self.comm.wait_event(self.ev_probe[gs])  # the previous probe of receive group slot gs is done
         with self.ops.on(self.comm), self._timed(self.comm_events, self.comm, timing):
-            exchange_fixed(self.sk[s], self.sr[s], self.sc[s], rk, rr, rc, rows=rows)
+            exchange_fixed(self.sk[s], self.srb[j % self.batches], self.sc[s], rk, rr, rc, rows=rows)
         self.ev_comm[s].record(self.comm)
 
     def reset_timing(self):
@@ -411,6 +417,7 @@ class ShardedProbe:
         self.stream.wait_stream(cur)
         self.pstream.wait_stream(cur)
         total = steps * self.batches  # run batches j: batch j % batches of step j // batches
+        self._run_steps = steps
         self._partition(keys, 0, timing)
         self._exchange(0, timing, rows=verify)
         m, l2 = 0, 0
@@ -423,8 +430,11 @@ class ShardedProbe:
                 g = i // self.group
                 self._probe(j0, g, timing)
                 if verify:
-                    bm, bl = o.checksum(self.outs[self._gslot(j)], self.chunk, self.group_row_map(j0, g), self.stream)
+                    gs = self._gslot(j)
+                    bm, bl = o.checksum(self.outs[gs], self.chunk, self.group_row_map(j0, g), self.stream)
                     m, l2 = m + bm, (l2 + bl) % (1 << 64)
+                    # the next user of receive slot gs waits for the verification's reads of it too
+                    self.ev_probe[gs].record(self.stream)
         cur.wait_stream(self.stream)
         cur.wait_stream(self.pstream)
         cur.wait_stream(self.comm)
@@ -440,6 +450,33 @@ class ShardedProbe:
             return (m, l2) if verify else None
         self.last_exact = False
         return (m, l2) if verify else None
+
+    def resolve_kept_groups(self):
+        """After a timed (key-only) run: fetch the probe rows of the groups whose results are still
+        held (the run's last two groups — the receive slots alternate) from their senders' kept
+        per-batch row buffers, with an untimed all-to-all per batch, and return (matches, l2 over
+        global rows, batch indices covered).  Shows that a timed step's matches name their probe
+        tuples although no row crossed during it.  Call right after run() (no verify)."""
+        o = self.ops
+        if self.last_exact:
+            raise RuntimeError("the last run fell back to the exact-size protocol: nothing kept")
+        o.synchronize()
+        groups = list(range(max(0, self.n_groups - 2), self.n_groups))
+        j0 = (self._run_steps - 1) * self.batches  # the run's last step
+        m, l2, covered = 0, 0, []
+        for g in groups:
+            first, last = self._group_range(g)
+            for i in range(first, last + 1):
+                gs, rk, rr, rc = self._recv(j0 + i)
+                with o.on(self.comm):
+                    dist.all_to_all_single(rr, self.srb[i])
+                covered.append(i)
+            self.stream.wait_stream(self.comm)
+            gs = self._gslot(j0 + first)
+            bm, bl = o.checksum(self.outs[gs], self.chunk, self.group_row_map(j0, g), self.stream)
+            m, l2 = m + bm, (l2 + bl) % (1 << 64)
+        o.synchronize()
+        return m, l2, covered
 
     # ---- exact-size protocol (fallback for skewed keys), batch by batch, not overlapped ----
     def step_exact(self, keys, row_base: int, verify: bool = False):

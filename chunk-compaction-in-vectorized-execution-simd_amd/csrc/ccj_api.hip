@@ -23,6 +23,18 @@ namespace {
 
 thread_local std::string g_err;
 
+// Phase boundary events (ccj_set_phase_events): the reference's CycleProfiler slots
+// (profiler.h:262-290) mapped onto this thread's next probe call's kernels.
+thread_local hipEvent_t g_phase[4] = {};
+thread_local uint32_t g_n_phase = 0;
+void phase_mark(hipStream_t s, uint32_t i) {
+  if (i < g_n_phase && g_phase[i]) (void)hipEventRecord(g_phase[i], s);
+}
+void phase_marks(hipStream_t s, uint32_t from, uint32_t to) {
+  for (uint32_t i = from; i <= to; ++i) phase_mark(s, i);
+}
+
+
 int fail(int code, const std::string &msg) {
   g_err = msg;
   return code;
@@ -281,7 +293,7 @@ int build_chain_host(const int64_t *keys, uint64_t n, ccj_table **out) {
     t->d_bucket = (int64_t *)d;
   }
   if (longest < 0xFFu) {  // 8-byte records {start | len << 32 | fp(node 0) << 40 | fp(node 1) << 52}
-    std::vector<uint64_t> rec(size);
+    std::vector<uint64_t> rec(size < 2 ? 2 : size, 0);  // read as aligned 16-byte pairs: >= 2 records
     for (uint64_t b = 0; b < size; ++b) {
       const uint64_t lo = off[b], len = off[b + 1] - off[b];
       const uint64_t fp0 = len ? ccj::bucket_fp(ccj::murmurhash64((uint64_t)chain[lo])) : 0u;
@@ -399,6 +411,13 @@ extern "C" {
 
 const char *ccj_last_error(void) { return g_err.c_str(); }
 
+int ccj_set_phase_events(void *const *events, uint32_t n) {
+  if (n > 4 || (n && !events)) return fail(CCJ_ERR_INVALID, "ccj_set_phase_events: at most 4 events");
+  for (uint32_t i = 0; i < 4; ++i) g_phase[i] = i < n ? (hipEvent_t)events[i] : nullptr;
+  g_n_phase = n;
+  return CCJ_OK;
+}
+
 int ccj_abi_version(void) { return CCJ_ABI_VERSION; }
 
 int ccj_device_init(int device) {
@@ -415,11 +434,11 @@ int ccj_table_build_reference(int kind, uint64_t n, uint64_t cf, int layout, ccj
   if (kind != CCJ_TABLE_LP && kind != CCJ_TABLE_CHAIN) return fail(CCJ_ERR_INVALID, "bad table kind");
   if (int rc = check_device()) return rc;
   *out = nullptr;
-  if (layout == CCJ_LAYOUT_REFERENCE || kind == CCJ_TABLE_CHAIN) {
+  if (layout != CCJ_LAYOUT_REFERENCE && layout != CCJ_LAYOUT_DEVICE) return fail(CCJ_ERR_INVALID, "bad layout");
+  if (layout == CCJ_LAYOUT_REFERENCE && kind == CCJ_TABLE_LP) {  // sequential insert order (L3 layout)
     std::vector<int64_t> keys = reference_keys(n, cf);
-    return kind == CCJ_TABLE_LP ? build_lp_host(keys.data(), n, out) : build_chain_host(keys.data(), n, out);
+    return build_lp_host(keys.data(), n, out);
   }
-  if (layout != CCJ_LAYOUT_DEVICE) return fail(CCJ_ERR_INVALID, "bad layout");
   hipStream_t s = (hipStream_t)stream;
   int64_t *d_keys = nullptr;
   if (hipMalloc(&d_keys, std::max<uint64_t>(n, 1) * sizeof(int64_t)) != hipSuccess)
@@ -430,7 +449,10 @@ int ccj_table_build_reference(int kind, uint64_t n, uint64_t cf, int layout, ccj
     return hip_fail(e, "gen reference keys");
   }
   const uint64_t dup = std::max<uint64_t>(1, std::min<uint64_t>(cf, n));  // first group: min(cf, n) copies
-  int rc = build_lp_device(d_keys, n, s, dup, out);
+  // chaining: the device's stable bucket sort gives the reference's chain order whatever the
+  // layout asked for (both layouts are the same table)
+  int rc = kind == CCJ_TABLE_LP ? build_lp_device(d_keys, n, s, dup, out) : ccj::build_chain_device(d_keys, n, s, dup, out);
+  if (rc == CCJ_OK && kind == CCJ_TABLE_CHAIN) (*out)->info.layout = layout;
   (void)hipStreamSynchronize(s);
   (void)hipFree(d_keys);
   return rc;
@@ -450,18 +472,26 @@ int ccj_table_build_on_device(int kind, const int64_t *d_keys, uint64_t n, ccj_s
   if (int rc = check_device()) return rc;
   *out = nullptr;
   if (kind == CCJ_TABLE_LP) return build_lp_device(d_keys, n, (hipStream_t)stream, 0, out);
-  if (kind == CCJ_TABLE_CHAIN) {
-    // Chain order must equal insertion order; until the device counting sort lands, stage on host.
-    std::vector<int64_t> h(n);
-    if (n) HIP_TRY(hipMemcpy(h.data(), d_keys, n * sizeof(int64_t), hipMemcpyDeviceToHost), "download keys");
-    return build_chain_host(h.data(), n, out);
-  }
+  if (kind == CCJ_TABLE_CHAIN) return ccj::build_chain_device(d_keys, n, (hipStream_t)stream, 0, out);
   return fail(CCJ_ERR_INVALID, "bad table kind");
 }
 
 int ccj_table_get_info(const ccj_table *t, ccj_table_info *info) {
   if (!t || !info) return fail(CCJ_ERR_INVALID, "ccj_table_get_info: null");
   *info = t->info;
+  return CCJ_OK;
+}
+
+int ccj_table_get_arrays(const ccj_table *t, ccj_table_arrays *a) {
+  if (!t || !a) return fail(CCJ_ERR_INVALID, "ccj_table_get_arrays: null");
+  *a = ccj_table_arrays{};
+  a->d_table = t->d_table;
+  a->positions = t->positions;
+  a->d_row = t->d_row;
+  a->d_bucket_off = t->d_off;
+  a->d_bucket16 = t->d_bucket;
+  a->d_bucket8 = t->d_bucket8;
+  a->n_bucket8 = t->d_bucket8 ? (t->info.size < 2 ? 2 : t->info.size) : 0;
   return CCJ_OK;
 }
 
@@ -641,6 +671,7 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   if (rows) out_row_map = a->out_sel;
   void *rest = (char *)ws + align256(L.positions * 8);
   const uint64_t out_chunks = L.positions / a->chunk + (L.positions % a->chunk ? 1 : 0);
+  phase_mark(s, 0);
   if (L.pl.lo_bits == 0) {  // the whole table is one window: identity order
     HIP_TRY(hipMemcpyAsync(pkeys, a->keys, a->n_rows * 8, hipMemcpyDeviceToDevice, s), "copy");
     HIP_TRY(ccj::launch_iota_u32(out_row_map, a->n_rows, s), "iota");
@@ -666,6 +697,7 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
     if (out_chunks > p.n_chunks)  // the layout's trailing chunks are empty in the exact form
       HIP_TRY(hipMemsetAsync(a->out_count + p.n_chunks, 0, (out_chunks - p.n_chunks) * 4, s), "count tail");
   }
+  phase_mark(s, 1);  // hash + home partition of every key (and, CCJ_PART_ROWS, keys + rows written out)
   p.keys = pkeys;
   p.xcd_swizzle = 1;  // consecutive chunks (one partition's rows) go to one XCD: its L2 holds the window
   // distinct build keys and no per-chunk rounds: the walk ends a row at its match (C2: 1.168 -> 1.013
@@ -704,6 +736,7 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
     const size_t exact_ws = ccj::slot_partition_workspace(a->n_rows, L.pl);
     void *rws = (char *)rest + align256(fixed > exact_ws ? fixed : exact_ws);
     HIP_TRY(ccj::launch_probe_rank(p, ix, rws, s), "rank walk launch");
+    phase_marks(s, 2, 3);
     return CCJ_OK;
   }
 #endif
@@ -718,6 +751,7 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
     }
 #endif
     HIP_TRY(ccj::launch_probe_flat(t->info.kind, p, s), "probe launch");
+    phase_marks(s, 2, 3);  // match + advance (the walk, which also writes the chunks with misses)
 #ifdef CCJ_TUNING
     if (p.stats) {
       unsigned long long h[8];
@@ -738,7 +772,9 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   q.out_pos = pos;
   q.n_pay = 0;
   hipError_t e = ccj::launch_probe_flat(t->info.kind, q, s);
+  phase_mark(s, 2);
   if (e == hipSuccess) e = ccj::launch_gather_payload(p, pos, s);
+  phase_mark(s, 3);
   if (!p.out_pos) (void)hipFreeAsync(pos, s);
   HIP_TRY(e, "partitioned probe + payload gather launch");
   return CCJ_OK;
@@ -819,10 +855,12 @@ int ccj_probe_ordered(const ccj_table *t, const ccj_probe_args *a, void *ws, siz
   uint2 *runs = (uint2 *)(w + O.runs);
   uint32_t *ovf_runs = (uint32_t *)(w + O.ovf_runs);
   const PartLayout &L = O.L;
+  phase_mark(s, 0);
   // 1. one-pass slot split of the live rows, recording where every tile's runs went
   HIP_TRY(ccj::launch_slot_split_fixed(a->keys, a->n_rows, L.pl, L.seg_cap, L.ovf_base, L.ovf_cap, cursors, pkeys,
                                        row_map, a->status, s, a->counts, a->chunk, runs, ovf_runs),
           "slot split");
+  phase_mark(s, 1);
   // 2. walk with the table window L2-resident: every row's Next-round word at its position
   ccj::ProbeParams q = p;
   q.keys = pkeys;
@@ -841,6 +879,7 @@ int ccj_probe_ordered(const ccj_table *t, const ccj_probe_args *a, void *ws, siz
   const uint32_t w16 = t->info.max_dup <= 1 && ccj_tune_int("CCJ_W16", 1) ? 1u : 0u;
   q.w16 = w16;
   HIP_TRY(ccj::launch_ordered_walk(t->info.kind, q, s), "ordered walk");
+  phase_mark(s, 2);
   // 3. the words back into row order, one split tile per workgroup
   HIP_TRY(ccj::launch_unsplit_words(runs, ovf_runs, reinterpret_cast<const uint16_t *>(row_map), w_pos, w_row,
                                     a->n_rows, L.parts, O.tile, a->status, s,
@@ -851,6 +890,7 @@ int ccj_probe_ordered(const ccj_table *t, const ccj_probe_args *a, void *ws, siz
   p.w16 = w16;
   p.xcd_swizzle = 0;
   HIP_TRY(ccj::launch_ordered_emit(t->info.kind, p, s), "ordered emit");
+  phase_mark(s, 3);  // gather: the round words back in row order + the reference-order emit
   return CCJ_OK;
 }
 
@@ -859,8 +899,10 @@ int ccj_probe(const ccj_table *t, const ccj_probe_args *a, ccj_stream stream) {
   if (int rc = fill_probe_params(t, a, p)) return rc;
   if (a->n_rows == 0) return CCJ_OK;  // no chunks: nothing to launch
   hipStream_t s = (hipStream_t)stream;
+  phase_mark(s, 0);
   if (p.n_pay == 0) {
     HIP_TRY(ccj::launch_probe(t->info.kind, p, s), "probe launch");
+    phase_marks(s, 1, 3);  // probe_chunks fuses hash, match, gather and advance
     return CCJ_OK;
   }
   // Wide payload: the probe records every match's table position, a second pass gathers rows.
@@ -870,7 +912,9 @@ int ccj_probe(const ccj_table *t, const ccj_probe_args *a, ccj_stream stream) {
   q.out_pos = pos;
   q.n_pay = 0;
   hipError_t e = ccj::launch_probe(t->info.kind, q, s);
+  phase_marks(s, 1, 2);
   if (e == hipSuccess) e = ccj::launch_gather_payload(p, pos, s);
+  phase_mark(s, 3);
   if (!p.out_pos) (void)hipFreeAsync(pos, s);
   HIP_TRY(e, "probe + payload gather launch");
   return CCJ_OK;
@@ -1035,6 +1079,14 @@ int ccj_probe_cost(const ccj_table *t, const int64_t *d_keys, uint64_t n, uint64
   HIP_TRY(ccj::launch_probe_cost(t->info.kind, t->d_table, t->d_off, (uint32_t)(t->info.size - 1), d_keys, n,
                                  (unsigned long long *)d_acc, (hipStream_t)stream),
           "probe cost");
+  return CCJ_OK;
+}
+
+int ccj_probe_cost_walk(const ccj_table *t, const int64_t *d_keys, uint64_t n, uint64_t *d_acc, ccj_stream stream) {
+  if (!t || (!d_keys && n) || !d_acc) return fail(CCJ_ERR_INVALID, "ccj_probe_cost_walk: bad argument");
+  HIP_TRY(ccj::launch_probe_cost(t->info.kind, t->d_table, t->d_off, (uint32_t)(t->info.size - 1), d_keys, n,
+                                 (unsigned long long *)d_acc, (hipStream_t)stream, true),
+          "probe cost (walk)");
   return CCJ_OK;
 }
 

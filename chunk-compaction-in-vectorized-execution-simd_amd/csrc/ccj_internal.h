@@ -170,6 +170,9 @@ hipError_t launch_scatter_payload(const int64_t *src, uint32_t n_cols, const uin
 // Largest multiplicity of one key (max_run = longest occupied run bounds the walk).
 hipError_t launch_lp_max_dup(const int64_t *slots, uint64_t n_slots, uint32_t max_run, uint32_t *out, hipStream_t s);
 hipError_t launch_lp_runs(const int64_t *slots, uint64_t n_slots, uint32_t *seg_stats, hipStream_t s);
+// The chaining table built on the device (ccj_build.hip): stable bucket sort -> CSR, row map,
+// 16- and 8-byte bucket records, longest chain; known_dup = 0: max_dup computed from the keys.
+int build_chain_device(const int64_t *d_keys, uint64_t n, hipStream_t s, uint64_t known_dup, ccj_table **out);
 constexpr uint64_t kRunSegment = 4096;
 // C3 probe stream; zipf: device copy of the rank table (kZipfBuckets + 1 entries, zipf_table()).
 hipError_t launch_gen_c3(int64_t *out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t n_build, uint64_t cf,
@@ -181,7 +184,8 @@ hipError_t launch_probe_visits(int kind, const int64_t *table, const uint32_t *o
                                const int64_t *keys, const uint32_t *sel, uint32_t count, uint32_t max_rounds,
                                int64_t *vals, uint32_t *len, hipStream_t s);
 hipError_t launch_probe_cost(int kind, const int64_t *table, const uint32_t *off, uint32_t mask,
-                             const int64_t *keys, uint64_t n, unsigned long long *acc, hipStream_t s);
+                             const int64_t *keys, uint64_t n, unsigned long long *acc, hipStream_t s,
+                             bool walk = false);
 hipError_t launch_result_checksum(const uint32_t *count, const uint32_t *sel, const int64_t *payload,
                                   uint64_t n_chunks, uint64_t cap, uint32_t chunk, uint64_t row_base,
                                   const uint64_t *row_map, unsigned long long *acc, hipStream_t s);

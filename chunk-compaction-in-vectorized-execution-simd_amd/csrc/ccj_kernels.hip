@@ -876,36 +876,72 @@ __global__ void gen_uniform(int64_t *out, uint64_t n, uint64_t seed, uint64_t fi
     out[t] = (int64_t)(splitmix_at(seed, first + t) % range);
 }
 
-template <int KIND>
+// Work accounting (roofline).  acc[0] += table words the reference examines (LP: every slot from
+// the home slot through the terminating empty, linear_probing_ht.cpp:72-110; chaining: every chain
+// key, chaining_ht.cpp:82-124), acc[1] += matches.  FM (ccj_probe_cost_walk): also what a walk that
+// ends a row at its first match examines (the throughput path's first_match walk, distinct-key
+// tables) — acc[2] += words (LP: home through the match, or through the empty slot on a miss;
+// chaining: chain keys through the match, or the whole chain), acc[3] += the aligned 32-byte windows
+// those words lie in (LP: 4-slot windows; chaining: 2-key windows of the chain array after round 0,
+// which the 8-byte bucket record's fingerprint / 16-byte record's first key serves).
+template <int KIND, bool FM>
 __global__ void probe_cost(const int64_t *table, const uint32_t *off, uint32_t mask, const int64_t *keys,
                            uint64_t n, unsigned long long *acc) {
-  unsigned long long ex = 0, mt = 0;
+  unsigned long long ex = 0, mt = 0, fw = 0, win = 0;
   for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
     const int64_t k = keys[t];
     const uint32_t h = (uint32_t)murmurhash64((uint64_t)k) & mask;
+    uint32_t first = 0;  // words examined through the first match (0: no match yet)
     if (KIND == CCJ_TABLE_LP) {
-      uint32_t s = h;
+      uint32_t s = h, w = 0;
       while (true) {
         const int64_t v = table[s];
         ++ex;
+        ++w;
         if (v == -1) break;
-        mt += v == k;
+        if (v == k) {
+          ++mt;
+          if (!first) first = w;
+        }
         s = (s + 1u) & mask;
       }
+      if (FM) {
+        const uint32_t L = first ? first : w;
+        fw += L;
+        win += ((h & 3u) + L - 1u) / 4u + 1u;  // aligned 4-slot windows from the home slot's
+      }
     } else {
-      for (uint32_t q = off[h], e = off[h + 1]; q < e; ++q) {
+      const uint32_t lo = off[h], e = off[h + 1];
+      for (uint32_t q = lo; q < e; ++q) {
         ++ex;
-        mt += table[q] == k;
+        if (table[q] == k) {
+          ++mt;
+          if (!first) first = q - lo + 1u;
+        }
+      }
+      if (FM) {
+        const uint32_t L = first ? first : e - lo;
+        fw += L;
+        // round 0 from the bucket record; later keys q in [lo + 1, lo + L) in aligned 2-key windows
+        if (L > 1) win += ((lo + L - 1u) >> 1) - ((lo + 1u) >> 1) + 1u;
       }
     }
   }
   for (int d = 32; d > 0; d >>= 1) {
     ex += __shfl_xor(ex, d);
     mt += __shfl_xor(mt, d);
+    if (FM) {
+      fw += __shfl_xor(fw, d);
+      win += __shfl_xor(win, d);
+    }
   }
   if ((threadIdx.x & 63) == 0) {
     atomicAdd(acc, ex);
     atomicAdd(acc + 1, mt);
+    if (FM) {
+      atomicAdd(acc + 2, fw);
+      atomicAdd(acc + 3, win);
+    }
   }
 }
 
@@ -2973,11 +3009,16 @@ hipError_t launch_gen_uniform(int64_t *out, uint64_t n, uint64_t seed, uint64_t 
 }
 
 hipError_t launch_probe_cost(int kind, const int64_t *table, const uint32_t *off, uint32_t mask,
-                             const int64_t *keys, uint64_t n, unsigned long long *acc, hipStream_t s) {
+                             const int64_t *keys, uint64_t n, unsigned long long *acc, hipStream_t s, bool walk) {
   if (n == 0) return hipSuccess;
   const dim3 g(grid_for(n, 256)), b(256);
-  if (kind == CCJ_TABLE_LP) hipLaunchKernelGGL(probe_cost<CCJ_TABLE_LP>, g, b, 0, s, table, off, mask, keys, n, acc);
-  else hipLaunchKernelGGL(probe_cost<CCJ_TABLE_CHAIN>, g, b, 0, s, table, off, mask, keys, n, acc);
+  if (kind == CCJ_TABLE_LP) {
+    if (walk) hipLaunchKernelGGL((probe_cost<CCJ_TABLE_LP, true>), g, b, 0, s, table, off, mask, keys, n, acc);
+    else hipLaunchKernelGGL((probe_cost<CCJ_TABLE_LP, false>), g, b, 0, s, table, off, mask, keys, n, acc);
+  } else {
+    if (walk) hipLaunchKernelGGL((probe_cost<CCJ_TABLE_CHAIN, true>), g, b, 0, s, table, off, mask, keys, n, acc);
+    else hipLaunchKernelGGL((probe_cost<CCJ_TABLE_CHAIN, false>), g, b, 0, s, table, off, mask, keys, n, acc);
+  }
   return hipGetLastError();
 }
 

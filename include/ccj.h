@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CCJ_ABI_VERSION 11  /* 11: the rank walk in the tuning build only; 10: CCJ_PART_ROWS with positions / payload columns; 9: CCJ_PART_SHARE, CU-masked streams; 8: CCJ_PART_RANK; 7: CCJ_PART_ROWS */
+#define CCJ_ABI_VERSION 12  /* 12: chaining tables built on the device (stable bucket sort), ccj_table_get_arrays; 11: the rank walk in the tuning build only; 10: CCJ_PART_ROWS with positions / payload columns; 9: CCJ_PART_SHARE, CU-masked streams; 8: CCJ_PART_RANK; 7: CCJ_PART_ROWS */
 
 enum ccj_status {
   CCJ_OK = 0,
@@ -56,7 +56,9 @@ enum ccj_layout {
   CCJ_LAYOUT_REFERENCE = 0,
   /* Built on the device.  LP: parallel atomicCAS insert — same occupied slots and same per-probe
    * match multiset as the reference, slot order inside a cluster may differ (L1/L2 parity).
-   * Chain: stable counting sort — identical to the reference order (L3). */
+   * Chain: stable bucket sort (histogram + scan + stable radix sort by bucket) — identical to the
+   * reference order (L3), every array byte-identical to the host build.  Chaining tables are built
+   * this way for either layout (the two are the same table). */
   CCJ_LAYOUT_DEVICE = 1
 };
 
@@ -81,6 +83,15 @@ typedef struct ccj_table_info {
 /* ---- device / errors ---------------------------------------------------------------------- */
 const char *ccj_last_error(void);
 int ccj_abi_version(void);
+/* Phase timing in the reference's 4-phase schema (CycleProfiler, profiler.h:262-290: 0 "Hash & Find
+ * Bucket", 1 "Match Tuples", 2 "Gather Tuples", 3 "Advance Pointers"): the caller's hipEvent_t
+ * handles (n <= 4; NULL / 0 clears), recorded on the call's stream by this thread's later probe
+ * calls at their kernel boundaries — events[0] before the first kernel, [1] after hashing and
+ * finding every row's bucket (the split of the partitioned / ordered paths), [2] after match +
+ * advance (the walk; this design fuses the two), [3] after the gather (C5 payload columns, or the
+ * ordered path's unsplit + reference-order emit).  A kernel that fuses several phases records
+ * their boundaries together (probe_chunks: [1], [2], [3] after its one launch). */
+int ccj_set_phase_events(void *const *events, uint32_t n);
 /* Selects the HIP device for this thread and checks it is gfx950. */
 int ccj_device_init(int device);
 
@@ -92,10 +103,30 @@ int ccj_table_build_reference(int kind, uint64_t n_rhs_tuples, uint64_t chunk_fa
                               ccj_stream stream, ccj_table **out);
 /* Same tables from caller keys, inserted in array order (host keys; CCJ_LAYOUT_REFERENCE). */
 int ccj_table_build_from_host(int kind, const int64_t *h_keys, uint64_t n, ccj_table **out);
-/* Same tables from device-resident keys, built on the device (CCJ_LAYOUT_DEVICE). */
+/* Same tables from device-resident keys, built on the device (CCJ_LAYOUT_DEVICE; chaining: the
+ * reference's chain order, max_dup computed from the keys). */
 int ccj_table_build_on_device(int kind, const int64_t *d_keys, uint64_t n, ccj_stream stream,
                               ccj_table **out);
 int ccj_table_get_info(const ccj_table *table, ccj_table_info *info);
+/* The table's device arrays (read-only views owned by the table), for checks and external
+ * kernels: LP: d_table = slots[positions] (padded to >= 4), d_row = slot -> build tuple (kNoRow
+ * 0xFFFFFFFF for empty slots); chaining: d_table = chain keys[positions] (bucket-major, insertion
+ * order, padded to a multiple of 4 with -1), d_row = chain position -> build tuple,
+ * d_bucket_off = uint32[size + 1] CSR offsets, d_bucket16 = per bucket {start | len << 32, first
+ * key} (int64 pairs), d_bucket8 = per bucket {start | len << 32 | fp0 << 40 | fp1 << 52} (n_bucket8
+ * = max(size, 2) entries; NULL when a chain has 255 or more keys).  No reference counterpart:
+ * the private members HashTable::linked_lists_ (chaining_ht.h:96) and LPHashTable::slots_
+ * (linear_probing_ht.h:66). */
+typedef struct ccj_table_arrays {
+  const int64_t *d_table;
+  uint64_t positions;
+  const uint32_t *d_row;
+  const uint32_t *d_bucket_off;
+  const int64_t *d_bucket16;
+  const uint64_t *d_bucket8;
+  uint64_t n_bucket8;
+} ccj_table_arrays;
+int ccj_table_get_arrays(const ccj_table *table, ccj_table_arrays *arrays);
 /* Attaches build-side payload columns (C5): d_payload is row-major int64
  * [n_keys][n_cols] in build-tuple order (the order keys were given to the builder).  The table
  * re-lays them out by table position (slot / chain index) so a match gathers one contiguous row.
@@ -403,6 +434,14 @@ int ccj_gen_reference_keys(int64_t *d_out, uint64_t first, uint64_t n, uint64_t 
  * the terminating empty; chain: chain keys visited), d_acc[1] += matches, over n probe keys. */
 int ccj_probe_cost(const ccj_table *table, const int64_t *d_keys, uint64_t n, uint64_t *d_acc,
                    ccj_stream stream);
+/* The same plus what a walk that ends each row at its FIRST match examines (the throughput path's
+ * walk on distinct-key tables, ccj_probe_partitioned): d_acc[0..1] as ccj_probe_cost, d_acc[2] +=
+ * table words examined through the first match (LP: home slot through the match, or through the
+ * terminating empty on a miss; chaining: chain keys through the match, or the whole chain),
+ * d_acc[3] += aligned 32-byte windows those words lie in (LP: 4-slot windows; chaining: 2-key
+ * windows of the chain array after round 0, which the bucket record serves).  d_acc: 4 words. */
+int ccj_probe_cost_walk(const ccj_table *table, const int64_t *d_keys, uint64_t n, uint64_t *d_acc,
+                        ccj_stream stream);
 /* Result verification without a download: d_acc[0] += matches, d_acc[1] += sum of the L2 term
  * fmix(row * gamma + fmix(payload + 1)) (oracle/ccj_gen.h ccj_l2_term) over every match of a
  * ccj_probe output, row = row_base + c*chunk + out_sel. */

@@ -381,3 +381,69 @@ def test_sharded_run_pipelined_steps_gloo(world, batches, group, subs, steps, sk
         assert exact == [skew_rank >= 0]
         if skew_rank < 0:
             assert probes == steps * ng
+
+
+def _timed_resolve_worker(rank, world, port, cfg, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "chunk-compaction-in-vectorized-execution-simd_amd"),
+                    os.path.join(root, "tests")]
+    from oracle import oracle as O
+    import ccj_dist
+    from test_dist_cpu import HostOps
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n_build, cf, n_probe, rng, seed, chunk, batches, group, subs, steps = cfg
+    ops = HostOps(subs=subs)
+    sp = ccj_dist.ShardedProbe(n_build, cf, n_probe, chunk, world, rank, batches=batches, ops=ops, group=group)
+    keys = O.uniform_keys(seed, rank * n_probe, (rank + 1) * n_probe, rng)
+    for rr in sp.rr:
+        rr.fill_(-7)  # poisoned: a timed run moves no rows
+    sp.run(torch.from_numpy(keys), rank * n_probe, steps=steps, timing=True)
+    assert not sp.last_exact
+    assert all(bool((rr == -7).all()) for rr in sp.rr), "rows crossed in a timed run"
+    m, l2, covered = sp.resolve_kept_groups()
+    tot = torch.tensor([m, l2 - (1 << 64) if l2 >= (1 << 63) else l2], dtype=torch.int64)
+    dist.all_reduce(tot)
+    # the exact answer over the covered batches' rows of EVERY source rank (this rank's share here)
+    table = O.Table(O.LP, O.ref_build_keys(n_build, cf))
+    wm, wl2 = 0, 0
+    for i in covered:
+        lo, n = sp._batch(i)
+        a, b = table.probe_totals(keys[lo:lo + n], chunk, row_base=rank * n_probe + lo)
+        wm, wl2 = wm + a, (wl2 + b) % (1 << 64)
+    wt = torch.tensor([wm, wl2 - (1 << 64) if wl2 >= (1 << 63) else wl2], dtype=torch.int64)
+    dist.all_reduce(wt)
+    q.put((rank, int(tot[0]), int(tot[1]) % (1 << 64), int(wt[0]), int(wt[1]) % (1 << 64), sorted(covered)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,batches,group,subs,steps", [(2, 5, 2, 1, 1), (2, 4, 1, 8, 2), (4, 3, 4, 1, 2)])
+def test_sharded_timed_run_rows_resolvable_gloo(world, batches, group, subs, steps):
+    """a timed run moves keys only (8 B per tuple), so its matches must stay traceable to
+    their probe rows through the senders' kept row buffers (one per batch).  After a timed run the
+    groups whose results are still held (the last two) get their rows by an untimed all-to-all of
+    those buffers, and their L1 + L2 over GLOBAL rows equal the exact answer for those batches on
+    every source rank; no row crossed during the run."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    cfg = (1 << 13, 2, 3 << 12, 3 << 12, 31, 256, batches, group, subs, steps)
+    procs = [ctx.Process(target=_timed_resolve_worker, args=(r, world, port, cfg, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        got = sorted(q.get(timeout=240) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for p in procs:
+        assert p.exitcode == 0
+    n_groups = -(-batches // group)
+    want_cov = sorted(range(max(0, n_groups - 2) * group, batches))
+    for rank, m, l2, wm, wl2, covered in got:
+        assert (m, l2) == (wm, wl2) and m > 0
+        assert covered == want_cov

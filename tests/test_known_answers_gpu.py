@@ -1,0 +1,108 @@
+"""The reference's own answer vectors replayed on the GPU (SURVEY §4 / §8c known answers).
+
+tests/golden/known_answers.json holds 11 `sum_cases` recorded from the compiled reference
+(oracle/_ref/ref_driver: its LPHashTable / HashTable + Probe / Next loop): LP and chaining, B 256
+and 2048, cf 1/2/4, 100 % and 10 % hits, SplitMix64 and mt19937_64 probe streams, and the C2-size
+2^26-key LP table.  Each is replayed through the C ABI:
+  - ccj_probe (probe_chunks): matches, L2, the order-sensitive L3 fold and the SURVEY checksum equal
+    the reference's (L3);
+  - ccj_probe_ordered where the table has >= 2^22 slots / buckets: the same four values (L3);
+  - ccj_probe_partitioned on a device-built table: CCJ_PART_ROWS where the keys are distinct
+    (LP, cf 1), plain mode with the row map otherwise: matches and L2 (L1 + L2).
+And simd_micro_bench.cpp's known answer (`#tuples: 134217728` for all 8 variants at scale 0: 2^27
+probes, a 128-key table, B = 256) through the C++ facade's Probe / SIMDProbe + Next / InOneNext /
+SIMDNext / SIMDInOneNext on both tables (tests/native/facade_micro_bench.cpp)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from helpers import known_answers
+from oracle import oracle as O
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import ccj  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "chunk-compaction-in-vectorized-execution-simd_amd")
+KA = known_answers()["sum_cases"]
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ccj.device_init(0)
+
+
+def _probe_keys(spec):
+    if spec["gen"] == 1:  # the SURVEY §4 driver's mt19937_64 stream, % range
+        return torch.from_numpy(O.mt64_keys(spec["seed"], spec["n_probe"], spec["range"])).to(DEV)
+    return ccj.gen_uniform_keys(spec["n_probe"], spec["seed"], spec["range"])  # == O.uniform_keys
+
+
+def _sums(out, B):
+    torch.cuda.synchronize()
+    return O.result_sums(out["count"].cpu().numpy(), out["sel"].cpu().numpy(), out["payload"].cpu().numpy(),
+                         out["cap"], B)
+
+
+@pytest.mark.parametrize("path", ["chunk", "ordered", "partitioned"])
+@pytest.mark.parametrize("name", sorted(KA))
+def test_reference_sum_vector_on_gpu(name, path):
+    entry = KA[name]
+    spec, want = entry["spec"], entry["variants"]["next"]
+    kind = ccj.LP if spec["kind"] == "lp" else ccj.CHAIN
+    B, n, cf = spec["B"], spec["n_build"], spec["cf"]
+    keys = _probe_keys(spec)
+    if path == "partitioned":
+        table = ccj.Table.reference(kind, n, cf, ccj.LAYOUT_DEVICE)
+        rows = kind == ccj.LP and int(table.max_dup) == 1
+        out = table.probe_partitioned(keys, B, rows=rows)
+        torch.cuda.synchronize()
+        assert int(out["status"].item()) == 0
+        got = ccj.result_checksum(out, 0) if rows else \
+            ccj.result_checksum(out, B, row_map=out["row_map"].to(torch.int64))
+        assert got == (want["matches"], want["l2"])
+    else:
+        table = ccj.Table.reference(kind, n, cf, ccj.LAYOUT_REFERENCE)
+        if path == "ordered":
+            if table.size < 1 << 22:
+                pytest.skip("ccj_probe_ordered's partitioned route needs >= 2^22 slots / buckets")
+            out = table.probe_ordered(keys, B, rounds=False)
+            assert not out.get("exact_retry")
+        else:
+            out = table.probe(keys, B, rounds=False)
+        torch.cuda.synchronize()
+        assert int(out["status"].item()) == 0
+        assert _sums(out, B) == (want["matches"], want["l2"], want["l3"], want["survey_chk"])
+    table.free()
+
+
+@pytest.fixture(scope="module")
+def micro_bench(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("micro") / "facade_micro_bench")
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-pthread", "-I", os.path.join(ROOT, "include"),
+                    "-I", os.path.join(PKG, "host"), "-o", exe,
+                    os.path.join(ROOT, "tests", "native", "facade_micro_bench.cpp"),
+                    os.path.join(PKG, "host", "ccj_operators.cpp"), "-L", PKG, "-lccj", f"-Wl,-rpath,{PKG}"],
+                   check=True)
+    return exe
+
+
+def test_micro_bench_known_answer_through_facade(micro_bench):
+    """simd_micro_bench.cpp --scale 0 --hit-frequency 1 --chunk-factor 1: all 8 variants (chaining /
+    LP x SIMD / scalar x Next / InOneNext) report #tuples 134217728 (the reference run)."""
+    p = subprocess.run([micro_bench, "0", "1", "1", "1"], capture_output=True, text=True, timeout=900)
+    assert p.returncode == 0, p.stderr[-2000:]
+    got = {}
+    for line in p.stdout.splitlines():
+        t = line.split()
+        if t and t[0] == "#tuples":
+            got[(t[1], t[2])] = int(t[3])
+    assert len(got) == 8, p.stdout
+    assert all(v == 134217728 for v in got.values()), got
