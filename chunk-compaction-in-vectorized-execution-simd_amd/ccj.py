@@ -45,7 +45,7 @@ class TableInfo(C.Structure):
 class TableArrays(C.Structure):
     _fields_ = [("d_table", C.c_void_p), ("positions", C.c_uint64), ("d_row", C.c_void_p),
                 ("d_bucket_off", C.c_void_p), ("d_bucket16", C.c_void_p), ("d_bucket8", C.c_void_p),
-                ("n_bucket8", C.c_uint64)]
+                ("n_bucket8", C.c_uint64), ("d_bucket_filter", C.c_void_p), ("n_filter_words", C.c_uint64)]
 
 
 class ProbeArgs(C.Structure):
@@ -336,6 +336,7 @@ class Table:
             out["off"] = get(a.d_bucket_off, self.size + 1, np.uint32)
             out["bucket16"] = get(a.d_bucket16, 2 * self.size, np.int64)
             out["bucket8"] = get(a.d_bucket8, a.n_bucket8, np.uint64) if a.d_bucket8 else None
+            out["filter"] = get(a.d_bucket_filter, a.n_filter_words, np.uint32) if a.d_bucket_filter else None
         return out
 
     def set_payload(self, d_payload, n_cols: int, stream=None):

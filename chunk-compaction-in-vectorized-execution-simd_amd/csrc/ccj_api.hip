@@ -313,6 +313,12 @@ int build_chain_host(const int64_t *keys, uint64_t n, ccj_table **out) {
   t->info.d_table = t->d_table;
   t->info.d_bucket_off = t->d_off;
   (void)hipGetDevice(&t->device);
+  hipError_t fe = ccj::build_chain_filter(t.get(), nullptr);  // (from the uploaded CSR, on the device)
+  if (fe == hipSuccess) fe = hipDeviceSynchronize();
+  if (fe != hipSuccess) {
+    ccj_table_free(t.release());
+    return hip_fail(fe, "chain bucket filter");
+  }
   *out = t.release();
   return CCJ_OK;
 }
@@ -492,6 +498,8 @@ int ccj_table_get_arrays(const ccj_table *t, ccj_table_arrays *a) {
   a->d_bucket16 = t->d_bucket;
   a->d_bucket8 = t->d_bucket8;
   a->n_bucket8 = t->d_bucket8 ? (t->info.size < 2 ? 2 : t->info.size) : 0;
+  a->d_bucket_filter = t->d_filt;
+  a->n_filter_words = t->d_filt ? t->info.size / 16 : 0;
   return CCJ_OK;
 }
 
@@ -526,6 +534,7 @@ int ccj_table_free(ccj_table *t) {
   if (t->d_off) (void)hipFree(t->d_off);
   if (t->d_bucket) (void)hipFree(t->d_bucket);
   if (t->d_bucket8) (void)hipFree(t->d_bucket8);
+  if (t->d_filt) (void)hipFree(t->d_filt);
   if (t->d_row) (void)hipFree(t->d_row);
   if (t->d_pay) (void)hipFree(t->d_pay);
   if (t->d_occ) (void)hipFree(t->d_occ);
@@ -547,6 +556,8 @@ int fill_probe_params(const ccj_table *t, const ccj_probe_args *a, ccj::ProbePar
   p.off = t->d_off;
   p.bucket = reinterpret_cast<const longlong2 *>(t->d_bucket);
   p.bucket8 = ccj_tune_int("CCJ_BUCKET8", 1) ? t->d_bucket8 : nullptr;
+  p.filt = t->d_filt;
+  p.filt_wb = t->info.kind == CCJ_TABLE_CHAIN ? ccj::slot_plan(t->info.size, CCJ_TABLE_CHAIN).window_bits : 0u;
   p.mask = (uint32_t)(t->info.size - 1);
   p.keys = a->keys;
   p.sel = a->sel;

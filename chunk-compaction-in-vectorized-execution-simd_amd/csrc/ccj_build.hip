@@ -89,6 +89,20 @@ __global__ __launch_bounds__(256) void chain_records(const uint32_t *off, const 
   if ((threadIdx.x & 63u) == 0 && best) atomicMax(longest, best);
 }
 
+// The bucket filter (probe_chain_filt): 2 bits per bucket, 16 buckets per word.
+__global__ void chain_filter(const uint32_t *off, const int64_t *chain, uint64_t words, uint32_t *filt) {
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < words; w += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t v = 0;
+    for (uint32_t i = 0; i < 16; ++i) {
+      const uint64_t b = w * 16 + i;
+      const uint32_t len = off[b + 1] - off[b];
+      const uint32_t code = len == 0 ? 0u : len == 1 ? 1u + (uint32_t)((murmurhash64((uint64_t)chain[off[b]]) >> 40) & 1u) : 3u;
+      v |= code << (2 * i);
+    }
+    filt[w] = v;
+  }
+}
+
 // Step 6: *flag = 1 if some run of equal keys in the sorted column is at least L long.
 __global__ void has_run(const int64_t *sorted, uint64_t n, uint64_t L, uint32_t *flag) {
   if (L < 2 || L > n) return;
@@ -176,6 +190,19 @@ int max_multiplicity(const int64_t *d_keys, uint64_t n, hipStream_t s, uint64_t 
 
 }  // namespace
 
+hipError_t build_chain_filter(ccj_table *t, hipStream_t s) {
+  const uint64_t size = t->info.size;
+  if (size < 128 || t->d_filt) return hipSuccess;  // (the filter walk needs >= 8 partitions of >= 16 buckets)
+  const uint64_t words = size / 16;
+  hipError_t e = hipMalloc((void **)&t->d_filt, words * 4);
+  if (e != hipSuccess) {
+    t->d_filt = nullptr;
+    return e;
+  }
+  hipLaunchKernelGGL(chain_filter, dim3(grid_of(words, 256)), dim3(256), 0, s, t->d_off, t->d_table, words, t->d_filt);
+  return hipGetLastError();
+}
+
 int build_chain_device(const int64_t *d_keys, uint64_t n, hipStream_t s, uint64_t known_dup, ccj_table **out) {
   uint64_t size = 1;
   while (size < 2 * n) size *= 2;  // chaining_ht.cpp:5-6
@@ -253,6 +280,14 @@ int build_chain_device(const int64_t *d_keys, uint64_t n, hipStream_t s, uint64_
   t->info.d_table = t->d_table;
   t->info.d_bucket_off = t->d_off;
   (void)hipGetDevice(&t->device);
+  hipError_t fe = build_chain_filter(t.get(), s);
+  if (fe == hipSuccess) fe = hipStreamSynchronize(s);
+  if (fe != hipSuccess) {
+    for (void *q : {(void *)t->d_table, (void *)t->d_off, (void *)t->d_row, (void *)t->d_bucket, (void *)t->d_bucket8,
+                    (void *)t->d_filt})
+      if (q) (void)hipFree(q);
+    return hip_err(fe, "bucket filter");
+  }
   *out = t.release();
   return CCJ_OK;
 }

@@ -17,6 +17,9 @@ struct ccj_table {
   // (bucket_fp) of the first two chain keys, len < 2^8 (absent when a chain is longer: the 16-byte
   // records serve alone)
   uint64_t *d_bucket8 = nullptr;
+  // chain: 2 bits per bucket, 16 buckets per word — 0 empty, 1 / 2 a one-key chain whose key has hash
+  // bit 40 = 0 / 1, 3 a longer chain (probe_chain_filt's LDS filter); absent for tables of < 128 buckets
+  uint32_t *d_filt = nullptr;
   uint32_t *d_row = nullptr;    // table position -> build tuple index (LP: kNoRow for empty slots)
   uint64_t positions = 0;       // allocated positions (LP slots / chain keys, padded)
   int64_t *d_pay = nullptr;     // position-major payload rows [positions][n_pay]
@@ -136,6 +139,11 @@ struct ProbeParams {
   // stops at its match instead of walking to the end of its run (same matches and multiplicities)
   uint32_t first_match;
   uint32_t key_aux;  // tuning build (CCJ_KEY_AUX): probe_walk2's key loads as buffer loads, policy key_aux - 1
+  // chaining, partitioned walk: the table's bucket filter (2 bits per bucket, 16 per word;
+  // ccj_build.hip) and the partitions' window bits — probe_chain_filt holds one partition's filter
+  // in LDS; NULL: probe_chain_win
+  const uint32_t *filt;
+  uint32_t filt_wb;
 };
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 constexpr uint32_t kEmitWave = 0xFFFFFFFFu;
@@ -173,6 +181,8 @@ hipError_t launch_lp_runs(const int64_t *slots, uint64_t n_slots, uint32_t *seg_
 // The chaining table built on the device (ccj_build.hip): stable bucket sort -> CSR, row map,
 // 16- and 8-byte bucket records, longest chain; known_dup = 0: max_dup computed from the keys.
 int build_chain_device(const int64_t *d_keys, uint64_t n, hipStream_t s, uint64_t known_dup, ccj_table **out);
+// The bucket filter of a finished chaining table (t->d_filt), from its offsets and chain keys.
+hipError_t build_chain_filter(ccj_table *t, hipStream_t s);
 constexpr uint64_t kRunSegment = 4096;
 // C3 probe stream; zipf: device copy of the rank table (kZipfBuckets + 1 entries, zipf_table()).
 hipError_t launch_gen_c3(int64_t *out, uint64_t n, uint64_t seed, uint64_t first_row, uint64_t n_build, uint64_t cf,

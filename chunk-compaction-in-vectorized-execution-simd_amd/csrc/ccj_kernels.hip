@@ -1245,6 +1245,7 @@ __global__ __launch_bounds__(kFlatThreads) void probe_chain_win(ProbeParams p) {
     const uint64_t n8 = (p.swz_chunks ? p.swz_chunks : p.n_chunks) & ~7ull;
     if (c < n8) c = (c & 7) * (n8 >> 3) + (c >> 3);
   }
+  c += p.chunk0;  // (the filter walk's overflow-area pass: chunks from chunk0 on)
   const uint64_t base = c * p.chunk;
   const uint32_t phys = flat_phys(p, base);
   const uint64_t obase = c * p.cap;
@@ -1390,6 +1391,191 @@ __global__ __launch_bounds__(kFlatThreads) void probe_chain_win(ProbeParams p) {
   if (p.status && (overflow || total > p.cap)) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
 }
 
+// probe_chain_filt: the chaining walk of the bucket-partitioned column with each partition's
+// bucket filter in LDS (VERDICT r3 task 5).  At C3 90 % of the rows miss, yet
+// probe_chain_win spends one L2 request per row on its bucket record (1.11 requests per row, bound
+// by the CU's ~90 reads in flight).  The filter holds 2 bits per bucket (ccj_build.hip
+// chain_filter): 0 = empty bucket, 1 / 2 = a one-key chain whose key has hash bit 40 = 0 / 1,
+// 3 = a longer chain; 2^18 buckets of a partition are 64 KiB.  A row needs the L2 only when its
+// code is 3 or equals 1 + its own hash bit 40 (C3: a miss passes with p ~ 0.09 + 0.30 / 2).
+// Persistent: one 1024-thread workgroup per CU; XCD x walks partitions [x P / 8, (x + 1) P / 8) in
+// order, all its workgroups on the same partition (its records and chains sit in the XCD's L2),
+// each loading the partition's filter into LDS once.  Work unit = a quarter chunk (512 rows); a
+// wave stages the unit's keys in registers, hashes and filters them, queues the passing rows (key,
+// row) in its LDS queue, then reads their 8-byte bucket records (rec8_first skips nodes whose 12-bit
+// fingerprint differs) and, where a node can still match, the 2-key windows of the chain.  Matches
+// of a chunk are appended to its output region through out_count[c] (zeroed by the launcher) with
+// one atomic per wave step: the order inside a chunk is free here (L1 / L2 parity), as in every
+// partitioned walk.  Chunks of the overflow area (key skew) are walked by probe_chain_win.
+constexpr int kFiltThreads = 1024;
+constexpr int kFiltWaves = kFiltThreads / kWave;
+constexpr uint32_t kFiltMaxWords = (1u << 18) / 16;  // 2 bits per bucket, windows <= 2^18 buckets
+__device__ __forceinline__ uint32_t filt_code_of(uint64_t h) { return 1u + (uint32_t)((h >> 40) & 1u); }
+
+// WORDS = false: matches appended to each chunk's output (the partitioned probe); WORDS = true: every
+// row's Next-round word at its position (the ordered probe, chain_words' output: the filter gives an
+// empty bucket's 0 rounds and a one-key chain's miss — 1 round, no match — without any read).
+// UNIT: rows per work unit (512: LDS = 64 KiB filter + 80 KiB queues; the words need 256 for their
+// per-wave word image).
+template <bool WORDS, uint32_t UNIT>
+__global__ __launch_bounds__(kFiltThreads) void probe_chain_filt(ProbeParams p) {
+  constexpr uint32_t kJ = UNIT / kWave;  // rows per lane and unit
+  __shared__ uint32_t s_f[kFiltMaxWords];          // the partition's filter (64 KiB)
+  __shared__ int64_t s_qk[kFiltWaves][UNIT];       // per wave: the passing rows' keys
+  __shared__ uint16_t s_qr[kFiltWaves][UNIT];      // and their rows in the unit
+  __shared__ uint32_t s_w[WORDS ? kFiltWaves : 1][WORDS ? UNIT : 1];  // WORDS: the unit's round words
+  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  const uint32_t x = blockIdx.x & 7u, k = blockIdx.x >> 3, K = gridDim.x >> 3;
+  const uint32_t P = p.seg_parts;
+  const uint32_t spc = (uint32_t)(p.seg_cap / p.chunk);  // chunks per segment
+  const uint32_t upc = p.chunk / UNIT;                   // units per chunk (chunk: a multiple of UNIT)
+  const uint32_t units = 8u * spc * upc;                 // units per partition
+  const uint32_t wb = p.filt_wb;
+  const uint32_t fwords = (1u << wb) / 16u;
+  const uint32_t wmask = (1u << wb) - 1u;
+  const bool rec8 = p.bucket8 != nullptr;
+  int64_t *qk = s_qk[wave];
+  uint16_t *qr = s_qr[wave];
+  uint32_t *sw = s_w[WORDS ? wave : 0];
+  for (uint32_t d = x * P / 8; d < (x + 1) * P / 8; ++d) {
+    __syncthreads();  // the previous partition's filter is no longer read
+    for (uint32_t w = tid * 4; w < fwords; w += kFiltThreads * 4)
+      *reinterpret_cast<u32x4 *>(&s_f[w]) = *reinterpret_cast<const u32x4 *>(p.filt + (uint64_t)d * fwords + w);
+    __syncthreads();
+    // this workgroup's units of partition d: u = k + K * (wave + kFiltWaves * i)
+    for (uint32_t u = k + K * wave; u < units; u += K * kFiltWaves) {
+      const uint32_t g = u / (spc * upc), r = u - g * spc * upc;
+      const uint64_t c = ((uint64_t)(d * 8 + g) * p.seg_cap) / p.chunk + r / upc;
+      const uint64_t base = c * p.chunk;
+      const uint32_t phys = flat_phys(p, base);
+      const uint32_t u0 = (r % upc) * UNIT;  // the unit's first row in its chunk
+      if (u0 >= phys) continue;
+      const uint32_t uend = phys - u0 < UNIT ? phys : u0 + UNIT;
+      int64_t kk[kJ];
+#pragma unroll
+      for (int j = 0; j < (int)kJ; ++j) {
+        const uint32_t i = u0 + (uint32_t)j * kWave + lane;
+        kk[j] = __builtin_nontemporal_load(p.keys + base + (i < uend ? i : u0));
+      }
+      // filter: queue the rows that may match (the previous unit's queue reads are done: LDS
+      // operations of one wave complete in order, and the fences keep the compiler's order)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      uint32_t qn = 0;
+#pragma unroll
+      for (int j = 0; j < (int)kJ; ++j) {
+        const uint32_t li = (uint32_t)j * kWave + lane, i = u0 + li;
+        const uint64_t h = murmurhash64((uint64_t)kk[j]);
+        const uint32_t bl = (uint32_t)h & wmask;
+        const uint32_t code = (s_f[bl >> 4] >> ((bl & 15u) * 2u)) & 3u;
+        const bool pass = i < uend && (code == 3u || code == filt_code_of(h));
+        const uint64_t bm = __ballot(pass);
+        if (pass) {
+          const uint32_t q = qn + lane_prefix(bm);
+          qk[q] = kk[j];
+          qr[q] = (uint16_t)li;
+        } else if (WORDS) {
+          sw[li] = code == 0u ? 0u : 1u << kMmRounds;  // no rounds, or a one-key chain that misses
+        }
+        qn += (uint32_t)__popcll(bm);
+      }
+      // the queue written by other lanes of this wave is read below
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // lookups: entry e = t * 64 + lane; records of up to 4 entries per lane in flight
+      const uint64_t obase = c * p.cap;
+      for (uint32_t t0 = 0; t0 * kWave < qn; t0 += 4) {
+        uint64_t rec[4];
+        int64_t key[4];
+        uint32_t row[4], kfp[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const uint32_t e = (t0 + (uint32_t)t) * kWave + lane;
+          const uint32_t ee = e < qn ? e : 0u;
+          key[t] = qk[ee];
+          row[t] = qr[ee];
+          const uint64_t h = murmurhash64((uint64_t)key[t]);
+          const uint32_t b = e < qn ? (uint32_t)h & p.mask : 0u;
+          rec[t] = rec8 ? p.bucket8[b] : (uint64_t)p.bucket[b].x;
+          kfp[t] = bucket_fp(h);
+        }
+        uint32_t nh[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const uint32_t e = (t0 + (uint32_t)t) * kWave + lane;
+          nh[t] = 0;
+          if (e >= qn) continue;
+          const uint32_t st = (uint32_t)rec[t];
+          const uint32_t len = rec8 ? (uint32_t)(rec[t] >> 32) & 0xFFu : (uint32_t)(rec[t] >> 32);
+          uint32_t cur = rec8 ? rec8_first(rec[t], kfp[t]) : st;  // nodes before it cannot hold the key
+          const uint32_t lim = st + len;
+          uint32_t mm = 0;
+          while (cur < lim) {  // the chain from the first node that can hold the key
+            const uint32_t blk = cur & ~1u;
+            const longlong2 v = *reinterpret_cast<const longlong2 *>(p.table + blk);
+            const uint32_t r0 = blk - st;  // node blk's round (chaining_ht.cpp:88-99: one node per Next)
+            if (cur == blk && v.x == key[t]) {
+              ++nh[t];
+              if (r0 < 32u) mm |= 1u << r0;
+            }
+            if (blk + 1u < lim && v.y == key[t]) {
+              ++nh[t];
+              if (r0 + 1u < 32u) mm |= 1u << (r0 + 1u);
+            }
+            cur = blk + 2u;
+          }
+          if (WORDS) sw[row[t]] = len <= kMmRounds ? (mm & ((1u << kMmRounds) - 1u)) | len << kMmRounds : kMmLong | len;
+        }
+        if (!WORDS) {  // append the matches: one atomic per wave step on the chunk's count
+          const uint32_t mine = nh[0] + nh[1] + nh[2] + nh[3];
+          const uint32_t incl = wave_incl_scan(mine);
+          const uint32_t tot = (uint32_t)__shfl((int)incl, kWave - 1);
+          if (tot) {
+            uint32_t ob = 0;
+            if (lane == 0) ob = atomicAdd(p.out_count + c, tot);
+            ob = (uint32_t)__shfl((int)ob, 0) + incl - mine;
+            bool over = false;
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+              for (uint32_t m = 0; m < nh[t]; ++m, ++ob) {
+                if (ob < p.cap) {
+                  p.out_sel[obase + ob] = u0 + row[t];
+                  if (p.out_payload) p.out_payload[obase + ob] = key[t];
+                } else {
+                  over = true;
+                }
+              }
+            if (over && p.status) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
+          }
+        }
+      }
+      if (WORDS) {  // the unit's words, coalesced at their positions
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int j = 0; j < (int)kJ; ++j) {
+          const uint32_t li = (uint32_t)j * kWave + lane, i = u0 + li;
+          if (i < uend) {
+            if (p.w16) __builtin_nontemporal_store(round_word16(sw[li]), (uint16_t *)p.out_w + base + i);
+            else __builtin_nontemporal_store(sw[li], p.out_w + base + i);
+          }
+        }
+      }
+    }
+  }
+}
+
+// The filter walks apply to the fixed-capacity split's segments of >= 8 partitions of <= 2^18
+// buckets (one XCD's range each), chunks a multiple of the work unit, no rounds asked for (partitioned
+// probe); the overflow area's chunks (key skew) go to the per-chunk walks.
+__device__ __host__ __forceinline__ bool chain_filt_applies(const ProbeParams &p, uint32_t unit) {
+  const uint32_t P = p.seg_parts;
+  return p.filt && p.seg_count && p.ovf_base && p.filt_wb <= 18 && p.filt_wb >= 4 && P >= 8 && P % 8 == 0 &&
+         p.chunk % unit == 0 && p.seg_cap % p.chunk == 0;
+}
+
 // Ordered probe of a chaining table (ccj_probe_ordered), step 2: probe_chain_win's walk of the
 // bucket-partitioned column, leaving each row's Next-round word at its position instead of emitting
 // matches.  The reference walks a row's whole chain, one node per Next round
@@ -1409,6 +1595,7 @@ __global__ __launch_bounds__(kFlatThreads) void chain_words(ProbeParams p) {
     const uint64_t n8 = (p.swz_chunks ? p.swz_chunks : p.n_chunks) & ~7ull;
     if (c < n8) c = (c & 7) * (n8 >> 3) + (c >> 3);
   }
+  c += p.chunk0;  // (the filter walk's overflow-area pass: chunks from chunk0 on)
   const uint64_t base = c * p.chunk;
   const uint32_t phys = flat_phys(p, base);
   stage_keys(s_key, p.keys + base, phys, tid);
@@ -1941,6 +2128,21 @@ __device__ __forceinline__ void dma16(const void *g, uint32_t lds) {
                : "memory");
 }
 constexpr uint32_t kRingSlot = 2 * 1024;  // one batch: 64 windows of 32 B, two DMA halves
+// The walks move each row's window start to the two lanes that DMA its halves with DPP quad-perms
+// (a0: lanes 2q and 2q + 1 get lane 2q's address, a1: lane 2q + 1's), and clamp the result into the
+// table so that a DMA can never leave it.  The clamp alone would turn a DPP that read a switched-off
+// lane (round 3: a structurised loop did) into silently wrong windows, so the tuning build checks
+// every move against the partner lanes' addresses fetched by ds_bpermute and raises
+// CCJ_FLAG_INTERNAL in args->status on a mismatch (tests/test_probe_gpu.py runs the walks there).
+__device__ __forceinline__ void dpp_check(const ProbeParams &p, uint32_t a, uint32_t a0, uint32_t a1, uint32_t lane) {
+#ifdef CCJ_TUNING
+  const uint32_t e0 = (uint32_t)__shfl((int)a, (int)(lane & ~1u));
+  const uint32_t e1 = (uint32_t)__shfl((int)a, (int)(lane | 1u));
+  if ((a0 != e0 || a1 != e1) && p.status) atomicOr(p.status, CCJ_FLAG_INTERNAL);
+#else
+  (void)p, (void)a, (void)a0, (void)a1, (void)lane;
+#endif
+}
 // Window prefetch (p.pf_dist): chunk c (its XCD's order, partitioned layout) touches the table lines
 // of slice (c + pf_dist) mod K of partition (c + pf_dist) / K, K = chunks per partition, so that
 // the next window is in L2 before its first chunk starts.  One LDS-DMA of wave 0 into `lds` (1 KiB
@@ -2113,6 +2315,7 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk1(ProbeParams p) {
     if (CCJ_ABLATED(p.ablate, 0x200u)) a &= 0x1FFFu;  // (timing only: windows from the first 64 KiB)
     uint32_t a0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, 0xA0, 0xF, 0xF, false);  // quad_perm 0,0,2,2
     uint32_t a1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, 0xF5, 0xF, 0xF, false);  // quad_perm 1,1,3,3
+    dpp_check(p, a, a0, a1, lane);
     a0 = a0 < last_start ? a0 : last_start;  // (a guard, as in probe_walk2: the DMA stays in the table)
     a1 = a1 < last_start ? a1 : last_start;
     const uint32_t slot = ring_lds + (uint32_t)b * kRingSlot;
@@ -2227,6 +2430,7 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk1(ProbeParams p) {
 // then the same emits.
 // The stage's key loads as buffer loads of cache policy AUX (tuning build: CCJ_KEY_AUX A/B of how
 // the streamed key lines share the L2 with the table window).
+#ifdef CCJ_TUNING
 template <int AUX, int KJ>
 __device__ __forceinline__ void stage_keys_aux(const int64_t *keys, uint32_t phys, uint32_t w0, uint32_t wend,
                                                uint32_t lane, int64_t (&k)[KJ]) {
@@ -2241,6 +2445,7 @@ __device__ __forceinline__ void stage_keys_aux(const int64_t *keys, uint32_t phy
   for (int j = 0; j < KJ; ++j)
     if (w0 + (uint32_t)j * kWave + lane >= wend) k[j] = 0;
 }
+#endif
 template <bool POS, int NB = 1>
 __global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
   constexpr int NW = 4;
@@ -2260,12 +2465,15 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
   // LDS for phase B and the emit's compaction
   int64_t k[kJ];
   uint32_t h[kJ];
+#ifdef CCJ_TUNING
   if (p.key_aux == 0u) {
+#endif
 #pragma unroll
     for (int j = 0; j < kJ; ++j) {
       const uint32_t i = w0 + (uint32_t)j * kWave + lane;
       k[j] = i < wend ? __builtin_nontemporal_load(p.keys + base + i) : 0;
     }
+#ifdef CCJ_TUNING
   } else {  // (tuning build only: p.key_aux = 1 + the buffer loads' cache-policy bits)
     switch (p.key_aux - 1u) {
       case 1: stage_keys_aux<1>(p.keys + base, phys, w0, wend, lane, k); break;
@@ -2278,6 +2486,7 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
       default: stage_keys_aux<0>(p.keys + base, phys, w0, wend, lane, k); break;
     }
   }
+#endif
 #pragma unroll
   for (int j = 0; j < kJ; ++j) {
     sm.key[w0 + (uint32_t)j * kWave + lane] = k[j];
@@ -2304,6 +2513,7 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
   auto issue = [&](uint32_t a, uint32_t slot) {
     uint32_t a0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, 0xA0, 0xF, 0xF, false);  // quad_perm 0,0,2,2
     uint32_t a1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)a, 0xF5, 0xF, 0xF, false);  // quad_perm 1,1,3,3
+    dpp_check(p, a, a0, a1, lane);  // (tuning build: the DPP gave the partner lanes' own addresses)
     a0 = a0 < last_start ? a0 : last_start;  // (a guard: whatever a DPP returns, the DMA stays in the table)
     a1 = a1 < last_start ? a1 : last_start;
     dma16(p.table + a0 + half, ring_lds + slot * kRingSlot);
@@ -2702,6 +2912,22 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
   const uint64_t size = (uint64_t)p.mask + 1;
   if (kind != CCJ_TABLE_LP) {
     if (!p.bucket) return hipErrorInvalidValue;  // every chaining table carries bucket records
+    // the LDS bucket filter walk (probe_chain_filt) for the fixed-capacity split's segments, when the
+    // table has a filter, the partitions are at most 2^18 buckets and there are >= 8 of them (one
+    // XCD's range each), the chunk is a multiple of 512 rows and no rounds are asked for; the
+    // overflow area's chunks (key skew) go to probe_chain_win
+    if (chain_filt_applies(p, 512) && !p.out_rounds && ccj_tune_int("CCJ_CHAIN_FILT", 1)) {
+      hipError_t e = hipMemsetAsync(p.out_count, 0, p.n_chunks * sizeof(uint32_t), s);
+      if (e != hipSuccess) return e;
+      const uint32_t grid = std::max<uint32_t>(8u, stream_cus(s) / 8 * 8);
+      hipLaunchKernelGGL((probe_chain_filt<false, 512>), dim3(grid), dim3(kFiltThreads), 0, s, p);
+      ProbeParams q = p;  // the overflow area's chunks, in plain order
+      q.chunk0 = p.ovf_base / p.chunk;
+      q.xcd_swizzle = 0;
+      if (p.n_chunks > q.chunk0)
+        hipLaunchKernelGGL((probe_chain_win<3>), dim3((unsigned)(p.n_chunks - q.chunk0)), b, 0, s, q);
+      return hipGetLastError();
+    }
     hipLaunchKernelGGL((probe_chain_win<3>), g, b, 0, s, p);
     return hipGetLastError();
   }
@@ -2884,6 +3110,16 @@ hipError_t launch_ordered_walk(int kind, const ProbeParams &p, hipStream_t s) {
   if (p.n_chunks == 0) return hipSuccess;
   if (kind == CCJ_TABLE_CHAIN) {
     if (!p.bucket) return hipErrorInvalidValue;  // every chaining table carries bucket records
+    if (chain_filt_applies(p, 256) && ccj_tune_int("CCJ_CHAIN_FILT", 1)) {  // the bucket filter in LDS
+      const uint32_t grid = std::max<uint32_t>(8u, stream_cus(s) / 8 * 8);
+      hipLaunchKernelGGL((probe_chain_filt<true, 256>), dim3(grid), dim3(kFiltThreads), 0, s, p);
+      ProbeParams q = p;  // the overflow area's chunks, in plain order
+      q.chunk0 = p.ovf_base / p.chunk;
+      q.xcd_swizzle = 0;
+      if (p.n_chunks > q.chunk0)
+        hipLaunchKernelGGL((chain_words<3>), dim3((unsigned)(p.n_chunks - q.chunk0)), dim3(kFlatThreads), 0, s, q);
+      return hipGetLastError();
+    }
     hipLaunchKernelGGL((chain_words<3>), dim3((unsigned)p.n_chunks), dim3(kFlatThreads), 0, s, p);
   } else if (ccj_tune_int("CCJ_OWALK", 1) == 1)
     hipLaunchKernelGGL((probe_walk1<1, true>), dim3((unsigned)p.n_chunks), dim3(kFlatThreads), 0, s, p);

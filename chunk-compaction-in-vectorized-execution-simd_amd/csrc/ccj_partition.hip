@@ -527,7 +527,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
                                                                 int64_t *out_k, uint32_t *out_r, uint32_t *status,
                                                                 const uint32_t *counts, uint32_t chunk, uint2 *runs,
                                                                 uint32_t *ovf_runs, uint32_t row_base, int64_t *sink_k,
-                                                                uint32_t *sink_r) {
+                                                                uint32_t *sink_r, uint32_t ablate) {
   constexpr uint32_t kTileKeys = (uint32_t)THREADS * PER;
   static_assert(MAXP <= THREADS, "one partition per thread in the scan");
   __shared__ int64_t s_k[kTileKeys];
@@ -556,7 +556,8 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
 #pragma unroll
     for (int it = 0; it < PER; ++it) {
       const uint32_t li = (uint32_t)it * THREADS + tid;
-      kk[it] = __builtin_nontemporal_load(keys + t0 + (li < tn ? li : 0u));
+      if CCJ_ABLATED(ablate, 0x20u) kk[it] = (int64_t)((t0 + li) * 0x9E3779B97F4A7C15ull >> 20);  // (timing: no key reads)
+      else kk[it] = __builtin_nontemporal_load(keys + t0 + (li < tn ? li : 0u));
     }
     if (COUNTS) {
       const uint64_t c0 = t0 / chunk, nc = (t0 + tn - 1) / chunk - c0 + 1;
@@ -575,6 +576,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
       const uint64_t oadj = s_oadj[d];
       const bool act = have_prev && q < p_tl && q < rc.w;
       const uint64_t dest = q < rc.z ? (rc.x | (uint64_t)rc.y << 32) + q : oadj + q;
+      if CCJ_ABLATED(ablate, 0x10u) continue;  // (timing: no stores)
       *(act ? out_k + dest : sink_k) = k;
       if constexpr (RUNS)  // the ordered probe: the row inside its tile, 16 bits
         *(act ? reinterpret_cast<uint16_t *>(out_r) + dest : reinterpret_cast<uint16_t *>(sink_r)) = (uint16_t)(si & 0xFFFFu);
@@ -606,7 +608,8 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
     uint32_t dr[PER];  // partition | rank in it << 10 (one register per key: no spills at 11 keys)
 #pragma unroll
     for (int it = 0; it < PER; ++it) {
-      const uint32_t d = (uint32_t)(murmurhash64((uint64_t)kc[it]) >> shift) & mask;
+      const uint32_t d = CCJ_ABLATED(ablate, 0x2000u) ? (uint32_t)((uint64_t)kc[it] >> shift) & mask  // (timing: no hash)
+                                                      : (uint32_t)(murmurhash64((uint64_t)kc[it]) >> shift) & mask;
       if constexpr (MAXP <= 64) {
         // few partitions (the owner split: one per rank): an LDS atomic per key would queue the
         // wave's 64 lanes on at most `parts` addresses (one address at N = 1).  Instead one ballot
@@ -718,7 +721,7 @@ static hipError_t launch_owner_split_small(const int64_t *keys, uint64_t n, uint
   uint32_t *sink_r = (uint32_t *)((char *)sink + kSplitSinkBytes / 16 * 8);
   hipLaunchKernelGGL((slot_split_pipe<false, kT, 64, kPer, false>), dim3((unsigned)grid), dim3(kT), 0, s, keys, n, shift, parts,
                      n_tiles, cur, sub_cap, (uint64_t)0, (uint64_t)0, out_keys, out_rows, status, nullptr, 0u, nullptr,
-                     nullptr, row_base, sink_k, sink_r);
+                     nullptr, row_base, sink_k, sink_r, 0u);
   return hipGetLastError();
 }
 
@@ -786,11 +789,11 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
     if (runs)                                                                                                       \
       hipLaunchKernelGGL((slot_split_pipe<C, kSplitThreads, MAXP, P, true>), dim3(grid), dim3(kSplitThreads), 0, s,  \
                          keys, n, shift, parts, n_tiles, cursors, cap, ovf_base, oc, out_keys, out_rows, status,     \
-                         counts, chunk, runs, ovf_runs, row_base, sink_k, sink_r);                                   \
+                         counts, chunk, runs, ovf_runs, row_base, sink_k, sink_r, ablate);                           \
     else                                                                                                            \
       hipLaunchKernelGGL((slot_split_pipe<C, kSplitThreads, MAXP, P, false>), dim3(grid), dim3(kSplitThreads), 0, s, \
                          keys, n, shift, parts, n_tiles, cursors, cap, ovf_base, oc, out_keys, out_rows, status,     \
-                         counts, chunk, runs, ovf_runs, row_base, sink_k, sink_r);                                   \
+                         counts, chunk, runs, ovf_runs, row_base, sink_k, sink_r, ablate);                           \
   } while (0)
     if (parts <= 64 && !runs && per == kSplitPer) {  // the owner split: ballot ranking (above)
       if (counts) CCJ_PIPE_LAUNCH(true, 64, kSplitPer);

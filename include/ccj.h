@@ -41,8 +41,10 @@ enum ccj_flag {
   CCJ_FLAG_CAP_OVERFLOW = 1u,   /* a chunk produced more than `cap` matches (extra matches dropped) */
   CCJ_FLAG_ROUND_OVERFLOW = 2u, /* a chunk took more than `max_rounds` rounds (counts not recorded) */
   CCJ_FLAG_BAD_INPUT = 4u,      /* count > chunk or a sel entry outside the chunk (rows skipped) */
-  CCJ_FLAG_PART_OVERFLOW = 8u   /* ccj_probe_partitioned: a fixed-capacity partition segment was full
+  CCJ_FLAG_PART_OVERFLOW = 8u,  /* ccj_probe_partitioned: a fixed-capacity partition segment was full
                                    (rows dropped): re-run with CCJ_PART_EXACT */
+  CCJ_FLAG_INTERNAL = 16u       /* an internal consistency check failed (raised by libccj_tuning.so's
+                                   checked walks only: a DPP address move disagreed with its lanes) */
 };
 
 enum ccj_table_kind {
@@ -125,6 +127,11 @@ typedef struct ccj_table_arrays {
   const int64_t *d_bucket16;
   const uint64_t *d_bucket8;
   uint64_t n_bucket8;
+  const uint32_t *d_bucket_filter; /* chaining: 2 bits per bucket, 16 per word (size / 16 words): 0
+                                      empty, 1 / 2 a one-key chain whose key has hash bit 40 = 0 / 1,
+                                      3 a longer chain — the partitioned walk's LDS filter; NULL
+                                      below 128 buckets */
+  uint64_t n_filter_words;
 } ccj_table_arrays;
 int ccj_table_get_arrays(const ccj_table *table, ccj_table_arrays *arrays);
 /* Attaches build-side payload columns (C5): d_payload is row-major int64

@@ -77,9 +77,16 @@ def _assert_same(host_t, dev_t):
     for k in ("table", "row", "off", "bucket16"):
         assert a[k].shape == b[k].shape, k
         assert np.array_equal(a[k], b[k]), (k, int(np.flatnonzero(a[k] != b[k])[0]))
-    assert (a["bucket8"] is None) == (b["bucket8"] is None)
-    if a["bucket8"] is not None:
-        assert np.array_equal(a["bucket8"], b["bucket8"])
+    for k in ("bucket8", "filter"):
+        assert (a[k] is None) == (b[k] is None), k
+        if a[k] is not None:
+            assert np.array_equal(a[k], b[k]), k
+    if a["filter"] is not None:  # the filter model: 0 empty, 1 / 2 one key (hash bit 40), 3 longer
+        ln = np.diff(a["off"].astype(np.int64))
+        bit = (_np_murmur(a["table"][a["off"][:-1].astype(np.int64) % len(a["table"])]) >> np.uint64(40)) & np.uint64(1)
+        code = np.where(ln == 0, 0, np.where(ln == 1, 1 + bit.astype(np.int64), 3)).astype(np.uint64)
+        words = (code.reshape(-1, 16) << (2 * np.arange(16, dtype=np.uint64))[None, :]).sum(axis=1)
+        assert np.array_equal(a["filter"].astype(np.uint64), words)
     return a
 
 

@@ -310,10 +310,16 @@ def test_device_build_reports_exact_max_dup(kind):
 
 @pytest.mark.parametrize("exact", [False, True])
 @pytest.mark.parametrize("n_build,cf,n_probe,rng", [(1 << 20, 1, 1 << 22, 1 << 21), (1 << 18, 3, 1 << 21, 1 << 19),
-                                                    (3000, 2, 40000, 9000)])
+                                                    (3000, 2, 40000, 9000), (1 << 22, 3, 3 << 21, 3 << 22),
+                                                    (1 << 21, 1, (1 << 22) + 4097, 10 << 21),
+                                                    (5 << 20, 2, 1 << 23, 5 << 20)])
 def test_partitioned_chaining_probe_l1_l2(n_build, cf, n_probe, rng, exact):
-    """Bucket-range-partitioned chaining probe (probe_chain_win: bucket record, then 2-key windows
-    of the CSR chain) — exact L1 + L2 against the membership answer, duplicates and misses included."""
+    """Bucket-range-partitioned chaining probe — exact L1 + L2 against the membership answer,
+    duplicates and misses included.  Tables of >= 8 partitions take probe_chain_filt (the
+    partition's 2-bit bucket filter in LDS, quarter-chunk work units, the overflow area by
+    probe_chain_win); smaller ones and the exact split probe_chain_win alone (bucket record, then
+    2-key windows of the CSR chain).  Shapes: 8 / 32 / 64 partitions, 90 % misses, ragged last
+    chunk, cf 2 / 3."""
     table = ccj.Table.reference(ccj.CHAIN, n_build, cf, ccj.LAYOUT_DEVICE)
     keys = ccj.gen_uniform_keys(n_probe, 23, rng)
     out = table.probe_partitioned(keys, 2048, exact=exact)
@@ -323,15 +329,18 @@ def test_partitioned_chaining_probe_l1_l2(n_build, cf, n_probe, rng, exact):
     assert (m, l2) == O.count_uniform(23, 0, n_probe, rng, n_build, cf)
 
 
-def test_partitioned_chaining_c3_skew():
-    """C3's Zipf-skewed hits overflow the fixed split (hot keys pile into one partition); the exact
-    split and the chain walk still give the exact answer."""
-    n_build, n_probe = 1 << 20, 1 << 22
+@pytest.mark.parametrize("n_build,n_probe", [(1 << 20, 1 << 22), (1 << 23, 1 << 24)])
+def test_partitioned_chaining_c3_skew(n_build, n_probe):
+    """C3's Zipf-skewed hits overflow the fixed split (hot keys pile into one partition's segments
+    and then the shared overflow area, which probe_chain_win walks beside the filter walk); the
+    exact split and the chain walks still give the exact answer."""
     table = ccj.Table.reference(ccj.CHAIN, n_build, 1, ccj.LAYOUT_DEVICE)
     keys = ccj.gen_c3_keys(n_probe, 42, n_build, 1)
     out = table.probe_partitioned(keys, 2048)  # retries with the exact split on overflow
     torch.cuda.synchronize()
     assert int(out["status"].item()) == 0
+    if n_build >= 1 << 23:  # 64 partitions: the hot keys spill into the overflow area, which holds them
+        assert not out.get("exact_retry")
     m, l2 = ccj.result_checksum(out, 2048, row_map=out["row_map"].to(torch.int64))
     assert (m, l2) == O.count_c3(42, 0, n_probe, n_build, 1)
 
