@@ -300,6 +300,7 @@ def bench_c3(args, dev, stream):
     stream.synchronize()
     log(f"[setup c3] {table.size} buckets, max chain {table.max_rounds}: {time.perf_counter() - t0:.1f} s")
     comp = None
+    comp_in = {}  # partitioned: the probe outputs plus one Next result per chunk, for the compactor
 
     def step(ev=None, pe=None):
         nonlocal comp
@@ -312,8 +313,8 @@ def bench_c3(args, dev, stream):
             # overflow area; status is checked after the timed region (no host sync inside it)
             table.probe_partitioned(keys, chunk, out=out, part=part, stream=stream, retry=False)
             with torch.cuda.stream(stream):  # partition order has no Next boundaries: one result per chunk
-                out["rounds"] = (out["count"] > 0).to(torch.int32)
-                out["round_counts"] = out["count"]
+                # (in the compactor's view only: the probe itself is asked for no rounds)
+                comp_in.update(out, rounds=(out["count"] > 0).to(torch.int32), round_counts=out["count"])
         elif args.path == "ordered":  # L3 through the bucket-partitioned layout (status read after timing)
             table.probe_ordered(keys, chunk, out=out, ws=ws_o, stream=stream, retry=False)
         else:
@@ -322,7 +323,8 @@ def bench_c3(args, dev, stream):
             ev[1].record(stream)
         if pe:
             ccj.PhaseEvents.disarm()
-        comp = ccj.compact(out, chunk, cols=[pkeys if part_mode else keys], rows=True, stream=stream)
+        comp = ccj.compact(comp_in if part_mode else out, chunk, cols=[pkeys if part_mode else keys], rows=True,
+                           stream=stream)
         if ev:
             ev[2].record(stream)
 

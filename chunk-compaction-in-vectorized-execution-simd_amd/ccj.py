@@ -328,8 +328,7 @@ class Table:
         torch.cuda.synchronize()
 
         def get(ptr, n, dt):
-            n_i64 = (n * np.dtype(dt).itemsize + 7) // 8
-            return _d2h_i64(ptr, n_i64).view(np.uint8)[:n * np.dtype(dt).itemsize].view(dt)
+            return _d2h_bytes(ptr, n * np.dtype(dt).itemsize).view(dt)
 
         out = dict(table=get(a.d_table, a.positions, np.int64), row=get(a.d_row, a.positions, np.uint32))
         if self.kind == CHAIN:
@@ -714,6 +713,18 @@ def _hip():
         _HIP.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
         _HIP.hipEventDestroy.argtypes = [C.c_void_p]
     return _HIP
+
+
+def _d2h_bytes(ptr, nbytes):
+    """Copy nbytes from a raw device pointer the library owns (hipMemcpy; caller synchronised)."""
+    import numpy as np
+    out = np.empty(nbytes, np.uint8)
+    if nbytes == 0:
+        return out
+    rc = _hip().hipMemcpy(out.ctypes.data_as(C.c_void_p), C.c_void_p(ptr), nbytes, 2)  # hipMemcpyDeviceToHost
+    if rc != 0:
+        raise CCJError(f"hipMemcpy failed ({rc})")
+    return out
 
 
 def _d2h_i64(ptr, n):

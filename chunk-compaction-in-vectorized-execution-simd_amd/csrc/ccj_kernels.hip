@@ -1407,164 +1407,176 @@ __global__ __launch_bounds__(kFlatThreads) void probe_chain_win(ProbeParams p) {
 // of a chunk are appended to its output region through out_count[c] (zeroed by the launcher) with
 // one atomic per wave step: the order inside a chunk is free here (L1 / L2 parity), as in every
 // partitioned walk.  Chunks of the overflow area (key skew) are walked by probe_chain_win.
-constexpr int kFiltThreads = 1024;
-constexpr int kFiltWaves = kFiltThreads / kWave;
+// match walk: 768 threads, two workgroups per CU (64 KiB of LDS each): 24 waves, <= 80 VGPRs; the
+// round-word walk needs more registers: 1024 threads, one workgroup per CU
+constexpr int kFiltThreads = 768, kFiltWordThreads = 1024;
+constexpr uint32_t kFiltUnit = 256;                  // rows per work unit (4 per lane: <= 64 VGPRs, 32 waves per CU)
 constexpr uint32_t kFiltMaxWords = (1u << 18) / 16;  // 2 bits per bucket, windows <= 2^18 buckets
 __device__ __forceinline__ uint32_t filt_code_of(uint64_t h) { return 1u + (uint32_t)((h >> 40) & 1u); }
 
 // WORDS = false: matches appended to each chunk's output (the partitioned probe); WORDS = true: every
 // row's Next-round word at its position (the ordered probe, chain_words' output: the filter gives an
 // empty bucket's 0 rounds and a one-key chain's miss — 1 round, no match — without any read).
-// UNIT: rows per work unit (512: LDS = 64 KiB filter + 80 KiB queues; the words need 256 for their
-// per-wave word image).
-template <bool WORDS, uint32_t UNIT>
-__global__ __launch_bounds__(kFiltThreads) void probe_chain_filt(ProbeParams p) {
-  constexpr uint32_t kJ = UNIT / kWave;  // rows per lane and unit
-  __shared__ uint32_t s_f[kFiltMaxWords];          // the partition's filter (64 KiB)
-  __shared__ int64_t s_qk[kFiltWaves][UNIT];       // per wave: the passing rows' keys
-  __shared__ uint16_t s_qr[kFiltWaves][UNIT];      // and their rows in the unit
-  __shared__ uint32_t s_w[WORDS ? kFiltWaves : 1][WORDS ? UNIT : 1];  // WORDS: the unit's round words
+// Each lane keeps its unit rows (4) in registers: no queue, so the workgroup's LDS is the filter
+// alone (64 KiB) and two workgroups share a CU (24 waves).  Every memory step of a unit is one batch
+// for all its rows, issued unconditionally (a row that needs no read loads the partition's first
+// record pair / the chain array's first pair: one line shared by every such lane, so an instruction
+// costs at most one extra L2 request): the rows' bucket records, then rounds of 2-key chain windows
+// while some row's chain can still hold its key.  The next unit's keys are loaded right after this
+// unit's records are issued, so their HBM latency overlaps the record and chain round trips.
+template <bool WORDS, int NT>
+__device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *s_f) {
+  constexpr uint32_t kJ = kFiltUnit / kWave;  // rows per lane and unit
+  constexpr uint32_t kFiltWaves = NT / kWave;
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   const uint32_t x = blockIdx.x & 7u, k = blockIdx.x >> 3, K = gridDim.x >> 3;
   const uint32_t P = p.seg_parts;
   const uint32_t spc = (uint32_t)(p.seg_cap / p.chunk);  // chunks per segment
-  const uint32_t upc = p.chunk / UNIT;                   // units per chunk (chunk: a multiple of UNIT)
+  const uint32_t upc = p.chunk / kFiltUnit;              // units per chunk (chunk: a multiple of kFiltUnit)
   const uint32_t units = 8u * spc * upc;                 // units per partition
   const uint32_t wb = p.filt_wb;
   const uint32_t fwords = (1u << wb) / 16u;
   const uint32_t wmask = (1u << wb) - 1u;
   const bool rec8 = p.bucket8 != nullptr;
-  int64_t *qk = s_qk[wave];
-  uint16_t *qr = s_qr[wave];
-  uint32_t *sw = s_w[WORDS ? wave : 0];
+  const uint32_t stride = K * kFiltWaves;
   for (uint32_t d = x * P / 8; d < (x + 1) * P / 8; ++d) {
     __syncthreads();  // the previous partition's filter is no longer read
-    for (uint32_t w = tid * 4; w < fwords; w += kFiltThreads * 4)
+    for (uint32_t w = tid * 4; w < fwords; w += NT * 4)
       *reinterpret_cast<u32x4 *>(&s_f[w]) = *reinterpret_cast<const u32x4 *>(p.filt + (uint64_t)d * fwords + w);
     __syncthreads();
-    // this workgroup's units of partition d: u = k + K * (wave + kFiltWaves * i)
-    for (uint32_t u = k + K * wave; u < units; u += K * kFiltWaves) {
+    const uint32_t b0 = (d << wb) & p.mask & ~1u;  // the partition's first bucket pair (idle rows read it)
+    // unit u of partition d: chunk c, rows [u0, uend) of it (uend <= u0: nothing live)
+    auto unit = [&](uint32_t u, uint64_t &c, uint32_t &u0, uint32_t &uend) {
       const uint32_t g = u / (spc * upc), r = u - g * spc * upc;
-      const uint64_t c = ((uint64_t)(d * 8 + g) * p.seg_cap) / p.chunk + r / upc;
-      const uint64_t base = c * p.chunk;
-      const uint32_t phys = flat_phys(p, base);
-      const uint32_t u0 = (r % upc) * UNIT;  // the unit's first row in its chunk
-      if (u0 >= phys) continue;
-      const uint32_t uend = phys - u0 < UNIT ? phys : u0 + UNIT;
-      int64_t kk[kJ];
+      c = ((uint64_t)(d * 8 + g) * p.seg_cap) / p.chunk + r / upc;
+      const uint32_t phys = u < units ? flat_phys(p, c * p.chunk) : 0u;
+      u0 = (r % upc) * kFiltUnit;
+      uend = phys <= u0 ? u0 : (phys - u0 < kFiltUnit ? phys : u0 + kFiltUnit);
+    };
+    auto load_keys = [&](uint64_t c, uint32_t u0, uint32_t uend, int64_t(&kk)[kJ]) {
 #pragma unroll
       for (int j = 0; j < (int)kJ; ++j) {
         const uint32_t i = u0 + (uint32_t)j * kWave + lane;
-        kk[j] = __builtin_nontemporal_load(p.keys + base + (i < uend ? i : u0));
+        kk[j] = __builtin_nontemporal_load(p.keys + c * p.chunk + (i < uend ? i : u0));
       }
-      // filter: queue the rows that may match (the previous unit's queue reads are done: LDS
-      // operations of one wave complete in order, and the fences keep the compiler's order)
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      uint32_t qn = 0;
+    };
+    uint32_t u = k + K * wave;
+    uint64_t c = 0;
+    uint32_t u0 = 0, uend = 0;
+    unit(u, c, u0, uend);
+    int64_t kk[kJ], kn[kJ];
+    if (u < units) load_keys(c, u0, uend, kk);
+    for (; u < units; u += stride) {
+      // filter, then this unit's bucket records (all rows at once)
+      uint32_t pass = 0, kfp[kJ];
+      uint64_t rec[kJ];
 #pragma unroll
       for (int j = 0; j < (int)kJ; ++j) {
-        const uint32_t li = (uint32_t)j * kWave + lane, i = u0 + li;
+        const uint32_t i = u0 + (uint32_t)j * kWave + lane;
         const uint64_t h = murmurhash64((uint64_t)kk[j]);
         const uint32_t bl = (uint32_t)h & wmask;
         const uint32_t code = (s_f[bl >> 4] >> ((bl & 15u) * 2u)) & 3u;
-        const bool pass = i < uend && (code == 3u || code == filt_code_of(h));
-        const uint64_t bm = __ballot(pass);
-        if (pass) {
-          const uint32_t q = qn + lane_prefix(bm);
-          qk[q] = kk[j];
-          qr[q] = (uint16_t)li;
-        } else if (WORDS) {
-          sw[li] = code == 0u ? 0u : 1u << kMmRounds;  // no rounds, or a one-key chain that misses
-        }
-        qn += (uint32_t)__popcll(bm);
+        const bool ps = i < uend && (code == 3u || code == filt_code_of(h));
+        pass |= (ps ? 1u : 0u) << j;
+        const uint32_t b = ps ? (uint32_t)h & p.mask : b0;
+        rec[j] = rec8 ? p.bucket8[b] : (uint64_t)p.bucket[b].x;
+        kfp[j] = ps ? bucket_fp(h) : code;  // (a rejected row keeps its code: 0 empty, else a one-key chain)
       }
-      // the queue written by other lanes of this wave is read below
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // lookups: entry e = t * 64 + lane; records of up to 4 entries per lane in flight
-      const uint64_t obase = c * p.cap;
-      for (uint32_t t0 = 0; t0 * kWave < qn; t0 += 4) {
-        uint64_t rec[4];
-        int64_t key[4];
-        uint32_t row[4], kfp[4];
+      // the next unit's keys, in flight during this unit's record and chain round trips
+      const uint32_t un = u + stride;
+      uint64_t cn = 0;
+      uint32_t u0n = 0, uendn = 0;
+      unit(un, cn, u0n, uendn);
+      load_keys(un < units ? cn : c, un < units ? u0n : u0, un < units ? uendn : uend, kn);
+      uint32_t cur[kJ], lim[kJ], st[kJ], mm[kJ], nh[kJ];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const uint32_t e = (t0 + (uint32_t)t) * kWave + lane;
-          const uint32_t ee = e < qn ? e : 0u;
-          key[t] = qk[ee];
-          row[t] = qr[ee];
-          const uint64_t h = murmurhash64((uint64_t)key[t]);
-          const uint32_t b = e < qn ? (uint32_t)h & p.mask : 0u;
-          rec[t] = rec8 ? p.bucket8[b] : (uint64_t)p.bucket[b].x;
-          kfp[t] = bucket_fp(h);
-        }
-        uint32_t nh[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const uint32_t e = (t0 + (uint32_t)t) * kWave + lane;
-          nh[t] = 0;
-          if (e >= qn) continue;
-          const uint32_t st = (uint32_t)rec[t];
-          const uint32_t len = rec8 ? (uint32_t)(rec[t] >> 32) & 0xFFu : (uint32_t)(rec[t] >> 32);
-          uint32_t cur = rec8 ? rec8_first(rec[t], kfp[t]) : st;  // nodes before it cannot hold the key
-          const uint32_t lim = st + len;
-          uint32_t mm = 0;
-          while (cur < lim) {  // the chain from the first node that can hold the key
-            const uint32_t blk = cur & ~1u;
-            const longlong2 v = *reinterpret_cast<const longlong2 *>(p.table + blk);
-            const uint32_t r0 = blk - st;  // node blk's round (chaining_ht.cpp:88-99: one node per Next)
-            if (cur == blk && v.x == key[t]) {
-              ++nh[t];
-              if (r0 < 32u) mm |= 1u << r0;
-            }
-            if (blk + 1u < lim && v.y == key[t]) {
-              ++nh[t];
-              if (r0 + 1u < 32u) mm |= 1u << (r0 + 1u);
-            }
-            cur = blk + 2u;
-          }
-          if (WORDS) sw[row[t]] = len <= kMmRounds ? (mm & ((1u << kMmRounds) - 1u)) | len << kMmRounds : kMmLong | len;
-        }
-        if (!WORDS) {  // append the matches: one atomic per wave step on the chunk's count
-          const uint32_t mine = nh[0] + nh[1] + nh[2] + nh[3];
-          const uint32_t incl = wave_incl_scan(mine);
-          const uint32_t tot = (uint32_t)__shfl((int)incl, kWave - 1);
-          if (tot) {
-            uint32_t ob = 0;
-            if (lane == 0) ob = atomicAdd(p.out_count + c, tot);
-            ob = (uint32_t)__shfl((int)ob, 0) + incl - mine;
-            bool over = false;
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-              for (uint32_t m = 0; m < nh[t]; ++m, ++ob) {
-                if (ob < p.cap) {
-                  p.out_sel[obase + ob] = u0 + row[t];
-                  if (p.out_payload) p.out_payload[obase + ob] = key[t];
-                } else {
-                  over = true;
-                }
-              }
-            if (over && p.status) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
-          }
-        }
+      for (int j = 0; j < (int)kJ; ++j) {
+        mm[j] = nh[j] = 0;
+        st[j] = (uint32_t)rec[j];
+        const uint32_t len = rec8 ? (uint32_t)(rec[j] >> 32) & 0xFFu : (uint32_t)(rec[j] >> 32);
+        lim[j] = (pass >> j) & 1u ? st[j] + len : 0u;
+        cur[j] = (pass >> j) & 1u ? (rec8 ? rec8_first(rec[j], kfp[j]) : st[j]) : 0u;  // nodes before cur cannot match
       }
-      if (WORDS) {  // the unit's words, coalesced at their positions
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // the chains, one 2-key window per row per round, all rows of the wave together
+      while (true) {
+        uint32_t more = 0;
+#pragma unroll
+        for (int j = 0; j < (int)kJ; ++j) more |= cur[j] < lim[j] ? 1u : 0u;
+        if (__ballot(more != 0u) == 0ull) break;
+        longlong2 v[kJ];
+#pragma unroll
+        for (int j = 0; j < (int)kJ; ++j)
+          v[j] = *reinterpret_cast<const longlong2 *>(p.table + (cur[j] < lim[j] ? cur[j] & ~1u : 0u));
 #pragma unroll
         for (int j = 0; j < (int)kJ; ++j) {
-          const uint32_t li = (uint32_t)j * kWave + lane, i = u0 + li;
-          if (i < uend) {
-            if (p.w16) __builtin_nontemporal_store(round_word16(sw[li]), (uint16_t *)p.out_w + base + i);
-            else __builtin_nontemporal_store(sw[li], p.out_w + base + i);
+          if (cur[j] < lim[j]) {
+            const uint32_t blk = cur[j] & ~1u;
+            const uint32_t r0 = blk - st[j];  // node blk's round (chaining_ht.cpp:88-99: one node per Next)
+            if (cur[j] == blk && v[j].x == kk[j]) {
+              ++nh[j];
+              if (r0 < 32u) mm[j] |= 1u << r0;
+            }
+            if (blk + 1u < lim[j] && v[j].y == kk[j]) {
+              ++nh[j];
+              if (r0 + 1u < 32u) mm[j] |= 1u << (r0 + 1u);
+            }
+            cur[j] = blk + 2u;
           }
         }
       }
+      if (WORDS) {  // the rows' Next-round words, coalesced at their positions
+#pragma unroll
+        for (int j = 0; j < (int)kJ; ++j) {
+          const uint32_t i = u0 + (uint32_t)j * kWave + lane;
+          const uint32_t len = (pass >> j) & 1u ? lim[j] - st[j] : (kfp[j] == 0u ? 0u : 1u);
+          const uint32_t word =
+              len <= kMmRounds ? (mm[j] & ((1u << kMmRounds) - 1u)) | len << kMmRounds : kMmLong | len;
+          if (i < uend) {
+            if (p.w16) __builtin_nontemporal_store(round_word16(word), (uint16_t *)p.out_w + c * p.chunk + i);
+            else __builtin_nontemporal_store(word, p.out_w + c * p.chunk + i);
+          }
+        }
+      } else {  // append the matches: one atomic per wave and unit on the chunk's count
+        uint32_t mine = 0;
+#pragma unroll
+        for (int j = 0; j < (int)kJ; ++j) mine += nh[j];
+        const uint32_t incl = wave_incl_scan(mine);
+        const uint32_t tot = (uint32_t)__shfl((int)incl, kWave - 1);
+        if (tot) {
+          uint32_t ob = 0;
+          if (lane == 0) ob = atomicAdd(p.out_count + c, tot);
+          ob = (uint32_t)__shfl((int)ob, 0) + incl - mine;
+          bool over = false;
+          const uint64_t obase = c * p.cap;
+#pragma unroll
+          for (int j = 0; j < (int)kJ; ++j)
+            for (uint32_t m = 0; m < nh[j]; ++m, ++ob) {
+              if (ob < p.cap) {
+                p.out_sel[obase + ob] = u0 + (uint32_t)j * kWave + lane;
+                if (p.out_payload) p.out_payload[obase + ob] = kk[j];
+              } else {
+                over = true;
+              }
+            }
+          if (over && p.status) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < (int)kJ; ++j) kk[j] = kn[j];
+      c = cn;
+      u0 = u0n;
+      uend = uendn;
     }
   }
+}
+
+__global__ __launch_bounds__(kFiltThreads, 6) void probe_chain_filt(ProbeParams p) {
+  __shared__ uint32_t s_f[kFiltMaxWords];  // the partition's filter (64 KiB)
+  chain_filt_body<false, kFiltThreads>(p, s_f);
+}
+__global__ __launch_bounds__(kFiltWordThreads) void chain_words_filt(ProbeParams p) {
+  __shared__ uint32_t s_f[kFiltMaxWords];
+  chain_filt_body<true, kFiltWordThreads>(p, s_f);
 }
 
 // The filter walks apply to the fixed-capacity split's segments of >= 8 partitions of <= 2^18
@@ -2823,11 +2835,13 @@ __global__ __launch_bounds__(kBlock) void emit_ordered(ProbeParams p) {
 
 // Ordered probe, step 3: the round words of one split tile back into row order.  The split
 // recorded where each (tile, partition) run went (runs / ovf_runs); the tile's runs are numbered
-// consecutively (an exclusive scan of their lengths), every thread takes entries j = tid, tid +
-// 1024, ... (consecutive positions inside a run: coalesced reads of the rows and the words),
-// finds j's partition by a binary search over the scan, and drops the word into an LDS image of
-// the tile at the row the split recorded there (16 bits: the row inside its tile); the image is
-// written out whole.  Rows that were not live stay 0.
+// consecutively (an exclusive scan of their lengths) — the order of the split's tile image — every
+// thread takes entries j = tid, tid + 1024, ..., finds j's partition by a binary search over the
+// scan, and drops the word into an LDS image of the tile at the row the split recorded for image
+// entry j (row_loc[t0 + j], 16 bits: the row inside its tile, written by the split in image order,
+// so these reads are whole lines; round 4 — before, the rows sat beside the words at the runs'
+// positions and both were read from partial lines); the image is written out whole.  Rows that were
+// not live stay 0.
 // C2: 4.6 ms, 22.5 GiB of DRAM traffic (the runs' partial lines: ~2x the 8 B read per row) =
 // 5.2 TB/s.  One binary search per thread over kPer consecutive entries (each load instruction then
 // spans ~kPer * 64 entries) measured 13.6 ms; tiles read in the split's XCD order 4.66 ms.
@@ -2886,7 +2900,8 @@ __global__ __launch_bounds__(kUnsplitThreads) void unsplit_words(const uint2 *ru
     W wv[kU];
 #pragma unroll
     for (uint32_t u = 0; u < kU; ++u) {
-      rm[u] = row_loc[pos[u]];
+      const uint32_t j = j0 + u * kUnsplitThreads;
+      rm[u] = row_loc[t0 + (j < total ? j : total - 1)];  // image order: consecutive, whole lines
       wv[u] = w_pos[pos[u]];
     }
 #pragma unroll
@@ -2916,11 +2931,12 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
     // table has a filter, the partitions are at most 2^18 buckets and there are >= 8 of them (one
     // XCD's range each), the chunk is a multiple of 512 rows and no rounds are asked for; the
     // overflow area's chunks (key skew) go to probe_chain_win
-    if (chain_filt_applies(p, 512) && !p.out_rounds && ccj_tune_int("CCJ_CHAIN_FILT", 1)) {
+    if (chain_filt_applies(p, kFiltUnit) && !p.out_rounds && ccj_tune_int("CCJ_CHAIN_FILT", 1)) {
       hipError_t e = hipMemsetAsync(p.out_count, 0, p.n_chunks * sizeof(uint32_t), s);
       if (e != hipSuccess) return e;
-      const uint32_t grid = std::max<uint32_t>(8u, stream_cus(s) / 8 * 8);
-      hipLaunchKernelGGL((probe_chain_filt<false, 512>), dim3(grid), dim3(kFiltThreads), 0, s, p);
+      // two 64 KiB workgroups per CU
+      const uint32_t grid = std::max<uint32_t>(8u, 2 * stream_cus(s) / 8 * 8);
+      hipLaunchKernelGGL(probe_chain_filt, dim3(grid), dim3(kFiltThreads), 0, s, p);
       ProbeParams q = p;  // the overflow area's chunks, in plain order
       q.chunk0 = p.ovf_base / p.chunk;
       q.xcd_swizzle = 0;
@@ -3110,9 +3126,9 @@ hipError_t launch_ordered_walk(int kind, const ProbeParams &p, hipStream_t s) {
   if (p.n_chunks == 0) return hipSuccess;
   if (kind == CCJ_TABLE_CHAIN) {
     if (!p.bucket) return hipErrorInvalidValue;  // every chaining table carries bucket records
-    if (chain_filt_applies(p, 256) && ccj_tune_int("CCJ_CHAIN_FILT", 1)) {  // the bucket filter in LDS
+    if (chain_filt_applies(p, kFiltUnit) && ccj_tune_int("CCJ_CHAIN_FILT", 1)) {  // the bucket filter in LDS
       const uint32_t grid = std::max<uint32_t>(8u, stream_cus(s) / 8 * 8);
-      hipLaunchKernelGGL((probe_chain_filt<true, 256>), dim3(grid), dim3(kFiltThreads), 0, s, p);
+      hipLaunchKernelGGL(chain_words_filt, dim3(grid), dim3(kFiltWordThreads), 0, s, p);
       ProbeParams q = p;  // the overflow area's chunks, in plain order
       q.chunk0 = p.ovf_base / p.chunk;
       q.xcd_swizzle = 0;
@@ -3177,35 +3193,21 @@ hipError_t launch_iota_u32(uint32_t *p, uint64_t n, hipStream_t s) {
 }
 
 // Device-to-device copy for the measured HBM copy ceiling ("report a measured
-// STREAM-copy ceiling on the box"): 16-byte non-temporal loads, four in flight per thread, then
-// the four stores; a grid of 8 workgroups per CU strides over the buffer.
+// STREAM-copy ceiling on the box"): one 16-byte non-temporal load and store per thread, one
+// workgroup per 4 KiB (no grid-stride loop).  tools/copybench.hip on the box (4 GiB, read + write
+// bytes / time; profiles/r4_copybench.log): this form 6.59 TB/s; plain loads / stores 6.29;
+// grid-stride persistent grids (8-32 workgroups per CU, 1-8 loads in flight per thread) 4.9-5.7 —
+// round 3's copy16 was one of those (5.16).
 __global__ __launch_bounds__(256) void copy16(const u32x4 *src, u32x4 *dst, uint64_t n16) {
-  const uint64_t stride = (uint64_t)gridDim.x * 1024;
-  for (uint64_t i = (uint64_t)blockIdx.x * 1024 + threadIdx.x; i < n16; i += stride) {
-    u32x4 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint64_t j = i + (uint64_t)u * 256;
-      v[u] = __builtin_nontemporal_load(src + (j < n16 ? j : i));
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint64_t j = i + (uint64_t)u * 256;
-      if (j < n16) __builtin_nontemporal_store(v[u], dst + j);
-    }
-  }
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n16) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
 }
 
 hipError_t launch_copy16(const void *src, void *dst, uint64_t n16, hipStream_t s) {
-  static const unsigned cus = [] {
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    return (unsigned)(n > 0 ? n : 1);
-  }();
-  const uint64_t need = (n16 + 1023) / 1024;
-  const unsigned grid = (unsigned)(need < 8ull * cus ? (need ? need : 1) : 8ull * cus);
-  hipLaunchKernelGGL(copy16, dim3(grid), dim3(256), 0, s, (const u32x4 *)src, (u32x4 *)dst, n16);
+  if (n16 == 0) return hipSuccess;
+  const uint64_t grid = (n16 + 255) / 256;
+  if (grid > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(copy16, dim3((unsigned)grid), dim3(256), 0, s, (const u32x4 *)src, (u32x4 *)dst, n16);
   return hipGetLastError();
 }
 

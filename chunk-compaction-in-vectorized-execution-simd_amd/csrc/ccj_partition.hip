@@ -578,13 +578,48 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
       const uint64_t dest = q < rc.z ? (rc.x | (uint64_t)rc.y << 32) + q : oadj + q;
       if CCJ_ABLATED(ablate, 0x10u) continue;  // (timing: no stores)
       *(act ? out_k + dest : sink_k) = k;
-      if constexpr (RUNS)  // the ordered probe: the row inside its tile, 16 bits
-        *(act ? reinterpret_cast<uint16_t *>(out_r) + dest : reinterpret_cast<uint16_t *>(sink_r)) = (uint16_t)(si & 0xFFFFu);
+      if constexpr (RUNS)  // the ordered probe: the row inside its tile (16 bits) at the entry's IMAGE index
+        // (tile-major, sequential: the unsplit reads it with whole lines, not from the runs' partial ones)
+        *(have_prev && q < p_tl ? reinterpret_cast<uint16_t *>(out_r) + p_t0 + q : reinterpret_cast<uint16_t *>(sink_r)) =
+            (uint16_t)(si & 0xFFFFu);
       else
         *(act ? out_r + dest : sink_r) = row_base + (uint32_t)(p_t0 + (si & 0xFFFFu));
       __builtin_amdgcn_sched_barrier(0);  // keep the LDS reads of later entries below (registers)
     }
   };
+#ifdef CCJ_SPLIT_STORES16
+  // (timing only, an experiment build (-DCCJ_SPLIT_STORES16): the same bytes stored as 16-byte stores — two keys / four rows
+  // per lane at their first entry's destination, rounded down to 16 bytes: wrong layout; does the
+  // split's time follow its store-instruction count?)
+  auto stores16 = [&]() {
+    typedef long long i64x2 __attribute__((ext_vector_type(2)));
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int it = 0; it < (PER + 1) / 2; ++it) {
+      const uint32_t q = 2u * ((uint32_t)it * THREADS + tid);
+      const uint32_t qq = q < kTileKeys - 1 ? q : 0u;
+      const i64x2 kv = {s_k[qq], s_k[qq + 1]};
+      const uint32_t si = s_i[qq], d = (si >> 16) & (uint32_t)(MAXP - 1);
+      const uint4 rc = s_rec[d];
+      const bool act = have_prev && q + 1 < p_tl && q < rc.z;
+      const uint64_t dest = ((rc.x | (uint64_t)rc.y << 32) + q) & ~1ull;
+      *(act ? reinterpret_cast<i64x2 *>(out_k + dest) : reinterpret_cast<i64x2 *>(sink_k)) = kv;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int it = 0; it < (PER + 3) / 4; ++it) {
+      const uint32_t q = 4u * ((uint32_t)it * THREADS + tid);
+      const uint32_t qq = q < kTileKeys - 3 ? q : 0u;
+      const u32x4 rv = {s_i[qq] & 0xFFFFu, s_i[qq + 1] & 0xFFFFu, s_i[qq + 2] & 0xFFFFu, s_i[qq + 3] & 0xFFFFu};
+      const uint32_t d = (s_i[qq] >> 16) & (uint32_t)(MAXP - 1);
+      const uint4 rc = s_rec[d];
+      const bool act = have_prev && q + 3 < p_tl && q < rc.z;
+      const uint64_t dest = ((rc.x | (uint64_t)rc.y << 32) + q) & ~3ull;
+      *(act ? reinterpret_cast<u32x4 *>(out_r + dest) : reinterpret_cast<u32x4 *>(sink_r)) = rv;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+#endif
   bool dropped = false;
   auto step = [&](uint64_t t, int64_t(&kc)[PER], uint32_t cc, int64_t(&kn)[PER], uint32_t &cn) {
     load(t + bpg, kn, cn);  // kn held the previous tile's keys, already in its image: a whole step of latency
@@ -638,7 +673,11 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
     if (lane == 63) s_wsum[wave] = incl;
     uint32_t r = 0;
     if (h) r = atomicAdd(&cur[(uint64_t)g * parts + opaque_v32(tid)], h);  // awaited after the stores are issued
+#ifdef CCJ_SPLIT_STORES16
+    stores16();
+#else
     stores();
+#endif
     __syncthreads();  // the previous image is read; s_wsum is complete
     uint32_t wpre = 0;
     for (uint32_t w = 0; w < wave; ++w) wpre += s_wsum[w];
@@ -795,6 +834,36 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
                          keys, n, shift, parts, n_tiles, cursors, cap, ovf_base, oc, out_keys, out_rows, status,     \
                          counts, chunk, runs, ovf_runs, row_base, sink_k, sink_r, ablate);                           \
   } while (0)
+#ifdef CCJ_TUNING
+    // (tuning build: two workgroups per CU instead of one lock-stepped 1024-thread workgroup —
+    // CCJ_SPLIT_T = 512: 512 threads x 10 keys; 1025: 1024 threads x 4 keys; both <= 76 KB of LDS)
+    const int st = ccj_tune_int("CCJ_SPLIT_T", 1024);
+    if ((st == 512 || st == 1025) && !runs && parts > 64 && parts <= kSplitParts / 2) {
+      const uint32_t tk = st == 512 ? 512u * 10u : 1024u * 4u;
+      const uint64_t nt = (n + tk - 1) / tk;
+      const unsigned g2 = std::min<unsigned>(2 * grid, 2 * scus);
+      if (st == 512) {
+        if (counts)
+          hipLaunchKernelGGL((slot_split_pipe<true, 512, kSplitParts / 2, 10, false>), dim3(g2), dim3(512), 0, s, keys, n,
+                             shift, parts, nt, cursors, cap, ovf_base, oc, out_keys, out_rows, status, counts, chunk,
+                             runs, ovf_runs, row_base, sink_k, sink_r, ablate);
+        else
+          hipLaunchKernelGGL((slot_split_pipe<false, 512, kSplitParts / 2, 10, false>), dim3(g2), dim3(512), 0, s, keys,
+                             n, shift, parts, nt, cursors, cap, ovf_base, oc, out_keys, out_rows, status, counts, chunk,
+                             runs, ovf_runs, row_base, sink_k, sink_r, ablate);
+      } else {
+        if (counts)
+          hipLaunchKernelGGL((slot_split_pipe<true, 1024, kSplitParts / 2, 4, false>), dim3(g2), dim3(1024), 0, s, keys,
+                             n, shift, parts, nt, cursors, cap, ovf_base, oc, out_keys, out_rows, status, counts, chunk,
+                             runs, ovf_runs, row_base, sink_k, sink_r, ablate);
+        else
+          hipLaunchKernelGGL((slot_split_pipe<false, 1024, kSplitParts / 2, 4, false>), dim3(g2), dim3(1024), 0, s, keys,
+                             n, shift, parts, nt, cursors, cap, ovf_base, oc, out_keys, out_rows, status, counts, chunk,
+                             runs, ovf_runs, row_base, sink_k, sink_r, ablate);
+      }
+      return hipGetLastError();
+    }
+#endif
     if (parts <= 64 && !runs && per == kSplitPer) {  // the owner split: ballot ranking (above)
       if (counts) CCJ_PIPE_LAUNCH(true, 64, kSplitPer);
       else CCJ_PIPE_LAUNCH(false, 64, kSplitPer);

@@ -331,7 +331,8 @@ extern "C" int ccj_pipeline_run(ccj_pipeline *pl, const int64_t *const *d_cols, 
     // 7.19 / 6.00 against 6.63 / 5.66 — positions 1.5 x rows there).
     const size_t ows = in_base || in_obase ? 0 : ccj_probe_ordered_workspace_size(t, in_phys, B);
     const bool dense = ows && ccj_probe_partitioned_positions(t, in_phys, B) * 3 <= in_phys * 4;
-    if (dense && ccj_tune_int("CCJ_PIPE_ORDERED", 1)) {
+    const bool ordered = dense && ccj_tune_int("CCJ_PIPE_ORDERED", 1);
+    if (ordered) {
       PL_TRY(L.ordered_ws.ensure(ows), "alloc");
       ccj_probe_args a{};
       a.keys = p.keys;
@@ -347,40 +348,44 @@ extern "C" int ccj_pipeline_run(ccj_pipeline *pl, const int64_t *const *d_cols, 
       a.out_round_counts = p.out_round_counts;
       a.status = p.status;
       if (int rc = ccj_probe_ordered(t, &a, L.ordered_ws.p, L.ordered_ws.bytes, stream)) return rc;
-      uint64_t st = 0;
-      PL_TRY(hipMemcpyAsync(&st, tot + 3, sizeof(st), hipMemcpyDeviceToHost, s), "copy status");
-      PL_TRY(hipStreamSynchronize(s), "sync");
-      if (st & CCJ_FLAG_PART_OVERFLOW) {
-        PL_TRY(hipMemsetAsync(tot + 3, 0, 8, s), "memset");
-        PL_TRY(ccj::launch_probe(t->info.kind, p, s), "pipeline probe");
-      }
     } else {
       PL_TRY(ccj::launch_probe(t->info.kind, p, s), "pipeline probe");
     }
 
-    // Output sizes: matches and non-empty Next results, per chunk and in total.
+    // Output sizes: matches and non-empty Next results, per chunk and in total (one D2H copy and
+    // synchronisation per join; the ordered route's skew-overflow flag rides in the same copy, so
+    // it costs a second one only when it fired: the chunk probe re-runs, the sizes are recomputed).
     PL_TRY(L.rows.ensure(in_chunks * 8), "alloc");
     PL_TRY(L.rows_pre.ensure(in_chunks * 8), "alloc");
     PL_TRY(L.segs.ensure(in_chunks * 8), "alloc");
     PL_TRY(L.segs_pre.ensure(in_chunks * 8), "alloc");
     size_t tb = ccj::scan_bytes(in_chunks);
     PL_TRY(L.scan_tmp.ensure(tb), "alloc");
-    const unsigned g = (unsigned)((in_chunks + 255) / 256);
-    hipLaunchKernelGGL(ccj::level_sizes, dim3(g), dim3(256), 0, s, p.out_count, p.out_rounds, p.out_round_counts, R,
-                       in_chunks, L.rows.as<uint64_t>(), L.segs.as<uint64_t>());
-    PL_TRY(hipGetLastError(), "level sizes");
-    PL_TRY(hipcub::DeviceScan::ExclusiveSum(L.scan_tmp.p, tb, L.rows.as<uint64_t>(), L.rows_pre.as<uint64_t>(),
-                                            (int)in_chunks, s),
-           "scan");
-    PL_TRY(hipcub::DeviceScan::ExclusiveSum(L.scan_tmp.p, tb, L.segs.as<uint64_t>(), L.segs_pre.as<uint64_t>(),
-                                            (int)in_chunks, s),
-           "scan");
-    hipLaunchKernelGGL(ccj::level_totals, dim3(1), dim3(1), 0, s, L.rows.as<uint64_t>(), L.rows_pre.as<uint64_t>(),
-                       L.segs.as<uint64_t>(), L.segs_pre.as<uint64_t>(), in_chunks, tot);
-    PL_TRY(hipGetLastError(), "level totals");
     uint64_t h[4];
-    PL_TRY(hipMemcpyAsync(h, tot, sizeof(h), hipMemcpyDeviceToHost, s), "copy sizes");
-    PL_TRY(hipStreamSynchronize(s), "sync");
+    auto sizes = [&]() -> int {
+      const unsigned g = (unsigned)((in_chunks + 255) / 256);
+      hipLaunchKernelGGL(ccj::level_sizes, dim3(g), dim3(256), 0, s, p.out_count, p.out_rounds, p.out_round_counts, R,
+                         in_chunks, L.rows.as<uint64_t>(), L.segs.as<uint64_t>());
+      PL_TRY(hipGetLastError(), "level sizes");
+      PL_TRY(hipcub::DeviceScan::ExclusiveSum(L.scan_tmp.p, tb, L.rows.as<uint64_t>(), L.rows_pre.as<uint64_t>(),
+                                              (int)in_chunks, s),
+             "scan");
+      PL_TRY(hipcub::DeviceScan::ExclusiveSum(L.scan_tmp.p, tb, L.segs.as<uint64_t>(), L.segs_pre.as<uint64_t>(),
+                                              (int)in_chunks, s),
+             "scan");
+      hipLaunchKernelGGL(ccj::level_totals, dim3(1), dim3(1), 0, s, L.rows.as<uint64_t>(), L.rows_pre.as<uint64_t>(),
+                         L.segs.as<uint64_t>(), L.segs_pre.as<uint64_t>(), in_chunks, tot);
+      PL_TRY(hipGetLastError(), "level totals");
+      PL_TRY(hipMemcpyAsync(h, tot, sizeof(h), hipMemcpyDeviceToHost, s), "copy sizes");
+      PL_TRY(hipStreamSynchronize(s), "sync");
+      return CCJ_OK;
+    };
+    if (int rc = sizes()) return rc;
+    if (ordered && (h[3] & CCJ_FLAG_PART_OVERFLOW)) {  // key skew filled the split's overflow area
+      PL_TRY(hipMemsetAsync(tot + 3, 0, 8, s), "memset");
+      PL_TRY(ccj::launch_probe(t->info.kind, p, s), "pipeline probe");
+      if (int rc = sizes()) return rc;
+    }
     if (h[3]) return ccj::api_fail(CCJ_ERR_LIMIT, "ccj_pipeline_run: probe status flags " + std::to_string(h[3]));
     const uint64_t T = h[0], S = h[1];
     res->rows_out[l] = T;
