@@ -594,6 +594,7 @@ struct PartLayout {
   uint32_t parts;
   uint64_t seg_cap, positions;
   uint64_t ovf_base, ovf_cap;  // overflow area after the segments (runs that do not fit: key skew)
+  uint64_t ovf_sub;            // its 8 per-XCD sub-areas (a multiple of chunk each; the last 64 positions: the sink)
 };
 PartLayout part_layout(const ccj_table *t, uint64_t n_rows, uint32_t chunk) {
   PartLayout L{};
@@ -605,7 +606,9 @@ PartLayout part_layout(const ccj_table *t, uint64_t n_rows, uint32_t chunk) {
   }
   L.seg_cap = ccj::slot_seg_cap(n_rows, L.pl, chunk);
   L.ovf_base = (uint64_t)L.parts * 8 * L.seg_cap;
-  L.ovf_cap = (n_rows / 16 + chunk + chunk - 1) / chunk * chunk;  // 1/16 of the rows + one chunk
+  // 1/16 of the rows, at least one chunk per sub-area, and the split's 64-position sink
+  L.ovf_cap = (n_rows / 16 + 8ull * chunk + 64 + chunk - 1) / chunk * chunk;
+  L.ovf_sub = (L.ovf_cap - 64) / 8 / chunk * chunk;
   L.positions = L.ovf_base + L.ovf_cap;
   return L;
 }
@@ -621,7 +624,7 @@ size_t ccj_probe_partitioned_workspace_size(const ccj_table *t, uint64_t n_rows,
   if (!t) return 0;
   const PartLayout L = part_layout(t, n_rows, chunk);
   // partitioned keys (positions) + the fixed split's cursors, or the exact split's pass scratch
-  const size_t fixed = align256(((uint64_t)L.parts * 8 + 1) * 4);
+  const size_t fixed = align256(((uint64_t)L.parts * 8 + 8) * 4);
   const size_t exact = ccj::slot_partition_workspace(n_rows, L.pl);
   // + the rank walk's per-block hit masks, hit counts and partition counters
 #ifdef CCJ_RANK_WALK
@@ -690,7 +693,7 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
     uint32_t *cursors = (uint32_t *)rest;
     // CCJ_PART_SHARE: 3/4 of the stream's CUs (a multiple of 8), the rest left to other streams
     const uint32_t share = (flags & CCJ_PART_SHARE) ? std::max<uint32_t>(8u, ccj::stream_cus(s) * 3 / 4 / 8 * 8) : 0u;
-    HIP_TRY(ccj::launch_slot_split_fixed(a->keys, a->n_rows, L.pl, L.seg_cap, L.ovf_base, L.ovf_cap, cursors, pkeys,
+    HIP_TRY(ccj::launch_slot_split_fixed(a->keys, a->n_rows, L.pl, L.seg_cap, L.ovf_base, L.ovf_cap, L.ovf_sub, cursors, pkeys,
                                          out_row_map, a->status, s, a->counts, a->chunk, nullptr, nullptr, 0, ~0u,
                                          share),
             "slot split");
@@ -699,6 +702,7 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
     p.seg_parts = L.parts;
     p.seg_cap = L.seg_cap;
     p.ovf_base = L.ovf_base;
+    p.ovf_sub = L.ovf_sub;
     p.swz_chunks = L.ovf_base / a->chunk;
     p.n_rows = L.positions;
     p.n_chunks = out_chunks;
@@ -743,7 +747,7 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
                     a->chunk % ccj::kRankChunkMultiple == 0 && ((flags & CCJ_PART_RANK) || ccj_tune_int("CCJ_RANK", 0));
   if (rank) {
     const ccj::RankIndex ix{t->d_occ, t->d_pre, t->d_ckeys, t->rank_wbits};
-    const size_t fixed = align256(((uint64_t)L.parts * 8 + 1) * 4);
+    const size_t fixed = align256(((uint64_t)L.parts * 8 + 8) * 4);
     const size_t exact_ws = ccj::slot_partition_workspace(a->n_rows, L.pl);
     void *rws = (char *)rest + align256(fixed > exact_ws ? fixed : exact_ws);
     HIP_TRY(ccj::launch_probe_rank(p, ix, rws, s), "rank walk launch");
@@ -828,7 +832,7 @@ OrderedLayout ordered_layout(const ccj_table *t, uint64_t n_rows, uint32_t chunk
   O.row_map = take(O.L.positions * 4);
   O.w_pos = take(O.L.positions * 4);
   O.w_row = take(n_rows * 4);
-  O.cursors = take(((uint64_t)O.L.parts * 8 + 1) * 4);
+  O.cursors = take(((uint64_t)O.L.parts * 8 + 8) * 4);
   O.runs = take(O.n_tiles * O.L.parts * 8);
   O.ovf_runs = take(O.n_tiles * O.L.parts * 4);
   O.total = off;
@@ -868,7 +872,7 @@ int ccj_probe_ordered(const ccj_table *t, const ccj_probe_args *a, void *ws, siz
   const PartLayout &L = O.L;
   phase_mark(s, 0);
   // 1. one-pass slot split of the live rows, recording where every tile's runs went
-  HIP_TRY(ccj::launch_slot_split_fixed(a->keys, a->n_rows, L.pl, L.seg_cap, L.ovf_base, L.ovf_cap, cursors, pkeys,
+  HIP_TRY(ccj::launch_slot_split_fixed(a->keys, a->n_rows, L.pl, L.seg_cap, L.ovf_base, L.ovf_cap, L.ovf_sub, cursors, pkeys,
                                        row_map, a->status, s, a->counts, a->chunk, runs, ovf_runs),
           "slot split");
   phase_mark(s, 1);
@@ -880,6 +884,7 @@ int ccj_probe_ordered(const ccj_table *t, const ccj_probe_args *a, void *ws, siz
   q.seg_parts = L.parts;
   q.seg_cap = L.seg_cap;
   q.ovf_base = L.ovf_base;
+  q.ovf_sub = L.ovf_sub;
   q.swz_chunks = L.ovf_base / a->chunk;
   q.n_rows = L.positions;
   q.n_chunks = L.positions / a->chunk + (L.positions % a->chunk ? 1 : 0);

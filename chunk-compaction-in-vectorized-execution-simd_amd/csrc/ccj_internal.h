@@ -104,9 +104,11 @@ struct ProbeParams {
   const uint32_t *seg_count;
   uint32_t seg_parts;
   uint64_t seg_cap;
-  // shared overflow area [ovf_base, n_rows): runs that did not fit their segment (key skew);
-  // its fill level is seg_count[seg_parts * 8].  0 = no overflow area.
+  // overflow area [ovf_base, n_rows): runs that did not fit their segment (key skew), in 8
+  // sub-areas of ovf_sub positions (a multiple of chunk), one per tile group g (XCD) with fill
+  // level seg_count[seg_parts * 8 + g].  0 = no overflow area.
   uint64_t ovf_base;
+  uint64_t ovf_sub;
   uint64_t swz_chunks;   // chunks dealt to XCDs in contiguous ranges (0: all); the overflow area's
                          // chunks follow in plain order so they do not unbalance the XCDs' shares
   uint32_t xcd_swizzle;  // 1: consecutive chunks go to the same XCD (L2 reuse of partitioned input)
@@ -226,13 +228,15 @@ hipError_t launch_slot_partition(const int64_t *keys, uint64_t n, const SlotPlan
 // One-pass fixed-capacity form: segment (partition d, XCD group g) = positions [(d*8+g)*cap, +cap);
 // cursors[g*parts + d] = rows that went to it (may exceed cap: CCJ_FLAG_PART_OVERFLOW raised).
 uint64_t slot_seg_cap(uint64_t n, const SlotPlan &pl, uint32_t chunk);
-// cursors[parts * 8] = rows that went to the overflow area [ovf_base, ovf_base + ovf_cap).
+// cursors[parts * 8 + g] = rows that tile group g (XCD) put in its overflow sub-area
+// [ovf_base + g * ovf_sub, + ovf_sub) (ovf_sub = 0: no overflow area); the last 64 positions of the
+// area [ovf_base, ovf_base + ovf_cap) are the pipelined form's sink.
 // counts: live rows per input chunk.  runs (optional; the ordered probe): per (tile, partition)
 // {segment position of the run, segment length | overflow-area length << 16}; ovf_runs: the
 // overflow-area position where that length is non-zero.  Tiles are slot_split_tile_keys(parts, runs) keys.
 // With runs, out_rows receives each position's row INSIDE ITS TILE as uint16_t (the unsplit's input).
 hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPlan &pl, uint64_t cap,
-                                   uint64_t ovf_base, uint64_t ovf_cap, uint32_t *cursors, int64_t *out_keys,
+                                   uint64_t ovf_base, uint64_t ovf_cap, uint64_t ovf_sub, uint32_t *cursors, int64_t *out_keys,
                                    uint32_t *out_rows, uint32_t *status, hipStream_t s,
                                    const uint32_t *counts = nullptr, uint32_t chunk = 0, uint2 *runs = nullptr,
                                    uint32_t *ovf_runs = nullptr, uint32_t row_base = 0, uint32_t shift = ~0u,

@@ -541,9 +541,10 @@ __device__ __forceinline__ uint32_t flat_phys(const ProbeParams &p, uint64_t bas
   const uint64_t rem = p.n_rows - base;
   uint32_t phys = rem < p.chunk ? (uint32_t)rem : p.chunk;
   if (p.seg_count && p.ovf_base && base >= p.ovf_base) {  // the overflow area's chunks
-    uint64_t live = p.seg_count[(uint64_t)p.seg_parts * 8];
-    live = live < p.n_rows - p.ovf_base ? live : p.n_rows - p.ovf_base;
-    const uint64_t off = base - p.ovf_base;
+    const uint64_t sub = p.ovf_sub ? (base - p.ovf_base) / p.ovf_sub : 8u;  // its group's sub-area
+    uint64_t live = sub < 8u ? p.seg_count[(uint64_t)p.seg_parts * 8 + sub] : 0u;
+    live = live < p.ovf_sub ? live : p.ovf_sub;
+    const uint64_t off = sub < 8u ? base - p.ovf_base - sub * p.ovf_sub : 0u;
     phys = live > off ? (live - off < phys ? (uint32_t)(live - off) : phys) : 0u;
   } else if (p.counts && !p.seg_count) {  // identity layout of a column with per-chunk live counts
     const uint32_t cn = p.counts[base / p.chunk];
@@ -1407,176 +1408,291 @@ __global__ __launch_bounds__(kFlatThreads) void probe_chain_win(ProbeParams p) {
 // of a chunk are appended to its output region through out_count[c] (zeroed by the launcher) with
 // one atomic per wave step: the order inside a chunk is free here (L1 / L2 parity), as in every
 // partitioned walk.  Chunks of the overflow area (key skew) are walked by probe_chain_win.
-// match walk: 768 threads, two workgroups per CU (64 KiB of LDS each): 24 waves, <= 80 VGPRs; the
-// round-word walk needs more registers: 1024 threads, one workgroup per CU
-constexpr int kFiltThreads = 768, kFiltWordThreads = 1024;
-constexpr uint32_t kFiltUnit = 256;                  // rows per work unit (4 per lane: <= 64 VGPRs, 32 waves per CU)
+// Both walks: 768 threads and two workgroups per CU (filter 64 KiB + 12 queues of 1.3 KiB each).
+// The walk is issue-bound (r4 v3 profile: ~520 VALU instructions per 256-row unit and wave, a
+// quarter of them 64-bit unit arithmetic), so v4 keeps the unit arithmetic scalar (wave index
+// through readfirstlane, no 64-bit division), reads bucket records for the passing rows only
+// (exec-masked), and walks chains on a packed queue: after the records, the unit's rows whose chain
+// can still hold their key (~10 % at C3) move to the wave's LDS queue, one per lane, so a chain
+// round is one 16-byte load and one compare per lane instead of four.
+constexpr int kFiltThreads = 768, kFiltWordThreads = 768;
+constexpr uint32_t kFiltUnit = 256;                  // rows per work unit (4 per lane)
+constexpr uint32_t kFiltQ = 64;                      // queue entries per wave (more: extra passes)
+#ifndef CCJ_FILT_DEFER
+#define CCJ_FILT_DEFER 0
+#endif
+constexpr bool kFiltDefer = CCJ_FILT_DEFER;  // matches appended one unit later (experiment: spills)
 constexpr uint32_t kFiltMaxWords = (1u << 18) / 16;  // 2 bits per bucket, windows <= 2^18 buckets
 __device__ __forceinline__ uint32_t filt_code_of(uint64_t h) { return 1u + (uint32_t)((h >> 40) & 1u); }
 
+template <bool WORDS>
+struct FiltQueue {  // one wave's chain rows of a unit
+  int64_t key[kFiltQ];
+  uint32_t cur[kFiltQ], lim[kFiltQ];
+  uint32_t st[WORDS ? kFiltQ : 1];  // the chain's first node (the round of a node)
+  uint8_t row[kFiltQ];              // the row in the unit
+};
+
 // WORDS = false: matches appended to each chunk's output (the partitioned probe); WORDS = true: every
 // row's Next-round word at its position (the ordered probe, chain_words' output: the filter gives an
-// empty bucket's 0 rounds and a one-key chain's miss — 1 round, no match — without any read).
-// Each lane keeps its unit rows (4) in registers: no queue, so the workgroup's LDS is the filter
-// alone (64 KiB) and two workgroups share a CU (24 waves).  Every memory step of a unit is one batch
-// for all its rows, issued unconditionally (a row that needs no read loads the partition's first
-// record pair / the chain array's first pair: one line shared by every such lane, so an instruction
-// costs at most one extra L2 request): the rows' bucket records, then rounds of 2-key chain windows
-// while some row's chain can still hold its key.  The next unit's keys are loaded right after this
-// unit's records are issued, so their HBM latency overlaps the record and chain round trips.
+// empty bucket's 0 rounds and a one-key chain's miss — 1 round, no match — without any read; a
+// passing row whose fingerprints rule its chain out has the chain's length in rounds, no match).
 template <bool WORDS, int NT>
-__device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *s_f) {
+__device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *s_f, FiltQueue<WORDS> *s_q) {
   constexpr uint32_t kJ = kFiltUnit / kWave;  // rows per lane and unit
-  constexpr uint32_t kFiltWaves = NT / kWave;
-  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+  constexpr uint32_t kWaves = NT / kWave;
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+  FiltQueue<WORDS> &q = s_q[wave];
   const uint32_t x = blockIdx.x & 7u, k = blockIdx.x >> 3, K = gridDim.x >> 3;
   const uint32_t P = p.seg_parts;
-  const uint32_t spc = (uint32_t)(p.seg_cap / p.chunk);  // chunks per segment
-  const uint32_t upc = p.chunk / kFiltUnit;              // units per chunk (chunk: a multiple of kFiltUnit)
-  const uint32_t units = 8u * spc * upc;                 // units per partition
+  const uint32_t chunk = p.chunk;
+  const uint32_t spc = (uint32_t)(p.seg_cap / chunk);  // chunks per segment
+  const uint32_t upc = chunk / kFiltUnit;              // units per chunk (chunk: a multiple of kFiltUnit)
+  const uint32_t ups = spc * upc;                      // units per segment
+  const bool cp2 = (chunk & (chunk - 1u)) == 0u;
+  const uint32_t cl2 = (uint32_t)__builtin_ctz(chunk);
   const uint32_t wb = p.filt_wb;
   const uint32_t fwords = (1u << wb) / 16u;
   const uint32_t wmask = (1u << wb) - 1u;
   const bool rec8 = p.bucket8 != nullptr;
-  const uint32_t stride = K * kFiltWaves;
+  const bool fm = WORDS ? p.w16 != 0u : p.first_match != 0u;  // distinct build keys
+  const uint32_t stride = K * kWaves;
   for (uint32_t d = x * P / 8; d < (x + 1) * P / 8; ++d) {
     __syncthreads();  // the previous partition's filter is no longer read
-    for (uint32_t w = tid * 4; w < fwords; w += NT * 4)
+    for (uint32_t w = threadIdx.x * 4; w < fwords; w += NT * 4)
       *reinterpret_cast<u32x4 *>(&s_f[w]) = *reinterpret_cast<const u32x4 *>(p.filt + (uint64_t)d * fwords + w);
     __syncthreads();
-    const uint32_t b0 = (d << wb) & p.mask & ~1u;  // the partition's first bucket pair (idle rows read it)
-    // unit u of partition d: chunk c, rows [u0, uend) of it (uend <= u0: nothing live)
-    auto unit = [&](uint32_t u, uint64_t &c, uint32_t &u0, uint32_t &uend) {
-      const uint32_t g = u / (spc * upc), r = u - g * spc * upc;
-      c = ((uint64_t)(d * 8 + g) * p.seg_cap) / p.chunk + r / upc;
-      const uint32_t phys = u < units ? flat_phys(p, c * p.chunk) : 0u;
-      u0 = (r % upc) * kFiltUnit;
+    // unit r of segment d * 8 + g (wave-uniform, scalar): rows [r * kFiltUnit, + kFiltUnit) of the
+    // segment, i.e. chunk c, rows [u0, uend) of it (uend <= u0: nothing live); the segment holds
+    // seg_count[g * P + d] rows.  A wave's units are u = g * ups + r = k + K * wave + stride * i,
+    // (g, r) advanced without division.
+    auto unit = [&](uint32_t g, uint32_t r, uint64_t &c, uint32_t &u0, uint32_t &uend) {
+      const uint32_t pos = r * kFiltUnit;
+      const uint32_t ci = cp2 ? pos >> cl2 : pos / chunk;
+      c = (uint64_t)(d * 8u + g) * spc + ci;
+      u0 = pos - ci * chunk;
+      const uint64_t fill = p.seg_count[g < 8u ? g * P + d : 0u];
+      uint64_t live = g < 8u ? fill : 0u;
+      live = live < p.seg_cap ? live : p.seg_cap;
+      const uint64_t off = (uint64_t)ci * chunk;
+      const uint32_t phys = live > off ? (live - off < chunk ? (uint32_t)(live - off) : chunk) : 0u;
       uend = phys <= u0 ? u0 : (phys - u0 < kFiltUnit ? phys : u0 + kFiltUnit);
+    };
+    auto advance = [&](uint32_t &g, uint32_t &r, uint32_t by) {
+      r += by;
+      while (g < 8u && r >= ups) {
+        r -= ups;
+        ++g;
+      }
     };
     auto load_keys = [&](uint64_t c, uint32_t u0, uint32_t uend, int64_t(&kk)[kJ]) {
 #pragma unroll
       for (int j = 0; j < (int)kJ; ++j) {
         const uint32_t i = u0 + (uint32_t)j * kWave + lane;
-        kk[j] = __builtin_nontemporal_load(p.keys + c * p.chunk + (i < uend ? i : u0));
+        kk[j] = __builtin_nontemporal_load(p.keys + c * chunk + (i < uend ? i : u0));
       }
     };
-    uint32_t u = k + K * wave;
+    uint32_t g = 0, r = 0;
+    advance(g, r, k + K * wave);
     uint64_t c = 0;
     uint32_t u0 = 0, uend = 0;
-    unit(u, c, u0, uend);
+    unit(g, r, c, u0, uend);
     int64_t kk[kJ], kn[kJ];
-    if (u < units) load_keys(c, u0, uend, kk);
-    for (; u < units; u += stride) {
-      // filter, then this unit's bucket records (all rows at once)
-      uint32_t pass = 0, kfp[kJ];
-      uint64_t rec[kJ];
+    if (g < 8u) load_keys(c, u0, uend, kk);
+    // match walk: the last queue pass of a unit appends its matches one unit later — its atomic's
+    // reply then lands under the next unit's record wait instead of costing a round trip of its own
+    // (wave-uniform: dtot matches of chunk dc, rows from du0; per lane: dkey, dw = the matches of
+    // the wave's earlier lanes << 16 | the lane's matches << 8 | its row in the unit, and lane 0's
+    // atomic reply dob)
+    uint32_t dtot = 0, du0 = 0, dw = 0, dob = 0;
+    uint64_t dc = 0;
+    int64_t dkey = 0;
+    auto append = [&](uint64_t oc, uint32_t ou0, uint32_t ob0, uint32_t ex, uint32_t nh, uint32_t row, int64_t key) {
+      uint32_t ob = (uint32_t)__shfl((int)ob0, 0) + ex;
+      bool over = false;
+      const uint64_t obase = oc * p.cap;
+      for (uint32_t m = 0; m < nh; ++m, ++ob) {
+        if (ob < p.cap) {
+          p.out_sel[obase + ob] = ou0 + row;
+          if (p.out_payload) p.out_payload[obase + ob] = key;
+        } else {
+          over = true;
+        }
+      }
+      if (over && p.status) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
+    };
+    while (g < 8u) {
+      // filter, then the passing rows' bucket records
+      uint32_t pass = 0, kfp[kJ], bk[kJ];
 #pragma unroll
       for (int j = 0; j < (int)kJ; ++j) {
         const uint32_t i = u0 + (uint32_t)j * kWave + lane;
         const uint64_t h = murmurhash64((uint64_t)kk[j]);
         const uint32_t bl = (uint32_t)h & wmask;
         const uint32_t code = (s_f[bl >> 4] >> ((bl & 15u) * 2u)) & 3u;
-        const bool ps = i < uend && (code == 3u || code == filt_code_of(h));
+        const bool ps = (i < uend) & ((code == 3u) | (code == filt_code_of(h)));  // (no branches)
         pass |= (ps ? 1u : 0u) << j;
-        const uint32_t b = ps ? (uint32_t)h & p.mask : b0;
-        rec[j] = rec8 ? p.bucket8[b] : (uint64_t)p.bucket[b].x;
+        bk[j] = (uint32_t)h & p.mask;
         kfp[j] = ps ? bucket_fp(h) : code;  // (a rejected row keeps its code: 0 empty, else a one-key chain)
       }
-      // the next unit's keys, in flight during this unit's record and chain round trips
-      const uint32_t un = u + stride;
-      uint64_t cn = 0;
-      uint32_t u0n = 0, uendn = 0;
-      unit(un, cn, u0n, uendn);
-      load_keys(un < units ? cn : c, un < units ? u0n : u0, un < units ? uendn : uend, kn);
-      uint32_t cur[kJ], lim[kJ], st[kJ], mm[kJ], nh[kJ];
+      uint64_t rec[kJ];
 #pragma unroll
       for (int j = 0; j < (int)kJ; ++j) {
-        mm[j] = nh[j] = 0;
-        st[j] = (uint32_t)rec[j];
+        rec[j] = 0;
+        if ((pass >> j) & 1u) rec[j] = rec8 ? p.bucket8[bk[j]] : (uint64_t)p.bucket[bk[j]].x;
+      }
+      // the next unit's keys, in flight during this unit's record and chain round trips
+      uint32_t gn = g, rn = r;
+      advance(gn, rn, stride);
+      uint64_t cn = 0;
+      uint32_t u0n = 0, uendn = 0;
+      unit(gn, rn, cn, u0n, uendn);
+      load_keys(gn < 8u ? cn : c, gn < 8u ? u0n : u0, gn < 8u ? uendn : uend, kn);
+      // slot j's chain range from its record: nodes [cur, lim) can still hold the key
+      auto range = [&](int j, uint32_t &st, uint32_t &cur, uint32_t &lim) {
+        const bool ps = (pass >> j) & 1u;
+        st = (uint32_t)rec[j];
         const uint32_t len = rec8 ? (uint32_t)(rec[j] >> 32) & 0xFFu : (uint32_t)(rec[j] >> 32);
-        lim[j] = (pass >> j) & 1u ? st[j] + len : 0u;
-        cur[j] = (pass >> j) & 1u ? (rec8 ? rec8_first(rec[j], kfp[j]) : st[j]) : 0u;  // nodes before cur cannot match
-      }
-      // the chains, one 2-key window per row per round, all rows of the wave together
-      while (true) {
-        uint32_t more = 0;
+        lim = ps ? st + len : 0u;
+        cur = ps ? (rec8 ? rec8_first(rec[j], kfp[j]) : st) : 0u;
+      };
+      // queue index of every chain row (slot-major); WORDS: the other rows' words now, coalesced
+      uint64_t qm[kJ];  // wave-uniform: slot j's chain rows, and the queue index of its first
+      uint32_t qs[kJ], qn = 0;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous unit's queue reads are done
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int j = 0; j < (int)kJ; ++j) more |= cur[j] < lim[j] ? 1u : 0u;
-        if (__ballot(more != 0u) == 0ull) break;
-        longlong2 v[kJ];
-#pragma unroll
-        for (int j = 0; j < (int)kJ; ++j)
-          v[j] = *reinterpret_cast<const longlong2 *>(p.table + (cur[j] < lim[j] ? cur[j] & ~1u : 0u));
-#pragma unroll
-        for (int j = 0; j < (int)kJ; ++j) {
-          if (cur[j] < lim[j]) {
-            const uint32_t blk = cur[j] & ~1u;
-            const uint32_t r0 = blk - st[j];  // node blk's round (chaining_ht.cpp:88-99: one node per Next)
-            if (cur[j] == blk && v[j].x == kk[j]) {
-              ++nh[j];
-              if (r0 < 32u) mm[j] |= 1u << r0;
-            }
-            if (blk + 1u < lim[j] && v[j].y == kk[j]) {
-              ++nh[j];
-              if (r0 + 1u < 32u) mm[j] |= 1u << (r0 + 1u);
-            }
-            cur[j] = blk + 2u;
-          }
+      for (int j = 0; j < (int)kJ; ++j) {
+        uint32_t st, cur, lim;
+        range(j, st, cur, lim);
+        const bool act = cur < lim;
+        const uint64_t bm = __ballot(act);
+        const uint32_t qi = qn + lane_prefix(bm);
+        qm[j] = bm;
+        qs[j] = qn;
+        qn += (uint32_t)__popcll(bm);
+        if (act && qi < kFiltQ) {
+          q.key[qi] = kk[j];
+          q.cur[qi] = cur;
+          q.lim[qi] = lim;
+          if (WORDS) q.st[WORDS ? qi : 0] = st;
+          q.row[qi] = (uint8_t)((uint32_t)j * kWave + lane);
         }
-      }
-      if (WORDS) {  // the rows' Next-round words, coalesced at their positions
-#pragma unroll
-        for (int j = 0; j < (int)kJ; ++j) {
+        if (WORDS) {
           const uint32_t i = u0 + (uint32_t)j * kWave + lane;
-          const uint32_t len = (pass >> j) & 1u ? lim[j] - st[j] : (kfp[j] == 0u ? 0u : 1u);
-          const uint32_t word =
-              len <= kMmRounds ? (mm[j] & ((1u << kMmRounds) - 1u)) | len << kMmRounds : kMmLong | len;
-          if (i < uend) {
-            if (p.w16) __builtin_nontemporal_store(round_word16(word), (uint16_t *)p.out_w + c * p.chunk + i);
-            else __builtin_nontemporal_store(word, p.out_w + c * p.chunk + i);
+          if (!act && i < uend) {
+            const uint32_t len = lim - st;
+            const uint32_t word = (pass >> j) & 1u ? (len <= kMmRounds ? len << kMmRounds : kMmLong | len)
+                                                   : (kfp[j] == 0u ? 0u : 1u << kMmRounds);
+            if (p.w16) __builtin_nontemporal_store(round_word16(word), (uint16_t *)p.out_w + c * chunk + i);
+            else __builtin_nontemporal_store(word, p.out_w + c * chunk + i);
           }
         }
-      } else {  // append the matches: one atomic per wave and unit on the chunk's count
-        uint32_t mine = 0;
+      }
+      if (!WORDS && dtot) {  // the previous unit's matches (its atomic replied before these records)
+        append(dc, du0, dob, dw >> 16, (dw >> 8) & 0xFFu, dw & 0xFFu, dkey);
+        dtot = 0;
+      }
+      for (uint32_t qb = 0; qb < qn; qb += kFiltQ) {
+        if (qb) {  // a unit with more than kFiltQ chain rows: the next kFiltQ of them
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int j = 0; j < (int)kJ; ++j) mine += nh[j];
-        const uint32_t incl = wave_incl_scan(mine);
-        const uint32_t tot = (uint32_t)__shfl((int)incl, kWave - 1);
-        if (tot) {
-          uint32_t ob = 0;
-          if (lane == 0) ob = atomicAdd(p.out_count + c, tot);
-          ob = (uint32_t)__shfl((int)ob, 0) + incl - mine;
-          bool over = false;
-          const uint64_t obase = c * p.cap;
-#pragma unroll
-          for (int j = 0; j < (int)kJ; ++j)
-            for (uint32_t m = 0; m < nh[j]; ++m, ++ob) {
-              if (ob < p.cap) {
-                p.out_sel[obase + ob] = u0 + (uint32_t)j * kWave + lane;
-                if (p.out_payload) p.out_payload[obase + ob] = kk[j];
-              } else {
-                over = true;
-              }
+          for (int j = 0; j < (int)kJ; ++j) {
+            const uint32_t qi = qs[j] + lane_prefix(qm[j]), e = qi - qb;
+            if (((qm[j] >> lane) & 1u) && qi >= qb && e < kFiltQ) {
+              uint32_t st, cur, lim;
+              range(j, st, cur, lim);
+              q.key[e] = kk[j];
+              q.cur[e] = cur;
+              q.lim[e] = lim;
+              if (WORDS) q.st[WORDS ? e : 0] = st;
+              q.row[e] = (uint8_t)((uint32_t)j * kWave + lane);
             }
-          if (over && p.status) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
+          }
+        }
+        // the queue written by other lanes of this wave is read below
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t ne = qn - qb < kFiltQ ? qn - qb : kFiltQ;
+        const bool live = lane < ne;
+        const int64_t key = q.key[lane];
+        const uint32_t lim = live ? q.lim[lane] : 0u;
+        const uint32_t st = WORDS ? q.st[WORDS ? lane : 0] : 0u;
+        const uint32_t row = q.row[lane];
+        uint32_t cur = live ? q.cur[lane] : 0u;
+        uint32_t nh = 0, mm = 0;
+        while (__ballot(cur < lim) != 0ull) {  // one 2-key window per chain row and round
+          const longlong2 v = *reinterpret_cast<const longlong2 *>(p.table + (cur < lim ? cur & ~1u : 0u));
+          if (cur < lim) {
+            const uint32_t blk = cur & ~1u;
+            const uint32_t r0 = blk - st;  // node blk's round (chaining_ht.cpp:88-99: one node per Next)
+            if (cur == blk && v.x == key) {
+              ++nh;
+              if (WORDS && r0 < 32u) mm |= 1u << r0;
+            }
+            if (blk + 1u < lim && v.y == key) {
+              ++nh;
+              if (WORDS && r0 + 1u < 32u) mm |= 1u << (r0 + 1u);
+            }
+            // distinct build keys: a row's only match ends its walk (its word's rounds are the
+            // chain's length from the record, and no later node can match)
+            cur = fm && nh ? lim : blk + 2u;
+          }
+        }
+        if (WORDS) {
+          if (live) {
+            const uint32_t len = lim - st;
+            const uint32_t word =
+                len <= kMmRounds ? (mm & ((1u << kMmRounds) - 1u)) | len << kMmRounds : kMmLong | len;
+            const uint64_t at = c * chunk + u0 + row;
+            if (p.w16) __builtin_nontemporal_store(round_word16(word), (uint16_t *)p.out_w + at);
+            else __builtin_nontemporal_store(word, p.out_w + at);
+          }
+        } else {  // append the matches: one atomic per wave and pass on the chunk's count
+          const uint32_t incl = wave_incl_scan(nh);
+          const uint32_t tot = (uint32_t)__shfl((int)incl, kWave - 1);
+          if (tot) {
+            uint32_t ob = 0;
+            if (lane == 0) ob = atomicAdd(p.out_count + c, tot);
+            // (a row's matches <= its chain's length < 256 with 8-byte records, so the wave's
+            // total < 2^16; tables without them append at once)
+            if (!kFiltDefer || qb + kFiltQ < qn || !rec8) {  // not the unit's last pass: append now
+              append(c, u0, ob, incl - nh, nh, row, key);
+            } else {  // the last pass: append after the next unit's records
+              dtot = tot;
+              dc = c;
+              du0 = u0;
+              dob = ob;
+              dw = (incl - nh) << 16 | nh << 8 | row;
+              dkey = key;
+            }
+          }
         }
       }
 #pragma unroll
       for (int j = 0; j < (int)kJ; ++j) kk[j] = kn[j];
+      g = gn;
+      r = rn;
       c = cn;
       u0 = u0n;
       uend = uendn;
     }
+    if (!WORDS && dtot) append(dc, du0, dob, dw >> 16, (dw >> 8) & 0xFFu, dw & 0xFFu, dkey);  // the partition's last unit
   }
 }
 
 __global__ __launch_bounds__(kFiltThreads, 6) void probe_chain_filt(ProbeParams p) {
   __shared__ uint32_t s_f[kFiltMaxWords];  // the partition's filter (64 KiB)
-  chain_filt_body<false, kFiltThreads>(p, s_f);
+  __shared__ FiltQueue<false> s_q[kFiltThreads / kWave];
+  chain_filt_body<false, kFiltThreads>(p, s_f, s_q);
 }
-__global__ __launch_bounds__(kFiltWordThreads) void chain_words_filt(ProbeParams p) {
+__global__ __launch_bounds__(kFiltWordThreads, 6) void chain_words_filt(ProbeParams p) {
   __shared__ uint32_t s_f[kFiltMaxWords];
-  chain_filt_body<true, kFiltWordThreads>(p, s_f);
+  __shared__ FiltQueue<true> s_q[kFiltWordThreads / kWave];
+  chain_filt_body<true, kFiltWordThreads>(p, s_f, s_q);
 }
 
 // The filter walks apply to the fixed-capacity split's segments of >= 8 partitions of <= 2^18
@@ -2929,7 +3045,7 @@ hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
     if (!p.bucket) return hipErrorInvalidValue;  // every chaining table carries bucket records
     // the LDS bucket filter walk (probe_chain_filt) for the fixed-capacity split's segments, when the
     // table has a filter, the partitions are at most 2^18 buckets and there are >= 8 of them (one
-    // XCD's range each), the chunk is a multiple of 512 rows and no rounds are asked for; the
+    // XCD's range each), the chunk is a multiple of 256 rows and no rounds are asked for; the
     // overflow area's chunks (key skew) go to probe_chain_win
     if (chain_filt_applies(p, kFiltUnit) && !p.out_rounds && ccj_tune_int("CCJ_CHAIN_FILT", 1)) {
       hipError_t e = hipMemsetAsync(p.out_count, 0, p.n_chunks * sizeof(uint32_t), s);
@@ -3127,7 +3243,7 @@ hipError_t launch_ordered_walk(int kind, const ProbeParams &p, hipStream_t s) {
   if (kind == CCJ_TABLE_CHAIN) {
     if (!p.bucket) return hipErrorInvalidValue;  // every chaining table carries bucket records
     if (chain_filt_applies(p, kFiltUnit) && ccj_tune_int("CCJ_CHAIN_FILT", 1)) {  // the bucket filter in LDS
-      const uint32_t grid = std::max<uint32_t>(8u, stream_cus(s) / 8 * 8);
+      const uint32_t grid = std::max<uint32_t>(8u, 2 * stream_cus(s) / 8 * 8);  // two workgroups per CU
       hipLaunchKernelGGL(chain_words_filt, dim3(grid), dim3(kFiltWordThreads), 0, s, p);
       ProbeParams q = p;  // the overflow area's chunks, in plain order
       q.chunk0 = p.ovf_base / p.chunk;

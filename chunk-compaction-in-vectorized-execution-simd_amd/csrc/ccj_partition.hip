@@ -248,7 +248,7 @@ __global__ void grouped_counts(const uint32_t *cur, uint32_t parts, uint64_t *ou
 }  // namespace
 
 // cursors, then the pipelined split's sink
-static size_t grouped_cursor_bytes(uint32_t parts) { return (((size_t)parts * 8 + 1) * 4 + 255) & ~(size_t)255; }
+static size_t grouped_cursor_bytes(uint32_t parts) { return (((size_t)parts * 8 + 8) * 4 + 255) & ~(size_t)255; }
 size_t partition_grouped_workspace(uint32_t parts) { return grouped_cursor_bytes(parts) + kSplitSinkBytes; }
 
 uint64_t partition_grouped_sub_cap(uint64_t n, uint32_t parts, uint32_t chunk) {
@@ -288,7 +288,7 @@ hipError_t launch_partition_grouped(const int64_t *keys, uint64_t n, uint32_t pa
     e = launch_owner_split_small(keys, n, parts, shift, sub_cap, cur, out_keys, out_rows, status, row_base,
                                  (char *)ws + grouped_cursor_bytes(parts), s);
   } else {
-    e = launch_slot_split_fixed(keys, n, pl, sub_cap, 0, 0, cur, out_keys, out_rows, status, s, nullptr, 0,
+    e = launch_slot_split_fixed(keys, n, pl, sub_cap, 0, 0, 0, cur, out_keys, out_rows, status, s, nullptr, 0,
                                 nullptr, nullptr, row_base, shift, wgs, (char *)ws + grouped_cursor_bytes(parts));
   }
   if (e) return e;
@@ -464,9 +464,10 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
       uint32_t olim = 0, r2 = 0;
       if (lim < h) {  // the rest of the run goes to the shared overflow area (key skew)
         const uint32_t extra = h - lim;
-        r2 = atomicAdd(&cur[(uint64_t)parts * 8], extra);
+        r2 = atomicAdd(&cur[(uint64_t)parts * 8 + g], extra);  // group g's overflow sub-area
         olim = r2 >= ovf_cap ? 0u : (uint32_t)(ovf_cap - r2 < extra ? ovf_cap - r2 : extra);
         dropped |= olim < extra;
+        r2 += g * (uint32_t)ovf_cap;
       }
       s_ovf[tid] = r2;
       s_olim[tid] = olim;
@@ -688,11 +689,12 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
       const uint64_t seg = (uint64_t)ptid * 8 + g;
       const uint32_t lim = r >= cap ? 0u : (uint32_t)(cap - r < h ? cap - r : h);
       uint32_t olim = 0, r2 = 0;
-      if (lim < h) {  // the rest of the run goes to the shared overflow area (key skew)
+      if (lim < h) {  // the rest of the run goes to group g's overflow sub-area (key skew)
         const uint32_t extra = h - lim;
-        r2 = atomicAdd(&cur[(uint64_t)parts * 8], extra);
+        r2 = atomicAdd(&cur[(uint64_t)parts * 8 + g], extra);
         olim = r2 >= ovf_cap ? 0u : (uint32_t)(ovf_cap - r2 < extra ? ovf_cap - r2 : extra);
         dropped |= olim < extra;
+        r2 += g * (uint32_t)ovf_cap;  // (the sub-area's place in the overflow area)
       }
       const uint64_t dadj = seg * cap + r - loc;  // mod 2^64: + the image index gives the dest
       s_rec[tid] = make_uint4((uint32_t)dadj, (uint32_t)(dadj >> 32), loc + lim, loc + lim + olim);
@@ -748,7 +750,7 @@ static hipError_t launch_owner_split_small(const int64_t *keys, uint64_t n, uint
                                           uint32_t *status, uint32_t row_base, void *sink, hipStream_t s) {
   constexpr int kT = 256, kPer = 8;
   constexpr uint32_t kTile = (uint32_t)kT * kPer;
-  hipError_t e = hipMemsetAsync(cur, 0, ((size_t)parts * 8 + 1) * 4, s);
+  hipError_t e = hipMemsetAsync(cur, 0, ((size_t)parts * 8 + 8) * 4, s);
   if (e || n == 0) return e;
   const uint64_t n_tiles = (n + kTile - 1) / kTile;
   // per_cu = 0: one workgroup per tile (not persistent), so that workgroups dispatched late —
@@ -787,7 +789,7 @@ uint32_t slot_split_tile_keys(uint32_t parts, bool runs) {
 }
 
 hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPlan &pl, uint64_t cap,
-                                   uint64_t ovf_base, uint64_t ovf_cap, uint32_t *cursors, int64_t *out_keys,
+                                   uint64_t ovf_base, uint64_t ovf_cap, uint64_t ovf_sub, uint32_t *cursors, int64_t *out_keys,
                                    uint32_t *out_rows, uint32_t *status, hipStream_t s, const uint32_t *counts,
                                    uint32_t chunk, uint2 *runs, uint32_t *ovf_runs, uint32_t row_base,
                                    uint32_t shift, uint32_t wgs, void *sink) {
@@ -795,7 +797,7 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
   // counts: a tile's chunks (tile / chunk + 2 at most) fit one count per thread
   if (counts && (chunk == 0 || slot_split_tile_keys(parts, runs != nullptr) / chunk + 2 > (uint32_t)kSplitThreads))
     return hipErrorInvalidValue;
-  hipError_t e = hipMemsetAsync(cursors, 0, ((size_t)parts * 8 + 1) * 4, s);
+  hipError_t e = hipMemsetAsync(cursors, 0, ((size_t)parts * 8 + 8) * 4, s);
   if (e || n == 0) return e;
   // One persistent 1024-thread workgroup per CU (<= 149 KB of LDS), a multiple of 8 (one tile group
   // per XCD).  Two 512-thread workgroups per CU on 6144-key tiles (same run length at 512
@@ -820,9 +822,10 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
   // the pipelined form needs a sink for its inactive lanes' stores: 64 positions of the overflow
   // area (8 per XCD group), or the caller's kSplitSinkBytes
   if ((ovf_cap >= 128 || sink) && ccj_tune_int("CCJ_SPLIT_PIPE", 1)) {
-    const uint64_t oc = sink ? ovf_cap : ovf_cap - 64;
-    int64_t *sink_k = sink ? (int64_t *)sink : out_keys + ovf_base + oc;
-    uint32_t *sink_r = sink ? (uint32_t *)((char *)sink + kSplitSinkBytes / 16 * 8) : out_rows + ovf_base + oc;
+    // (the 8 overflow sub-areas of ovf_sub positions end at least 64 positions before the area's end)
+    const uint64_t oc = ovf_sub;
+    int64_t *sink_k = sink ? (int64_t *)sink : out_keys + ovf_base + ovf_cap - 64;
+    uint32_t *sink_r = sink ? (uint32_t *)((char *)sink + kSplitSinkBytes / 16 * 8) : out_rows + ovf_base + ovf_cap - 64;
 #define CCJ_PIPE_LAUNCH(C, MAXP, P)                                                                                   \
   do {                                                                                                              \
     if (runs)                                                                                                       \
@@ -882,7 +885,7 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
   }
 #define CCJ_SPLIT_LAUNCH(C, MAXP, P)                                                                              \
   hipLaunchKernelGGL((slot_split_fixed<C, kSplitThreads, MAXP, P>), dim3(grid), dim3(kSplitThreads), 0, s, keys, n,      \
-                     shift, parts, n_tiles, cursors, cap, ovf_base, ovf_cap, out_keys, out_rows, status, ablate,         \
+                     shift, parts, n_tiles, cursors, cap, ovf_base, ovf_sub, out_keys, out_rows, status, ablate,         \
                      counts, chunk, runs, ovf_runs, row_base)
   if (parts > kSplitParts / 2) {  // 1024 partitions: 10 keys per thread
     if (counts) CCJ_SPLIT_LAUNCH(true, kSplitParts, 10);

@@ -312,14 +312,15 @@ def test_device_build_reports_exact_max_dup(kind):
 @pytest.mark.parametrize("n_build,cf,n_probe,rng", [(1 << 20, 1, 1 << 22, 1 << 21), (1 << 18, 3, 1 << 21, 1 << 19),
                                                     (3000, 2, 40000, 9000), (1 << 22, 3, 3 << 21, 3 << 22),
                                                     (1 << 21, 1, (1 << 22) + 4097, 10 << 21),
-                                                    (5 << 20, 2, 1 << 23, 5 << 20)])
+                                                    (5 << 20, 2, 1 << 23, 5 << 20), (1 << 20, 2, 1 << 22, 1 << 20)])
 def test_partitioned_chaining_probe_l1_l2(n_build, cf, n_probe, rng, exact):
     """Bucket-range-partitioned chaining probe — exact L1 + L2 against the membership answer,
     duplicates and misses included.  Tables of >= 8 partitions take probe_chain_filt (the
     partition's 2-bit bucket filter in LDS, quarter-chunk work units, the overflow area by
     probe_chain_win); smaller ones and the exact split probe_chain_win alone (bucket record, then
     2-key windows of the CSR chain).  Shapes: 8 / 32 / 64 partitions, 90 % misses, ragged last
-    chunk, cf 2 / 3."""
+    chunk, cf 2 / 3, and every row a hit (all 256 rows of a filter-walk unit in its chain queue:
+    four queue passes per unit)."""
     table = ccj.Table.reference(ccj.CHAIN, n_build, cf, ccj.LAYOUT_DEVICE)
     keys = ccj.gen_uniform_keys(n_probe, 23, rng)
     out = table.probe_partitioned(keys, 2048, exact=exact)
