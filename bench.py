@@ -323,8 +323,10 @@ def bench_c3(args, dev, stream):
             ev[1].record(stream)
         if pe:
             ccj.PhaseEvents.disarm()
+        # the carried probe column is the join key: filled from the payload (equal on every match;
+        # include/ccj.h ccj_compact_args.key_cols) — the gathered form is timed beside (untimed here)
         comp = ccj.compact(comp_in if part_mode else out, chunk, cols=[pkeys if part_mode else keys], rows=True,
-                           stream=stream)
+                           stream=stream, key_cols=[0])
         if ev:
             ev[2].record(stream)
 
@@ -342,9 +344,22 @@ def bench_c3(args, dev, stream):
     wall = time.perf_counter() - t0
     probe_ms = sum(a.elapsed_time(b) for a, b, _ in evs) / args.steps
     comp_ms = sum(b.elapsed_time(c) for _, b, c in evs) / args.steps
+    # the general compaction (every carried column gathered through the selection vector, as
+    # DataChunk::Append does), timed after the steps on the last step's probe output
+    gev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(2)) for _ in range(3)]
+    for a, b in gev:
+        a.record(stream)
+        g = ccj.compact(comp_in if part_mode else out, chunk, cols=[pkeys if part_mode else keys], rows=True,
+                        stream=stream)
+        b.record(stream)
+    stream.synchronize()
+    comp_gather_ms = min(a.elapsed_time(b) for a, b in gev)
     phases = phase_report(pev, args.path)
     phases["compaction_ms"] = comp_ms
-    phases["kernels"]["compaction"] = "ccj_compact (NaiveCompactor closed form: scans + copy_rows_flat)"
+    phases["compaction_gather_ms"] = comp_gather_ms
+    phases["kernels"]["compaction"] = ("ccj_compact (NaiveCompactor closed form: scans + copy_rows_flat; the "
+                                       "carried join-key column filled from the payload, key_cols)")
+    phases["kernels"]["compaction_gather"] = "ccj_compact with the key column gathered by sel (DataChunk::Append's form)"
     if part_mode:
         phases["kernels"]["match_tuples_and_advance_pointers"] = "probe_chain_win<3> (bucket records, 2-key windows)"
         phases["kernels"]["gather_tuples"] = "— (the walk writes each match's payload)"
@@ -366,6 +381,9 @@ def bench_c3(args, dev, stream):
         c_rows = part["row_map"].to(torch.int64)[c_rows]
     n_comp = int(idx.numel())
     key_ok = bool(torch.equal(c_key, c_pay))  # the carried key column == the matched key
+    # the gathered form (DataChunk::Append through sel) gives the same key column, row for row
+    g_ok = int(g["n"].item()) == n_oc and bool(torch.equal(g["cols"][0][idx], c_key))
+    del g
     comp_l2 = None
     if not args.no_verify:  # checker only (the oracle's L2 term), untimed
         from oracle import oracle as O
@@ -374,7 +392,8 @@ def bench_c3(args, dev, stream):
     examined, _, walked, windows = table.probe_cost_walk(keys, stream=stream)
     parity = {"status_flags": int(out["status"].item()) | int(comp["status"].item()), "matches": matches,
               "l2": hex(l2), "compacted_rows": n_comp, "compacted_l2": None if comp_l2 is None else hex(comp_l2),
-              "compaction_keeps_all": n_comp == matches and key_ok and comp_l2 in (None, l2)}
+              "compaction_keeps_all": n_comp == matches and key_ok and comp_l2 in (None, l2),
+              "gathered_key_column_equal": g_ok}
     cpu = None
     if not args.no_verify or not args.no_cpu:
         from oracle import oracle as O

@@ -64,7 +64,7 @@ class CompactArgs(C.Structure):
                 ("cols", C.c_void_p * 16), ("out_cols", C.c_void_p * 16), ("out_payload", C.c_void_p),
                 ("out_row", C.c_void_p), ("out_chunk_counts", C.c_void_p), ("out_cap_rows", C.c_uint64),
                 ("out_n_chunks", C.c_void_p), ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t),
-                ("status", C.c_void_p)]
+                ("status", C.c_void_p), ("key_cols", C.c_uint32)]
 
 
 EXPORTS = ["ccj_last_error", "ccj_abi_version", "ccj_device_init", "ccj_table_build_reference",
@@ -537,12 +537,14 @@ class Table:
 
 
 def compact(probe_out, chunk: int, cols=(), payload: bool = True, rows: bool = True, stream=None,
-            threshold: int = 0):
+            threshold: int = 0, key_cols=()):
     """Device compaction of a probe output's Next results (include/ccj.h ccj_compact).
 
     Returns dict(n_chunks (int), counts, cols [list], payload, row, status) — dense output chunks of
     `chunk` rows in the (fixed) NaiveCompactor order; with threshold T, results of >= T rows pass
-    through as their own chunk (0 = chunk: NaiveCompactor).
+    through as their own chunk (0 = chunk: NaiveCompactor).  key_cols: indices of `cols` that are
+    the probe's join-key column — filled from the payload (equal on every equi-join match) instead
+    of gathered (include/ccj.h ccj_compact_args.key_cols).
     """
     import torch
     dev = probe_out["count"].device
@@ -571,8 +573,9 @@ def compact(probe_out, chunk: int, cols=(), payload: bool = True, rows: bool = T
     a.n_chunks, a.cap, a.max_rounds, a.chunk = n_chunks, cap, probe_out["max_rounds"], chunk
     a.n_cols = len(cols)
     a.threshold = threshold
+    a.key_cols = sum(1 << k for k in key_cols)
     for i, col in enumerate(cols):
-        a.cols[i] = col.data_ptr()
+        a.cols[i] = col.data_ptr() if col is not None else None
         a.out_cols[i] = o["cols"][i].data_ptr()
     a.out_payload = o["payload"].data_ptr() if payload else None
     a.out_row = o["row"].data_ptr() if rows else None

@@ -954,8 +954,11 @@ int ccj_compact(const ccj_compact_args *a, ccj_stream stream) {
   if (!a->count || !a->sel || !a->rounds || !a->round_counts || !a->out_chunk_counts || !a->workspace)
     return fail(CCJ_ERR_INVALID, "ccj_compact: missing buffer (round counts are required)");
   if (a->out_payload && !a->payload) return fail(CCJ_ERR_INVALID, "ccj_compact: out_payload needs payload");
+  if (a->key_cols >> a->n_cols) return fail(CCJ_ERR_INVALID, "ccj_compact: key_cols names a column past n_cols");
+  if (a->key_cols && !a->payload) return fail(CCJ_ERR_INVALID, "ccj_compact: key_cols needs payload");
   for (uint32_t q = 0; q < a->n_cols; ++q)
-    if (!a->cols[q] || !a->out_cols[q]) return fail(CCJ_ERR_INVALID, "ccj_compact: null column");
+    if ((!a->cols[q] && !((a->key_cols >> q) & 1u)) || !a->out_cols[q])
+      return fail(CCJ_ERR_INVALID, "ccj_compact: null column");
   if (a->workspace_bytes < ccj::compact_workspace(a->n_chunks, a->cap, a->chunk, a->max_rounds, a->threshold))
     return fail(CCJ_ERR_INVALID, "ccj_compact: workspace too small");
   HIP_TRY(ccj::launch_compact(*a, (hipStream_t)stream), "compact launch");

@@ -121,7 +121,8 @@ __global__ __launch_bounds__(256) void copy_rows_flat(CompactParams p) {
         }
         if (dest >= cap_rows) continue;
         const uint64_t row = c * B + p.a.sel[src + j];
-        for (uint32_t q = 0; q < p.a.n_cols; ++q) p.a.out_cols[q][dest] = p.a.cols[q][row];
+        for (uint32_t q = 0; q < p.a.n_cols; ++q)
+          p.a.out_cols[q][dest] = (p.a.key_cols >> q) & 1u ? p.a.payload[src + j] : p.a.cols[q][row];
         if (p.a.out_payload) p.a.out_payload[dest] = p.a.payload[src + j];
         if (p.a.out_row) p.a.out_row[dest] = row;
       }
@@ -176,7 +177,9 @@ __global__ __launch_bounds__(256) void copy_rows_flat(CompactParams p) {
     }
     if (dest >= cap_rows) continue;
     const uint64_t row = c * B + p.a.sel[obase + m];
-    for (uint32_t q = 0; q < p.a.n_cols; ++q) p.a.out_cols[q][dest] = p.a.cols[q][row];
+    // (a join-key column equals the payload on every output row: read densely, not gathered)
+    for (uint32_t q = 0; q < p.a.n_cols; ++q)
+      p.a.out_cols[q][dest] = (p.a.key_cols >> q) & 1u ? p.a.payload[obase + m] : p.a.cols[q][row];
     if (p.a.out_payload) p.a.out_payload[dest] = p.a.payload[obase + m];
     if (p.a.out_row) p.a.out_row[dest] = row;
   }

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CCJ_ABI_VERSION 12  /* 12: chaining tables built on the device (stable bucket sort), ccj_table_get_arrays; 11: the rank walk in the tuning build only; 10: CCJ_PART_ROWS with positions / payload columns; 9: CCJ_PART_SHARE, CU-masked streams; 8: CCJ_PART_RANK; 7: CCJ_PART_ROWS */
+#define CCJ_ABI_VERSION 13  /* 13: ccj_compact_args.key_cols, per-XCD overflow sub-areas of the partitioned layout; 12: chaining tables built on the device (stable bucket sort), ccj_table_get_arrays; 11: the rank walk in the tuning build only; 10: CCJ_PART_ROWS with positions / payload columns; 9: CCJ_PART_SHARE, CU-masked streams; 8: CCJ_PART_RANK; 7: CCJ_PART_ROWS */
 
 enum ccj_status {
   CCJ_OK = 0,
@@ -290,6 +290,11 @@ int ccj_probe_partitioned(const ccj_table *table, const ccj_probe_args *args, ui
  * Output: dense chunks of `chunk` rows: out_cols[k] = input column k at the matched row,
  * out_payload = the probe payload (reference result column m+1; column m is never written by the
  * reference and is not materialised), out_row = global probe row (c*chunk + sel).
+ * key_cols: bit k says input column k is the probe's join-key column.  The join is an equi-join
+ * and the payload is the matched build key, so on every output row that column equals the
+ * payload: it is filled from the (dense) payload instead of gathered through the selection
+ * vector — same output, without reading a 10 %-dense gather's whole lines of the key column
+ * (cols[k] may then be NULL; needs payload).
  * Needs out_round_counts from the probe (the Next boundaries). */
 #define CCJ_MAX_COLS 16
 typedef struct ccj_compact_args {
@@ -314,6 +319,7 @@ typedef struct ccj_compact_args {
   void *workspace;              /* device scratch of ccj_compact_workspace_size(...) bytes */
   size_t workspace_bytes;
   uint32_t *status;             /* device word (ccj_flag bits) or NULL */
+  uint32_t key_cols;            /* bit k: column k is the join key (filled from payload; see above) */
 } ccj_compact_args;
 
 size_t ccj_compact_workspace_size(uint64_t n_chunks, uint64_t cap, uint32_t chunk, uint32_t max_rounds,

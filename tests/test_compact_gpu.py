@@ -130,3 +130,31 @@ def test_threshold_gated_compaction(kind, chunk, threshold):
     assert np.array_equal(comp["payload"].cpu().numpy()[:n_out * chunk][valid], want_pay[valid])
     assert np.array_equal(comp["cols"][0].cpu().numpy()[:n_out * chunk][valid], want_cols[0][valid])
     assert valid.sum() == total
+
+
+@pytest.mark.parametrize("kind", [ccj.LP, ccj.CHAIN])
+@pytest.mark.parametrize("chunk,cf", [(256, 1), (2048, 3), (1000, 2)])
+def test_compact_join_key_column_from_payload(kind, chunk, cf):
+    """key_cols: the carried join-key column filled from the payload (probe key == build key on
+    every match of the equi-join) equals the gathered one row for row; a NULL source column is
+    accepted for it, and the other carried columns are still gathered."""
+    bkeys = ref_keys(30000, cf)
+    n_probe = 40 * chunk + 5
+    keys = O.uniform_keys(chunk + cf, 0, n_probe, 45000)
+    extra = np.arange(n_probe, dtype=np.int64) * 7 - 3
+    table = ccj.Table.from_host(kind, bkeys)
+    dkeys, dext = torch.from_numpy(keys).cuda(), torch.from_numpy(extra).cuda()
+    out = table.probe(dkeys, chunk)
+    g = ccj.compact(out, chunk, cols=[dkeys, dext])
+    k = ccj.compact(out, chunk, cols=[dkeys, dext], key_cols=[0])
+    z = ccj.compact(out, chunk, cols=[None, dext], key_cols=[0])
+    torch.cuda.synchronize()
+    n = int(g["n"].item())
+    assert n > 0 and int(k["n"].item()) == n and int(z["n"].item()) == n
+    cnt = g["counts"][:n].to(torch.int64)
+    valid = (torch.arange(chunk, device=cnt.device)[None, :] < cnt[:, None]).reshape(-1)
+    for o in (k, z):
+        assert int(o["status"].item()) == 0
+        for q in range(2):
+            assert torch.equal(o["cols"][q][:n * chunk][valid], g["cols"][q][:n * chunk][valid])
+        assert torch.equal(o["payload"][:n * chunk][valid], g["payload"][:n * chunk][valid])
