@@ -959,6 +959,10 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
                                            n_build_total, 1, threads=args.cpu_threads)
                     wm_, wl_ = wm_ + a, (wl_ + b) % (1 << 64)
             resolved.update(l1_ok=wm_ == resolved["matches"], l2_ok=hex(wl_) == resolved["l2"])
+    # the local probe alone (untimed steps over): the run's last group re-probed with nothing else
+    # on the device, the slowest rank's — its own time beside the busy time shared with the other
+    # two streams (the local probe against the single-GPU probe of the same table)
+    probe_alone = slowest(sp.probe_alone_ms()) if not exact_fallback else None
     # verification (untimed): global L1 / L2 against the exact membership answer
     m, l2 = sp.step(keys, rank * n_probe, verify=True)
     examined, received = 0, 0
@@ -999,6 +1003,8 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
             # per step, slowest rank; the three streams overlap, so these are busy times, not a sum
             "partition_ms": phase["partition_ms"], "exchange_ms": phase["exchange_ms"],
             "local_probe_ms": probe_ms,
+            "local_probe_alone_ms": probe_alone,
+            "local_probe_alone_rows": sp.group * sp.slots,
             "exchange": ("key-only all-to-all in timed steps (8 B per tuple + segment counts); each sender keeps its "
                          "rows per batch, so the held groups' matches are resolved to global rows after timing "
                          "(parity.timed_step_rows_resolved)"),

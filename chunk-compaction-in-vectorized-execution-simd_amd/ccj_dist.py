@@ -478,6 +478,28 @@ class ShardedProbe:
         o.synchronize()
         return m, l2, covered
 
+    def probe_alone_ms(self, reps: int = 3) -> float:
+        """After a run: the run's last group probed again with nothing else on the device (every
+        stream drained first) — the local probe's own time, beside `local_probe_ms`, which is its
+        busy time while the partition and exchange streams share the GPU.  Min over `reps`."""
+        o = self.ops
+        if self.last_exact:
+            raise RuntimeError("the last run fell back to the exact-size protocol")
+        o.synchronize()
+        g = self.n_groups - 1
+        first, _ = self._group_range(g)
+        gs = self._gslot((self._run_steps - 1) * self.batches + first)
+        best = None
+        for _ in range(reps):
+            a, b = o.event(True), o.event(True)
+            a.record(self.stream)
+            o.probe_group(self.rk[gs], self.cc[gs], self.parts[gs], self.outs[gs], self.chunk, self.stream)
+            b.record(self.stream)
+            o.synchronize()
+            t = a.elapsed_time(b)
+            best = t if best is None else min(best, t)
+        return best
+
     # ---- exact-size protocol (fallback for skewed keys), batch by batch, not overlapped ----
     def step_exact(self, keys, row_base: int, verify: bool = False):
         o = self.ops
