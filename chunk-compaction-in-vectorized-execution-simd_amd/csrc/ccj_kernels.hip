@@ -1418,10 +1418,6 @@ __global__ __launch_bounds__(kFlatThreads) void probe_chain_win(ProbeParams p) {
 constexpr int kFiltThreads = 768, kFiltWordThreads = 768;
 constexpr uint32_t kFiltUnit = 256;                  // rows per work unit (4 per lane)
 constexpr uint32_t kFiltQ = 64;                      // queue entries per wave (more: extra passes)
-#ifndef CCJ_FILT_DEFER
-#define CCJ_FILT_DEFER 0
-#endif
-constexpr bool kFiltDefer = CCJ_FILT_DEFER;  // matches appended one unit later (experiment: spills)
 constexpr uint32_t kFiltMaxWords = (1u << 18) / 16;  // 2 bits per bucket, windows <= 2^18 buckets
 __device__ __forceinline__ uint32_t filt_code_of(uint64_t h) { return 1u + (uint32_t)((h >> 40) & 1u); }
 
@@ -1437,8 +1433,23 @@ struct FiltQueue {  // one wave's chain rows of a unit
 // row's Next-round word at its position (the ordered probe, chain_words' output: the filter gives an
 // empty bucket's 0 rounds and a one-key chain's miss — 1 round, no match — without any read; a
 // passing row whose fingerprints rule its chain out has the chain's length in rounds, no match).
+// Chunk slots of the match walk (per workgroup, LDS): the workgroup takes whole chunks of the
+// partition (k, k + K, ...), its waves take their units in order from an LDS counter, and a chunk's
+// matches are counted in LDS — no device atomic per unit (that reply was a round trip in every
+// unit's critical path) — the unit that completes a chunk writes its count.  Slot m % kFiltSlots
+// serves the workgroup's m-th chunk; a wave whose unit belongs to a chunk more than kFiltSlots
+// ahead of the oldest unfinished one waits for that slot (gen) — the oldest chunk never waits.
+constexpr uint32_t kFiltSlots = 32;
+struct FiltSlots {
+  uint32_t next;                 // the workgroup's next unit
+  uint32_t cnt[kFiltSlots];      // matches of the slot's chunk so far
+  uint32_t done[kFiltSlots];     // its units finished
+  uint32_t gen[kFiltSlots];      // the chunk ordinal allowed to use the slot
+};
+
 template <bool WORDS, int NT>
-__device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *s_f, FiltQueue<WORDS> *s_q) {
+__device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *s_f, FiltQueue<WORDS> *s_q,
+                                                FiltSlots *s_s) {
   constexpr uint32_t kJ = kFiltUnit / kWave;  // rows per lane and unit
   constexpr uint32_t kWaves = NT / kWave;
   const uint32_t lane = threadIdx.x & (kWave - 1);
@@ -1450,6 +1461,7 @@ __device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *
   const uint32_t spc = (uint32_t)(p.seg_cap / chunk);  // chunks per segment
   const uint32_t upc = chunk / kFiltUnit;              // units per chunk (chunk: a multiple of kFiltUnit)
   const uint32_t ups = spc * upc;                      // units per segment
+  const uint32_t cpp = 8u * spc;                       // chunks per partition
   const bool cp2 = (chunk & (chunk - 1u)) == 0u;
   const uint32_t cl2 = (uint32_t)__builtin_ctz(chunk);
   const uint32_t wb = p.filt_wb;
@@ -1458,20 +1470,32 @@ __device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *
   const bool rec8 = p.bucket8 != nullptr;
   const bool fm = WORDS ? p.w16 != 0u : p.first_match != 0u;  // distinct build keys
   const uint32_t stride = K * kWaves;
+  // match walk: the workgroup's units, in order — j = m * upc + kk is unit kk of its m-th chunk
+  const uint32_t n_mine = k < cpp ? (cpp - k + K - 1) / K : 0u;  // the workgroup's chunks per partition
+  const uint32_t nu = n_mine * upc;
+  auto take = [&]() {  // wave-uniform: the workgroup's next unit
+    uint32_t j = 0;
+    if (lane == 0) j = atomicAdd(&s_s->next, 1u);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)j);
+  };
   for (uint32_t d = x * P / 8; d < (x + 1) * P / 8; ++d) {
-    __syncthreads();  // the previous partition's filter is no longer read
+    __syncthreads();  // the previous partition's filter and chunk slots are no longer used
     for (uint32_t w = threadIdx.x * 4; w < fwords; w += NT * 4)
       *reinterpret_cast<u32x4 *>(&s_f[w]) = *reinterpret_cast<const u32x4 *>(p.filt + (uint64_t)d * fwords + w);
+    if (!WORDS) {
+      if (threadIdx.x == 0) s_s->next = 0;
+      if (threadIdx.x < kFiltSlots) {
+        s_s->cnt[threadIdx.x] = 0;
+        s_s->done[threadIdx.x] = 0;
+        s_s->gen[threadIdx.x] = threadIdx.x;
+      }
+    }
     __syncthreads();
-    // unit r of segment d * 8 + g (wave-uniform, scalar): rows [r * kFiltUnit, + kFiltUnit) of the
-    // segment, i.e. chunk c, rows [u0, uend) of it (uend <= u0: nothing live); the segment holds
-    // seg_count[g * P + d] rows.  A wave's units are u = g * ups + r = k + K * wave + stride * i,
-    // (g, r) advanced without division.
-    auto unit = [&](uint32_t g, uint32_t r, uint64_t &c, uint32_t &u0, uint32_t &uend) {
-      const uint32_t pos = r * kFiltUnit;
-      const uint32_t ci = cp2 ? pos >> cl2 : pos / chunk;
+    // a unit (wave-uniform, scalar): chunk c, rows [u0, uend) of it (uend <= u0: nothing live), and
+    // (match walk) the workgroup's chunk ordinal m.  Segment d * 8 + g holds seg_count[g * P + d] rows.
+    auto unit_at = [&](uint32_t g, uint32_t ci, uint32_t kk, uint64_t &c, uint32_t &u0, uint32_t &uend) {
       c = (uint64_t)(d * 8u + g) * spc + ci;
-      u0 = pos - ci * chunk;
+      u0 = kk * kFiltUnit;
       const uint64_t fill = p.seg_count[g < 8u ? g * P + d : 0u];
       uint64_t live = g < 8u ? fill : 0u;
       live = live < p.seg_cap ? live : p.seg_cap;
@@ -1479,12 +1503,26 @@ __device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *
       const uint32_t phys = live > off ? (live - off < chunk ? (uint32_t)(live - off) : chunk) : 0u;
       uend = phys <= u0 ? u0 : (phys - u0 < kFiltUnit ? phys : u0 + kFiltUnit);
     };
+    // WORDS: the static order — a wave's units are u = g * ups + r = k + K * wave + stride * i,
+    // (g, r) advanced without division
     auto advance = [&](uint32_t &g, uint32_t &r, uint32_t by) {
       r += by;
       while (g < 8u && r >= ups) {
         r -= ups;
         ++g;
       }
+    };
+    auto unit_static = [&](uint32_t g, uint32_t r, uint64_t &c, uint32_t &u0, uint32_t &uend) {
+      const uint32_t pos = r * kFiltUnit;
+      const uint32_t ci = cp2 ? pos >> cl2 : pos / chunk;
+      unit_at(g, ci, r - ci * upc, c, u0, uend);
+    };
+    // match walk: unit j of the workgroup (valid: j < nu)
+    auto unit_dyn = [&](uint32_t j, uint64_t &c, uint32_t &u0, uint32_t &uend, uint32_t &m) {
+      const uint32_t jj = j < nu ? j : 0u;
+      m = jj / upc;
+      const uint32_t pc = k + K * m, g = pc / spc;
+      unit_at(j < nu ? g : 8u, pc - g * spc, jj - m * upc, c, u0, uend);
     };
     auto load_keys = [&](uint64_t c, uint32_t u0, uint32_t uend, int64_t(&kk)[kJ]) {
 #pragma unroll
@@ -1493,122 +1531,119 @@ __device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *
         kk[j] = __builtin_nontemporal_load(p.keys + c * chunk + (i < uend ? i : u0));
       }
     };
-    uint32_t g = 0, r = 0;
-    advance(g, r, k + K * wave);
+    uint32_t g = 0, r = 0, j = 0, m = 0;
     uint64_t c = 0;
     uint32_t u0 = 0, uend = 0;
-    unit(g, r, c, u0, uend);
+    bool more;
+    if (WORDS) {
+      advance(g, r, k + K * wave);
+      unit_static(g, r, c, u0, uend);
+      more = g < 8u;
+    } else {
+      j = take();
+      unit_dyn(j, c, u0, uend, m);
+      more = j < nu;
+    }
     int64_t kk[kJ], kn[kJ];
-    if (g < 8u) load_keys(c, u0, uend, kk);
-    // match walk: the last queue pass of a unit appends its matches one unit later — its atomic's
-    // reply then lands under the next unit's record wait instead of costing a round trip of its own
-    // (wave-uniform: dtot matches of chunk dc, rows from du0; per lane: dkey, dw = the matches of
-    // the wave's earlier lanes << 16 | the lane's matches << 8 | its row in the unit, and lane 0's
-    // atomic reply dob)
-    uint32_t dtot = 0, du0 = 0, dw = 0, dob = 0;
-    uint64_t dc = 0;
-    int64_t dkey = 0;
-    auto append = [&](uint64_t oc, uint32_t ou0, uint32_t ob0, uint32_t ex, uint32_t nh, uint32_t row, int64_t key) {
-      uint32_t ob = (uint32_t)__shfl((int)ob0, 0) + ex;
-      bool over = false;
-      const uint64_t obase = oc * p.cap;
-      for (uint32_t m = 0; m < nh; ++m, ++ob) {
-        if (ob < p.cap) {
-          p.out_sel[obase + ob] = ou0 + row;
-          if (p.out_payload) p.out_payload[obase + ob] = key;
-        } else {
-          over = true;
-        }
-      }
-      if (over && p.status) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
-    };
-    while (g < 8u) {
+    if (more) load_keys(c, u0, uend, kk);
+    while (more) {
       // filter, then the passing rows' bucket records
       uint32_t pass = 0, kfp[kJ], bk[kJ];
 #pragma unroll
-      for (int j = 0; j < (int)kJ; ++j) {
-        const uint32_t i = u0 + (uint32_t)j * kWave + lane;
-        const uint64_t h = murmurhash64((uint64_t)kk[j]);
+      for (int jj = 0; jj < (int)kJ; ++jj) {
+        const uint32_t i = u0 + (uint32_t)jj * kWave + lane;
+        const uint64_t h = murmurhash64((uint64_t)kk[jj]);
         const uint32_t bl = (uint32_t)h & wmask;
         const uint32_t code = (s_f[bl >> 4] >> ((bl & 15u) * 2u)) & 3u;
         const bool ps = (i < uend) & ((code == 3u) | (code == filt_code_of(h)));  // (no branches)
-        pass |= (ps ? 1u : 0u) << j;
-        bk[j] = (uint32_t)h & p.mask;
-        kfp[j] = ps ? bucket_fp(h) : code;  // (a rejected row keeps its code: 0 empty, else a one-key chain)
+        pass |= (ps ? 1u : 0u) << jj;
+        bk[jj] = (uint32_t)h & p.mask;
+        kfp[jj] = ps ? bucket_fp(h) : code;  // (a rejected row keeps its code: 0 empty, else a one-key chain)
       }
       uint64_t rec[kJ];
 #pragma unroll
-      for (int j = 0; j < (int)kJ; ++j) {
-        rec[j] = 0;
-        if ((pass >> j) & 1u) rec[j] = rec8 ? p.bucket8[bk[j]] : (uint64_t)p.bucket[bk[j]].x;
+      for (int jj = 0; jj < (int)kJ; ++jj) {
+        rec[jj] = 0;
+        if ((pass >> jj) & 1u) rec[jj] = rec8 ? p.bucket8[bk[jj]] : (uint64_t)p.bucket[bk[jj]].x;
       }
       // the next unit's keys, in flight during this unit's record and chain round trips
-      uint32_t gn = g, rn = r;
-      advance(gn, rn, stride);
+      uint32_t gn = g, rn = r, jn = 0, mn = 0;
       uint64_t cn = 0;
       uint32_t u0n = 0, uendn = 0;
-      unit(gn, rn, cn, u0n, uendn);
-      load_keys(gn < 8u ? cn : c, gn < 8u ? u0n : u0, gn < 8u ? uendn : uend, kn);
-      // slot j's chain range from its record: nodes [cur, lim) can still hold the key
-      auto range = [&](int j, uint32_t &st, uint32_t &cur, uint32_t &lim) {
-        const bool ps = (pass >> j) & 1u;
-        st = (uint32_t)rec[j];
-        const uint32_t len = rec8 ? (uint32_t)(rec[j] >> 32) & 0xFFu : (uint32_t)(rec[j] >> 32);
+      bool moren;
+      if (WORDS) {
+        advance(gn, rn, stride);
+        unit_static(gn, rn, cn, u0n, uendn);
+        moren = gn < 8u;
+      } else {
+        jn = take();
+        unit_dyn(jn, cn, u0n, uendn, mn);
+        moren = jn < nu;
+      }
+      load_keys(moren ? cn : c, moren ? u0n : u0, moren ? uendn : uend, kn);
+      // slot jj's chain range from its record: nodes [cur, lim) can still hold the key
+      auto range = [&](int jj, uint32_t &st, uint32_t &cur, uint32_t &lim) {
+        const bool ps = (pass >> jj) & 1u;
+        st = (uint32_t)rec[jj];
+        const uint32_t len = rec8 ? (uint32_t)(rec[jj] >> 32) & 0xFFu : (uint32_t)(rec[jj] >> 32);
         lim = ps ? st + len : 0u;
-        cur = ps ? (rec8 ? rec8_first(rec[j], kfp[j]) : st) : 0u;
+        cur = ps ? (rec8 ? rec8_first(rec[jj], kfp[jj]) : st) : 0u;
       };
       // queue index of every chain row (slot-major); WORDS: the other rows' words now, coalesced
-      uint64_t qm[kJ];  // wave-uniform: slot j's chain rows, and the queue index of its first
+      uint64_t qm[kJ];  // wave-uniform: slot jj's chain rows, and the queue index of its first
       uint32_t qs[kJ], qn = 0;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous unit's queue reads are done
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int j = 0; j < (int)kJ; ++j) {
+      for (int jj = 0; jj < (int)kJ; ++jj) {
         uint32_t st, cur, lim;
-        range(j, st, cur, lim);
+        range(jj, st, cur, lim);
         const bool act = cur < lim;
         const uint64_t bm = __ballot(act);
         const uint32_t qi = qn + lane_prefix(bm);
-        qm[j] = bm;
-        qs[j] = qn;
+        qm[jj] = bm;
+        qs[jj] = qn;
         qn += (uint32_t)__popcll(bm);
         if (act && qi < kFiltQ) {
-          q.key[qi] = kk[j];
+          q.key[qi] = kk[jj];
           q.cur[qi] = cur;
           q.lim[qi] = lim;
           if (WORDS) q.st[WORDS ? qi : 0] = st;
-          q.row[qi] = (uint8_t)((uint32_t)j * kWave + lane);
+          q.row[qi] = (uint8_t)((uint32_t)jj * kWave + lane);
         }
         if (WORDS) {
-          const uint32_t i = u0 + (uint32_t)j * kWave + lane;
+          const uint32_t i = u0 + (uint32_t)jj * kWave + lane;
           if (!act && i < uend) {
             const uint32_t len = lim - st;
-            const uint32_t word = (pass >> j) & 1u ? (len <= kMmRounds ? len << kMmRounds : kMmLong | len)
-                                                   : (kfp[j] == 0u ? 0u : 1u << kMmRounds);
+            const uint32_t word = (pass >> jj) & 1u ? (len <= kMmRounds ? len << kMmRounds : kMmLong | len)
+                                                    : (kfp[jj] == 0u ? 0u : 1u << kMmRounds);
             if (p.w16) __builtin_nontemporal_store(round_word16(word), (uint16_t *)p.out_w + c * chunk + i);
             else __builtin_nontemporal_store(word, p.out_w + c * chunk + i);
           }
         }
       }
-      if (!WORDS && dtot) {  // the previous unit's matches (its atomic replied before these records)
-        append(dc, du0, dob, dw >> 16, (dw >> 8) & 0xFFu, dw & 0xFFu, dkey);
-        dtot = 0;
+      // match walk: this unit's chunk slot (a chunk kFiltSlots ahead of an unfinished one waits)
+      const uint32_t slot = m % kFiltSlots;
+      if (!WORDS && m >= kFiltSlots) {
+        while ((uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(&s_s->gen[slot], __ATOMIC_RELAXED,
+                                                                              __HIP_MEMORY_SCOPE_WORKGROUP)) != m)
+          __builtin_amdgcn_s_sleep(2);
       }
       for (uint32_t qb = 0; qb < qn; qb += kFiltQ) {
         if (qb) {  // a unit with more than kFiltQ chain rows: the next kFiltQ of them
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
 #pragma unroll
-          for (int j = 0; j < (int)kJ; ++j) {
-            const uint32_t qi = qs[j] + lane_prefix(qm[j]), e = qi - qb;
-            if (((qm[j] >> lane) & 1u) && qi >= qb && e < kFiltQ) {
+          for (int jj = 0; jj < (int)kJ; ++jj) {
+            const uint32_t qi = qs[jj] + lane_prefix(qm[jj]), e = qi - qb;
+            if (((qm[jj] >> lane) & 1u) && qi >= qb && e < kFiltQ) {
               uint32_t st, cur, lim;
-              range(j, st, cur, lim);
-              q.key[e] = kk[j];
+              range(jj, st, cur, lim);
+              q.key[e] = kk[jj];
               q.cur[e] = cur;
               q.lim[e] = lim;
               if (WORDS) q.st[WORDS ? e : 0] = st;
-              q.row[e] = (uint8_t)((uint32_t)j * kWave + lane);
+              q.row[e] = (uint8_t)((uint32_t)jj * kWave + lane);
             }
           }
         }
@@ -1651,48 +1686,62 @@ __device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *
             if (p.w16) __builtin_nontemporal_store(round_word16(word), (uint16_t *)p.out_w + at);
             else __builtin_nontemporal_store(word, p.out_w + at);
           }
-        } else {  // append the matches: one atomic per wave and pass on the chunk's count
+        } else {  // append the matches: their places from the chunk's LDS count (one LDS atomic per pass)
           const uint32_t incl = wave_incl_scan(nh);
           const uint32_t tot = (uint32_t)__shfl((int)incl, kWave - 1);
           if (tot) {
             uint32_t ob = 0;
-            if (lane == 0) ob = atomicAdd(p.out_count + c, tot);
-            // (a row's matches <= its chain's length < 256 with 8-byte records, so the wave's
-            // total < 2^16; tables without them append at once)
-            if (!kFiltDefer || qb + kFiltQ < qn || !rec8) {  // not the unit's last pass: append now
-              append(c, u0, ob, incl - nh, nh, row, key);
-            } else {  // the last pass: append after the next unit's records
-              dtot = tot;
-              dc = c;
-              du0 = u0;
-              dob = ob;
-              dw = (incl - nh) << 16 | nh << 8 | row;
-              dkey = key;
+            if (lane == 0) ob = atomicAdd(&s_s->cnt[slot], tot);
+            ob = (uint32_t)__shfl((int)ob, 0) + incl - nh;
+            bool over = false;
+            const uint64_t obase = c * p.cap;
+            for (uint32_t e = 0; e < nh; ++e, ++ob) {
+              if (ob < p.cap) {  // (non-temporal: the partition's records and chains keep the L2)
+                __builtin_nontemporal_store(u0 + row, p.out_sel + obase + ob);
+                if (p.out_payload) __builtin_nontemporal_store(key, p.out_payload + obase + ob);
+              } else {
+                over = true;
+              }
             }
+            if (over && p.status) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
           }
         }
       }
+      if (!WORDS && lane == 0) {  // the unit is done; the chunk's last unit writes its count and frees the slot
+        // (this wave's LDS adds to cnt completed before this one: LDS operations of a wave are in order)
+        if (atomicAdd(&s_s->done[slot], 1u) == upc - 1u) {
+          const uint32_t total = atomicAdd(&s_s->cnt[slot], 0u);
+          p.out_count[c] = total < p.cap ? total : (uint32_t)p.cap;
+          if (total > p.cap && p.status) atomicOr(p.status, CCJ_FLAG_CAP_OVERFLOW);
+          s_s->cnt[slot] = 0;
+          s_s->done[slot] = 0;
+          __hip_atomic_store(&s_s->gen[slot], m + kFiltSlots, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
 #pragma unroll
-      for (int j = 0; j < (int)kJ; ++j) kk[j] = kn[j];
+      for (int jj = 0; jj < (int)kJ; ++jj) kk[jj] = kn[jj];
       g = gn;
       r = rn;
+      j = jn;
+      m = mn;
       c = cn;
       u0 = u0n;
       uend = uendn;
+      more = moren;
     }
-    if (!WORDS && dtot) append(dc, du0, dob, dw >> 16, (dw >> 8) & 0xFFu, dw & 0xFFu, dkey);  // the partition's last unit
   }
 }
 
 __global__ __launch_bounds__(kFiltThreads, 6) void probe_chain_filt(ProbeParams p) {
   __shared__ uint32_t s_f[kFiltMaxWords];  // the partition's filter (64 KiB)
   __shared__ FiltQueue<false> s_q[kFiltThreads / kWave];
-  chain_filt_body<false, kFiltThreads>(p, s_f, s_q);
+  __shared__ FiltSlots s_s;
+  chain_filt_body<false, kFiltThreads>(p, s_f, s_q, &s_s);
 }
 __global__ __launch_bounds__(kFiltWordThreads, 6) void chain_words_filt(ProbeParams p) {
   __shared__ uint32_t s_f[kFiltMaxWords];
   __shared__ FiltQueue<true> s_q[kFiltWordThreads / kWave];
-  chain_filt_body<true, kFiltWordThreads>(p, s_f, s_q);
+  chain_filt_body<true, kFiltWordThreads>(p, s_f, s_q, nullptr);
 }
 
 // The filter walks apply to the fixed-capacity split's segments of >= 8 partitions of <= 2^18

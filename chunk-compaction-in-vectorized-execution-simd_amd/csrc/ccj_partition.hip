@@ -567,9 +567,8 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
   };
   uint32_t have_prev = opaque_u32(0u), p_tl = 0;
   uint64_t p_t0 = 0;
-  auto stores = [&]() {
-#pragma unroll
-    for (int it = 0; it < PER; ++it) {
+  auto store_one = [&](int it) {
+    {
       const uint32_t q = (uint32_t)it * THREADS + tid;
       const int64_t k = s_k[q];
       const uint32_t si = s_i[q], d = (si >> 16) & (uint32_t)(MAXP - 1);
@@ -577,7 +576,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
       const uint64_t oadj = s_oadj[d];
       const bool act = have_prev && q < p_tl && q < rc.w;
       const uint64_t dest = q < rc.z ? (rc.x | (uint64_t)rc.y << 32) + q : oadj + q;
-      if CCJ_ABLATED(ablate, 0x10u) continue;  // (timing: no stores)
+      if CCJ_ABLATED(ablate, 0x10u) return;  // (timing: no stores)
       *(act ? out_k + dest : sink_k) = k;
       if constexpr (RUNS)  // the ordered probe: the row inside its tile (16 bits) at the entry's IMAGE index
         // (tile-major, sequential: the unsplit reads it with whole lines, not from the runs' partial ones)
@@ -588,6 +587,19 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
       __builtin_amdgcn_sched_barrier(0);  // keep the LDS reads of later entries below (registers)
     }
   };
+  auto stores = [&]() {
+#pragma unroll
+    for (int it = 0; it < PER; ++it) store_one(it);
+  };
+  // The previous tile's first KS entries are stored between the rankings of this tile's keys, so
+  // their issue overlaps the hash / LDS-atomic work; the rest after the segment reservations,
+  // which they hide as before.  C2, same box, interleaved 3x: all stores after the reservations
+  // 5.51-5.54 ms, KS = 7 4.76-4.77 (KS 4 / 10 on another box 4.90 / 4.94 against 4.84 at 7).
+  // (-DCCJ_SPLIT_KS=k builds other values for A/B; 0 = all after the reservations.)
+#ifndef CCJ_SPLIT_KS
+#define CCJ_SPLIT_KS 7
+#endif
+  constexpr int kKS = MAXP > 64 && CCJ_SPLIT_KS < PER ? CCJ_SPLIT_KS : 0;
 #ifdef CCJ_SPLIT_STORES16
   // (timing only, an experiment build (-DCCJ_SPLIT_STORES16): the same bytes stored as 16-byte stores — two keys / four rows
   // per lane at their first entry's destination, rounded down to 16 bytes: wrong layout; does the
@@ -624,6 +636,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
   bool dropped = false;
   auto step = [&](uint64_t t, int64_t(&kc)[PER], uint32_t cc, int64_t(&kn)[PER], uint32_t &cn) {
     load(t + bpg, kn, cn);  // kn held the previous tile's keys, already in its image: a whole step of latency
+    if (kKS) __syncthreads();  // (the previous image is complete before any of it is stored)
     const uint64_t t0 = t * kTileKeys;
     const uint32_t tn = tile_rows(t);
     uint32_t live = 0;
@@ -665,6 +678,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
         dr[it] = d | (lv ? rk : 0u) << 10;
       } else {
         dr[it] = d | ((live >> it) & 1u ? atomicAdd(&s_hist[d], 1u) : 0u) << 10;
+        if (it < kKS) store_one(it);
       }
     }
     __syncthreads();
@@ -677,7 +691,12 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
 #ifdef CCJ_SPLIT_STORES16
     stores16();
 #else
-    stores();
+    if (kKS) {
+#pragma unroll
+      for (int it = kKS; it < PER; ++it) store_one(it);
+    } else {
+      stores();
+    }
 #endif
     __syncthreads();  // the previous image is read; s_wsum is complete
     uint32_t wpre = 0;
