@@ -599,7 +599,11 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
 #ifndef CCJ_SPLIT_KS
 #define CCJ_SPLIT_KS 7
 #endif
-  constexpr int kKS = MAXP > 64 && CCJ_SPLIT_KS < PER ? CCJ_SPLIT_KS : 0;
+#ifndef CCJ_SPLIT_KS_OWNER
+#define CCJ_SPLIT_KS_OWNER 0  // (the owner split's ballot ranking: -DCCJ_SPLIT_KS_OWNER=k for A/B)
+#endif
+  constexpr int kKSw = MAXP > 64 ? CCJ_SPLIT_KS : CCJ_SPLIT_KS_OWNER;
+  constexpr int kKS = kKSw < PER ? kKSw : 0;
 #ifdef CCJ_SPLIT_STORES16
   // (timing only, an experiment build (-DCCJ_SPLIT_STORES16): the same bytes stored as 16-byte stores — two keys / four rows
   // per lane at their first entry's destination, rounded down to 16 bytes: wrong layout; does the
@@ -676,6 +680,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
         const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
         const uint32_t rk = (uint32_t)__shfl((int)base, (int)d) + below;
         dr[it] = d | (lv ? rk : 0u) << 10;
+        if (it < kKS) store_one(it);
       } else {
         dr[it] = d | ((live >> it) & 1u ? atomicAdd(&s_hist[d], 1u) : 0u) << 10;
         if (it < kKS) store_one(it);
