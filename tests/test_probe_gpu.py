@@ -252,9 +252,10 @@ def table_slots(table):
 
 @pytest.mark.parametrize("distinct", [1, 7, 3000])
 def test_partitioned_probe_skew_falls_back_to_exact(distinct):
-    """Heavy skew overflows the one-pass split's fixed segments: the ABI raises
-    FLAG_PART_OVERFLOW (rows dropped) and the wrapper re-runs with the exact split."""
-    n_build, n_probe = 1 << 20, 3 << 20
+    """Heavy skew overflows the one-pass split's fixed segments and then its overflow area (n/16
+    rows): the ABI raises FLAG_PART_OVERFLOW (rows dropped) and the wrapper re-runs with the exact
+    split.  A handful of distinct keys cannot fit; 3000 keys over 3·2^20 probes may."""
+    n_build, n_probe = 1 << 20, (1 << 24) if distinct <= 7 else 3 << 20
     table = ccj.Table.reference(ccj.LP, n_build, 1, ccj.LAYOUT_DEVICE)
     g = np.random.default_rng(distinct)
     vals = g.integers(0, 2 * n_build, size=distinct)
@@ -268,7 +269,7 @@ def test_partitioned_probe_skew_falls_back_to_exact(distinct):
     assert int(out["status"].item()) == 0
     assert bool(out.get("exact_retry")) == overflow
     if distinct <= 7:
-        assert overflow  # a handful of keys cannot spread over 1024 partitions x 8 groups
+        assert overflow  # a handful of keys cannot spread over the partitions' segments and the overflow area
     # expected answer by membership (reference generator: every key < n_build matches once)
     hit = keys_h < n_build
     rows = np.nonzero(hit)[0].astype(np.uint64)
