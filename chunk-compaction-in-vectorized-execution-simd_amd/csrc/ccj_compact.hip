@@ -132,6 +132,34 @@ __global__ __launch_bounds__(256) void copy_rows_flat(CompactParams p) {
     }
     return;
   }
+  const bool b2 = (B & (B - 1)) == 0;  // a power-of-two chunk (every bench chunk): shifts, not divisions
+  const uint32_t bl2 = (uint32_t)__builtin_ctzll(B);
+  const uint64_t obase = c * p.a.cap;
+  // One round (every chunk of the partitioned probe: its matches are one compactor input): round 0's
+  // values are wave-uniform — no scans or searches over the lanes.  The match's row and payload are
+  // read once, before any store (the stores may alias them for the compiler).
+  if (rounds <= 1) {
+    const uint32_t rc0 = rounds ? p.a.round_counts[c * p.a.max_rounds] : 0u;
+    const bool rb0 = rounds && p.bypass(rc0);
+    const uint64_t tr0 = p.nonfull[c], fb0 = (e_of(tr0, B) + p.full[c]) * B;
+    for (uint32_t m = lane; m < total; m += 64) {
+      uint64_t dest;
+      if (rb0) {
+        dest = fb0 + m;
+      } else {
+        const uint64_t u = tr0 + m, k = b2 ? u >> bl2 : u / B;
+        dest = (k + (F ? full_before(p, F, k) : 0)) * B + (u - k * B);
+      }
+      if (dest >= cap_rows) continue;
+      const uint64_t row = c * B + p.a.sel[obase + m];
+      const int64_t pay = p.a.payload[obase + m];
+      for (uint32_t q = 0; q < p.a.n_cols; ++q)
+        p.a.out_cols[q][dest] = (p.a.key_cols >> q) & 1u ? pay : p.a.cols[q][row];
+      if (p.a.out_payload) p.a.out_payload[dest] = pay;
+      if (p.a.out_row) p.a.out_row[dest] = row;
+    }
+    return;
+  }
   const uint32_t rc = lane < rounds ? p.a.round_counts[c * p.a.max_rounds + lane] : 0u;
   const bool byp = lane < rounds && p.bypass(rc);
   // exclusive prefixes over rounds: source offset, P-stream rows, pass-through results
@@ -151,7 +179,6 @@ __global__ __launch_bounds__(256) void copy_rows_flat(CompactParams p) {
   fs -= byp ? 1u : 0u;
   const uint64_t t_r = p.nonfull[c] + ps, f_r = p.full[c] + fs;
   const uint64_t fbase = (e_of(t_r, B) + f_r) * B;  // lane r's pass-through destination
-  const uint64_t obase = c * p.a.cap;
   // Every lane runs every iteration (cross-lane reads need the source lanes active).
   for (uint32_t m0 = 0; m0 < total; m0 += 64) {
     const uint32_t m = m0 + lane;
@@ -172,15 +199,16 @@ __global__ __launch_bounds__(256) void copy_rows_flat(CompactParams p) {
     if (rb) {
       dest = fb + j;
     } else {
-      const uint64_t u = tr + j, k = u / B;
+      const uint64_t u = tr + j, k = b2 ? u >> bl2 : u / B;
       dest = (k + (F ? full_before(p, F, k) : 0)) * B + (u - k * B);
     }
     if (dest >= cap_rows) continue;
     const uint64_t row = c * B + p.a.sel[obase + m];
+    const int64_t pay = p.a.payload[obase + m];
     // (a join-key column equals the payload on every output row: read densely, not gathered)
     for (uint32_t q = 0; q < p.a.n_cols; ++q)
-      p.a.out_cols[q][dest] = (p.a.key_cols >> q) & 1u ? p.a.payload[obase + m] : p.a.cols[q][row];
-    if (p.a.out_payload) p.a.out_payload[dest] = p.a.payload[obase + m];
+      p.a.out_cols[q][dest] = (p.a.key_cols >> q) & 1u ? pay : p.a.cols[q][row];
+    if (p.a.out_payload) p.a.out_payload[dest] = pay;
     if (p.a.out_row) p.a.out_row[dest] = row;
   }
 }
