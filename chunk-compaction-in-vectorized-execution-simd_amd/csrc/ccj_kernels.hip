@@ -3011,21 +3011,29 @@ __global__ __launch_bounds__(kBlock) void emit_ordered(ProbeParams p) {
 // 5.2 TB/s.  One binary search per thread over kPer consecutive entries (each load instruction then
 // spans ~kPer * 64 entries) measured 13.6 ms; tiles read in the split's XCD order 4.66 ms.
 constexpr int kUnsplitThreads = 1024;
+// Threads of the unsplit's workgroup when the partitions fit (one per thread in the runs' scan): 512
+// (32 KiB of LDS, four tiles in flight per CU instead of two) against 1024, same box, interleaved:
+// unsplit + emit 7.55 → 6.82 ms at C2 ordered (20.26 → 19.53 ms per step), 6.53-6.56 → 5.81-5.84 ms
+// at C3 ordered (profiles/r4_ab_r4ak_unsplit_nt.log); 256 threads leave C2 / C3's 512 partitions
+// to the 1024-thread form.
+#ifndef CCJ_UNSPLIT_NT
+#define CCJ_UNSPLIT_NT 512
+#endif
 constexpr uint32_t kUnsplitMaxTile = 13u * kUnsplitThreads;  // the split's largest tile (13 keys per thread)
 
-template <typename W>
-__global__ __launch_bounds__(kUnsplitThreads) void unsplit_words(const uint2 *runs, const uint32_t *ovf_runs,
+template <typename W, int NT>
+__global__ __launch_bounds__(NT) void unsplit_words(const uint2 *runs, const uint32_t *ovf_runs,
                                                                  const uint16_t *row_loc, const W *w_pos,
                                                                  W *w_row, uint64_t n, uint32_t parts,
                                                                  uint32_t tile, uint32_t *status) {
   __shared__ __attribute__((aligned(16))) W s_img[kUnsplitMaxTile];
-  __shared__ uint32_t s_loc[kUnsplitThreads + 1];
-  __shared__ uint2 s_run[kUnsplitThreads];
-  __shared__ uint32_t s_wsum[kUnsplitThreads / 64];
+  __shared__ uint32_t s_loc[NT + 1];
+  __shared__ uint2 s_run[NT];
+  __shared__ uint32_t s_wsum[NT / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint64_t t = blockIdx.x, t0 = t * tile;
   const uint32_t tn = (uint32_t)(n - t0 < tile ? n - t0 : tile);
-  for (uint32_t i = tid; i < tn; i += kUnsplitThreads) s_img[i] = 0;
+  for (uint32_t i = tid; i < tn; i += NT) s_img[i] = 0;
   const uint2 r = tid < parts ? runs[t * parts + tid] : make_uint2(0u, 0u);
   const uint32_t len = (r.y & 0xFFFFu) + (r.y >> 16);
   uint32_t incl = wave_incl_scan(len);
@@ -3044,11 +3052,11 @@ __global__ __launch_bounds__(kUnsplitThreads) void unsplit_words(const uint2 *ru
   // kU entries per thread per pass, all their loads in flight together (a load under `if`, or one
   // waiting on the previous entry's, made each entry two dependent round trips)
   constexpr uint32_t kU = 4;
-  for (uint32_t j0 = tid; j0 < total; j0 += kU * kUnsplitThreads) {
+  for (uint32_t j0 = tid; j0 < total; j0 += kU * NT) {
     uint64_t pos[kU];
 #pragma unroll
     for (uint32_t u = 0; u < kU; ++u) {
-      uint32_t j = j0 + u * kUnsplitThreads;
+      uint32_t j = j0 + u * NT;
       j = j < total ? j : total - 1;  // (a repeat of the last entry: the same word to the same row)
       uint32_t lo = 0, hi = parts;    // the last d with s_loc[d] <= j
       while (hi - lo > 1) {
@@ -3065,7 +3073,7 @@ __global__ __launch_bounds__(kUnsplitThreads) void unsplit_words(const uint2 *ru
     W wv[kU];
 #pragma unroll
     for (uint32_t u = 0; u < kU; ++u) {
-      const uint32_t j = j0 + u * kUnsplitThreads;
+      const uint32_t j = j0 + u * NT;
       rm[u] = row_loc[t0 + (j < total ? j : total - 1)];  // image order: consecutive, whole lines
       wv[u] = w_pos[pos[u]];
     }
@@ -3080,10 +3088,10 @@ __global__ __launch_bounds__(kUnsplitThreads) void unsplit_words(const uint2 *ru
   // 16-byte stores where the tile's rows start 16-byte aligned (round 2d), single words for the rest
   constexpr uint32_t kPer16 = 16 / sizeof(W);
   const uint32_t vec = ((t0 * sizeof(W)) % 16 == 0) ? tn / kPer16 * kPer16 : 0u;
-  for (uint32_t g = tid; g * kPer16 < vec; g += kUnsplitThreads)
+  for (uint32_t g = tid; g * kPer16 < vec; g += NT)
     __builtin_nontemporal_store(*reinterpret_cast<const u32x4 *>(&s_img[g * kPer16]),
                                 reinterpret_cast<u32x4 *>(w_row + t0 + g * kPer16));
-  for (uint32_t i = vec + tid; i < tn; i += kUnsplitThreads) __builtin_nontemporal_store(s_img[i], w_row + t0 + i);
+  for (uint32_t i = vec + tid; i < tn; i += NT) __builtin_nontemporal_store(s_img[i], w_row + t0 + i);
 }
 
 hipError_t launch_probe_flat(int kind, const ProbeParams &p, hipStream_t s) {
@@ -3315,11 +3323,22 @@ hipError_t launch_unsplit_words(const uint2 *runs, const uint32_t *ovf_runs, con
   if (n == 0) return hipSuccess;
   if (tile > kUnsplitMaxTile || parts > (uint32_t)kUnsplitThreads) return hipErrorInvalidValue;
   const uint64_t n_tiles = (n + tile - 1) / tile;
+  const dim3 grid((unsigned)n_tiles);
+  if (parts <= (uint32_t)CCJ_UNSPLIT_NT) {  // one partition per thread in the runs' scan
+    constexpr int NT = CCJ_UNSPLIT_NT;
+    if (w16)
+      hipLaunchKernelGGL((unsplit_words<uint16_t, NT>), grid, dim3(NT), 0, s, runs, ovf_runs, row_loc,
+                         (const uint16_t *)w_pos, (uint16_t *)w_row, n, parts, tile, status);
+    else
+      hipLaunchKernelGGL((unsplit_words<uint32_t, NT>), grid, dim3(NT), 0, s, runs, ovf_runs, row_loc,
+                         (const uint32_t *)w_pos, (uint32_t *)w_row, n, parts, tile, status);
+    return hipGetLastError();
+  }
   if (w16)
-    hipLaunchKernelGGL(unsplit_words<uint16_t>, dim3((unsigned)n_tiles), dim3(kUnsplitThreads), 0, s, runs, ovf_runs,
+    hipLaunchKernelGGL((unsplit_words<uint16_t, kUnsplitThreads>), grid, dim3(kUnsplitThreads), 0, s, runs, ovf_runs,
                        row_loc, (const uint16_t *)w_pos, (uint16_t *)w_row, n, parts, tile, status);
   else
-    hipLaunchKernelGGL(unsplit_words<uint32_t>, dim3((unsigned)n_tiles), dim3(kUnsplitThreads), 0, s, runs, ovf_runs,
+    hipLaunchKernelGGL((unsplit_words<uint32_t, kUnsplitThreads>), grid, dim3(kUnsplitThreads), 0, s, runs, ovf_runs,
                        row_loc, (const uint32_t *)w_pos, (uint32_t *)w_row, n, parts, tile, status);
   return hipGetLastError();
 }
