@@ -22,6 +22,8 @@ Step = one pass of the hot path over one batch:
       and 2^30 probe keys of its own; a step = owner partition + RCCL all-to-all (xGMI) + local
       probe.
 Prints ONE JSON line on rank 0 with roofline and cpu_baseline objects.
+The default c2 line also carries `other_workloads`: C3 and C5 timed in the same run, each with its
+own parity checks and roofline (--no-other-workloads skips them).
 """
 from __future__ import annotations
 
@@ -100,6 +102,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1 << 28, help="probe keys in the multi-thread CPU sample")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-other", action="store_true", help="C2: do not time the other paths beside the headline")
+    ap.add_argument("--no-other-workloads", action="store_true",
+                    help="C2: do not run C3 and C5 after the headline (other_workloads)")
     ap.add_argument("--no-rows", action="store_true",
                     help="partitioned path without CCJ_PART_ROWS (the walk writes every output; A/B)")
     ap.add_argument("--lib", default="product",
@@ -455,7 +459,7 @@ def bench_c3(args, dev, stream):
         "cpu_baseline": cpu,
         "parity": parity,
     }
-    print(json.dumps(line), flush=True)
+    return line
 
 
 def bench_pipeline(args):
@@ -626,12 +630,53 @@ def main():
     dev = torch.device("cuda", local)
     stream = torch.cuda.Stream(device=dev)
 
-    n_build, n_probe, chunk = args.n_build, args.n_probe, args.chunk
-    layout = ccj.LAYOUT_DEVICE if args.layout == "device" else ccj.LAYOUT_REFERENCE
     if world > 1 or args.sharded:
         return bench_multi(args, world, rank, local, dev, stream, dist)
-    if args.workload == "c3":
-        return bench_c3(args, dev, stream)
+    line = bench_c3(args, dev, stream) if args.workload == "c3" else bench_single(args, dev, stream)
+    if args.workload == "c2" and not args.no_other_workloads:
+        line["other_workloads"] = other_workloads(args, dev, stream)
+    print(json.dumps(line), flush=True)
+
+
+def other_workloads(args, dev, stream):
+    """BASELINE configs[2] (C3) and configs[4] (C5) timed in the same run as the C2 headline, each
+    on its own buffers after the C2 ones are freed: the driver's default bench.py line then carries
+    all three single-GPU workloads, each with its L1 / L2 check against the exact
+    membership answer, its roofline (traffic from its committed counter profile) and its phases."""
+    import copy
+    res = []
+    for w in ("c3", "c5"):
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        a = copy.copy(args)
+        a.workload, a.path, a.no_cpu, a.no_other = w, "partitioned", True, True
+        a.steps, a.warmup = max(1, min(args.steps, 10)), min(args.warmup, 2)
+        t0 = time.perf_counter()
+        try:
+            ln = bench_c3(a, dev, stream) if w == "c3" else bench_single(a, dev, stream)
+        except Exception as e:  # the C2 headline above stands on its own; report the failure beside it
+            res.append({"workload": w, "error": f"{type(e).__name__}: {e}"[:500]})
+            continue
+        keep = {"workload": ln["config"]["workload"], "value": ln["value"], "unit": ln["unit"],
+                "ms_per_step": ln["ms_per_step"], "steps": a.steps, "warmup": a.warmup, "path": ln.get("path"),
+                "roofline": ln["roofline"], "phases": ln.get("phases"), "parity": ln["parity"],
+                "wall_s": time.perf_counter() - t0}
+        if "compaction_ms" in ln:
+            keep["compaction_ms"] = ln["compaction_ms"]
+        res.append(keep)
+        log(f"[other] {w}: {ln['ms_per_step']:.2f} ms/step, parity {ln['parity']}")
+        del ln
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return res
+
+
+def bench_single(args, dev, stream):
+    """C2 (or C5) on one GPU: the BASELINE metric's step, its parity checks, roofline and CPU
+    baseline; returns the JSON line's dict."""
+    world, rank = 1, 0
+    n_build, n_probe, chunk = args.n_build, args.n_probe, args.chunk
+    layout = ccj.LAYOUT_DEVICE if args.layout == "device" else ccj.LAYOUT_REFERENCE
 
     # ---- setup (untimed, as the reference builds before its timer: main.cpp:62-68 vs :92-94) ----
     t0 = time.perf_counter()
@@ -686,8 +731,6 @@ def main():
     for _ in range(args.warmup):
         step()
     stream.synchronize()
-    if dist:
-        dist.barrier()
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     pev = [ccj.PhaseEvents() for _ in range(args.steps)]  # the reference's 4-phase schema, per step
@@ -699,15 +742,9 @@ def main():
         evs[i][1].record(stream)
     stream.synchronize()
     torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
     wall = time.perf_counter() - t0
     ccj.PhaseEvents.disarm()
     phases = phase_report(pev, args.path, c5)
-    if dist:
-        t = torch.tensor([wall], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
     ms_per_step = wall * 1e3 / args.steps
     total_tuples = n_probe * world
@@ -873,9 +910,7 @@ def main():
                 "parity": "L3 (reference order)" if o not in ("partitioned", "rank") else "L1/L2",
                 "kernel": PATH_KERNELS[o], "check": o_par} for o, (o_ms, o_par) in other_runs.items()],
         }
-        print(json.dumps(line), flush=True)
-    if dist:
-        dist.destroy_process_group()
+    return line
 
 
 def bench_multi(args, world, rank, local, dev, stream, dist):

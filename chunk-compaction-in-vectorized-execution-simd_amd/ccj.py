@@ -148,7 +148,7 @@ def lib():
         L.ccj_partition_grouped_workspace_size.restype = C.c_size_t
         L.ccj_partition_grouped_sub_cap.argtypes = [u64, C.c_uint32, C.c_uint32]
         L.ccj_partition_grouped_sub_cap.restype = u64
-        L.ccj_partition_by_owner_grouped.argtypes = [vp, u64, C.c_uint32, C.c_uint32, u64, vp, vp, vp, vp, vp,
+        L.ccj_partition_by_owner_grouped.argtypes = [vp, u64, C.c_uint32, C.c_uint32, u64, C.c_uint32, vp, vp, vp, vp, vp,
                                                      C.c_size_t, vp]
         L.ccj_pipeline_create.argtypes = [C.POINTER(vp), C.c_uint32, C.c_uint32, i32, C.POINTER(vp)]
         L.ccj_pipeline_run.argtypes = [vp, C.POINTER(vp), u64, vp, C.POINTER(PipelineResult)]
@@ -198,13 +198,17 @@ class PhaseEvents:
             if h.hipEventCreate(C.byref(e)) != 0:
                 raise CCJError("hipEventCreate failed")
 
+    _armed = None  # the instance whose events the library holds (one-shot: the next probe call clears them)
+
     def arm(self):
         arr = (C.c_void_p * 4)(*[e.value for e in self.ev])
         check(lib().ccj_set_phase_events(arr, 4), "ccj_set_phase_events")
+        PhaseEvents._armed = id(self)
 
     @staticmethod
     def disarm():
         check(lib().ccj_set_phase_events(None, 0), "ccj_set_phase_events")
+        PhaseEvents._armed = None
 
     def ms(self):
         h = _hip()
@@ -218,6 +222,8 @@ class PhaseEvents:
 
     def __del__(self):
         try:
+            if PhaseEvents._armed == id(self):  # never leave the library holding destroyed events
+                PhaseEvents.disarm()
             for e in self.ev:
                 _hip().hipEventDestroy(e)
         except Exception:
@@ -634,13 +640,15 @@ OWNER_GROUPS = 8  # CCJ_OWNER_GROUPS
 
 class GroupedOwnerPartitioner:
     """One-pass fixed-capacity owner partitioning (ccj_partition_by_owner_grouped): destination d's
-    region is OWNER_GROUPS sub-segments of sub_cap slots, sub-segment (d, g) at (d*8 + g)*sub_cap
-    holding counts[d*8 + g] rows (u32 row ids row_base + i)."""
+    region is OWNER_GROUPS sub-segments of sub_cap slots, sub-segment (s, g) at (s*8 + g)*sub_cap
+    holding counts[s*8 + g] rows (u32 row ids row_base + i), s = d — or, with self_last = the
+    caller's rank, s = parts - 1 for the own rank and d - (d > self_last) for the peers."""
 
-    def __init__(self, n: int, parts: int, sub_cap: int, device=None):
+    def __init__(self, n: int, parts: int, sub_cap: int, device=None, self_last: int = -1):
         import torch
         dev = device or torch.device("cuda", torch.cuda.current_device())
         self.n, self.parts, self.sub_cap = n, parts, sub_cap
+        self.self_last = self_last if 0 <= self_last < parts else 0xFFFFFFFF
         self.ws_bytes = lib().ccj_partition_grouped_workspace_size(parts)
         self.ws = torch.empty(max(self.ws_bytes, 8), dtype=torch.uint8, device=dev)
 
@@ -648,7 +656,7 @@ class GroupedOwnerPartitioner:
         assert keys.numel() == self.n and out_keys.numel() >= self.parts * OWNER_GROUPS * self.sub_cap
         assert out_counts.numel() >= self.parts * OWNER_GROUPS
         check(lib().ccj_partition_by_owner_grouped(_ptr(keys), self.n, self.parts, row_base, self.sub_cap,
-                                                   _ptr(out_keys), _ptr(out_rows), _ptr(out_counts), _ptr(status),
+                                                   self.self_last, _ptr(out_keys), _ptr(out_rows), _ptr(out_counts), _ptr(status),
                                                    _ptr(self.ws), self.ws_bytes, _stream(stream)),
               "ccj_partition_by_owner_grouped")
 

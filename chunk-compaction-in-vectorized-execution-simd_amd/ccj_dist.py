@@ -5,8 +5,10 @@ Per step, on every rank, the 2^30 local probe keys go through in B batches, pipe
 HIP streams (partition, comm, probe) with double-buffered send/receive slots:
   1. owner partition of batch i (ccj_partition_by_owner_fixed, HIP): destination d's keys and u32
      row ids in fixed-capacity segment d, true counts beside them;
-  2. all-to-all of counts and keys with equal splits (all_to_all_single calls on the comm stream:
-     the tuple shuffle over xGMI, the only data-path collective; no host round trip);
+  2. all-to-all of counts and keys to the N - 1 peers with equal splits (all_to_all_single calls on
+     the comm stream: the tuple shuffle over xGMI, the only data-path collective; no host round
+     trip); the rank's own segment — last in its send buffer — is copied locally, never through
+     RCCL (exchange_peers);
   3. local probe of the received segments, GROUP batches at a time (ccj_segment_chunk_counts +
      ccj_probe_partitioned: the live rows split by home-slot window, then walked with the window
      L2-resident) while the comm stream moves the next group's batches;
@@ -69,14 +71,35 @@ def batch_count(n_probe: int, world: int, chunk: int, at_least: int = 1, subs: i
     return b
 
 
-def exchange_fixed(send_keys, send_rows, send_counts, recv_keys, recv_rows, recv_counts, group=None, rows=True):
-    """All-to-all of fixed-capacity segments: equal splits, so no sizes travel through the host.
-    rows=False: counts and keys only (a timed step: the rows stay with their sender)."""
+def slot_of(d: int, rank: int, world: int) -> int:
+    """Slot of destination d in a rank's send buffers (ccj.h ccj_partition_by_owner_grouped,
+    self_last = rank): the peers in rank order, then the rank's own region last."""
+    return world - 1 if d == rank else d - (d > rank)
+
+
+def exchange_peers(send, recv, per, world, rank, copy, group=None):
+    """Move one buffer laid out in `world` slots of `per` elements (slots 0 .. world-2: the peers in
+    rank order, slot world-1: the rank's own): ONE all_to_all_single with equal splits to the peers
+    and a zero self split, so the peer regions are contiguous in rank order on both sides and no
+    sizes travel through the host; the own slot never enters RCCL — `copy` moves it locally (at
+    N = 8 an eighth of the bytes, which RCCL's copy kernel moved at ~0.75 TB/s)."""
+    n = (world - 1) * per
+    if world > 1:
+        splits = [0 if d == rank else per for d in range(world)]
+        dist.all_to_all_single(recv[:n], send[:n], splits, splits, group=group)
+    copy(recv[n:n + per], send[n:n + per])
+
+
+def exchange_fixed(send_keys, send_rows, send_counts, recv_keys, recv_rows, recv_counts, world, rank, seg, subs,
+                   copy, group=None, rows=True):
+    """All-to-all of fixed-capacity segments (slot layout of exchange_peers): seg keys (and rows)
+    and subs counts per source.  rows=False: counts and keys only (a timed step: the rows stay
+    with their sender)."""
     assert send_keys.numel() * send_keys.element_size() <= MAX_A2A_BYTES
-    dist.all_to_all_single(recv_counts, send_counts, group=group)
-    dist.all_to_all_single(recv_keys, send_keys, group=group)
+    exchange_peers(send_counts, recv_counts, subs, world, rank, copy, group)
+    exchange_peers(send_keys, recv_keys, seg, world, rank, copy, group)
     if rows:
-        dist.all_to_all_single(recv_rows, send_rows, group=group)
+        exchange_peers(send_rows, recv_rows, seg, world, rank, copy, group)
 
 
 def exchange(send_keys, send_rows, send_counts, group=None):
@@ -170,9 +193,17 @@ class DeviceOps:
     def sub_capacity(self, n, world, chunk):
         return self.ccj.grouped_sub_cap(n, world, chunk)
 
-    def fixed_partitioner(self, n, world, sub_cap):
-        p = self.ccj.GroupedOwnerPartitioner(n, world, sub_cap, device=self.device)
+    def fixed_partitioner(self, n, world, sub_cap, self_last):
+        p = self.ccj.GroupedOwnerPartitioner(n, world, sub_cap, device=self.device, self_last=self_last)
         return lambda keys, row_base, sk, sr, sc, status, stream: p(keys, row_base, sk, sr, sc, status, stream=stream)
+
+    def copy(self, dst, src):
+        """dst[:] = src on the current stream (the rank's own segment: ccj_copy_device, 16-byte
+        non-temporal loads and stores)."""
+        if src.numel() * src.element_size() % 16 == 0:
+            self.ccj.copy_device(dst, src, stream=torch.cuda.current_stream())
+        else:
+            dst.copy_(src)
 
     def segment_chunk_counts(self, seg_counts, seg_cap, chunk, out, status, stream):
         self.ccj.segment_chunk_counts(seg_counts, seg_cap, chunk, out, status, stream=stream)
@@ -193,13 +224,15 @@ class DeviceOps:
         self.table.probe_partitioned(keys, chunk, counts=counts, out=out, part=part, stream=stream, retry=False,
                                      share=True, rows=rows)
 
-    def group_rows(self, part, recv_rows, n_probe, seg_cap, slots, stream):
+    def group_rows(self, part, recv_rows, n_probe, seg_cap, slots, stream, src):
         """Global probe row of every position of a group's partitioned layout (gap positions hold
-        arbitrary values: only matched positions are ever looked up)."""
+        arbitrary values: only matched positions are ever looked up); src[s] = the source rank of
+        receive slot s."""
         n = recv_rows.numel()
         with torch.cuda.stream(stream):
             q = torch.arange(n, device=recv_rows.device) % slots
-            recv = (q // seg_cap) * n_probe + recv_rows.to(torch.int64)
+            srcs = torch.tensor(src, dtype=torch.int64, device=recv_rows.device)
+            recv = srcs[q // seg_cap] * n_probe + recv_rows.to(torch.int64)
             if part.get("rows_mode"):  # out_sel holds receive slots: the map is by slot
                 return recv
             rm = part["row_map"].to(torch.int64).clamp_(0, n - 1)
@@ -229,6 +262,10 @@ class ShardedProbe:
         self.ops = ops or DeviceOps()
         o = self.ops
         self.world, self.rank, self.chunk, self.n_probe = world, rank, chunk, n_probe
+        # receive slot s holds source src_of_slot[s]'s segment (exchange_peers: peers, then own)
+        self.src_of_slot = [0] * world
+        for d in range(world):
+            self.src_of_slot[slot_of(d, rank, world)] = d
         self.stream = stream or o.stream("probe")
         self.comm = o.stream()
         self.pstream = o.stream("partition")  # partitions run beside the previous probe
@@ -319,7 +356,7 @@ class ShardedProbe:
         s = j % 2
         lo, n = self._batch(j % self.batches)
         if n not in self.fparts:
-            self.fparts[n] = self.ops.fixed_partitioner(n, self.world, self.sub_cap)
+            self.fparts[n] = self.ops.fixed_partitioner(n, self.world, self.sub_cap, self.rank)
         self.pstream.wait_event(self.ev_comm[s])  # the previous all-to-all from send slot s is done
         with self._timed(self.part_events, self.pstream, timing):
             self.fparts[n](keys[lo:lo + n], lo, self.sk[s], self.srb[j % self.batches], self.sc[s], self.status,
@@ -333,7 +370,8 @@ class ShardedProbe:
         if (j % self.batches) % self.group == 0:
             self.comm.wait_event(self.ev_probe[gs])  # the previous probe of receive group slot gs is done
         with self.ops.on(self.comm), self._timed(self.comm_events, self.comm, timing):
-            exchange_fixed(self.sk[s], self.srb[j % self.batches], self.sc[s], rk, rr, rc, rows=rows)
+            exchange_fixed(self.sk[s], self.srb[j % self.batches], self.sc[s], rk, rr, rc, self.world, self.rank,
+                           self.seg_cap, self.subs, self.ops.copy, rows=rows)
         self.ev_comm[s].record(self.comm)
 
     def reset_timing(self):
@@ -387,7 +425,8 @@ class ShardedProbe:
 
     def group_row_map(self, j0, g):
         gs = self._gslot(j0 + self._group_range(g)[0])
-        return self.ops.group_rows(self.parts[gs], self.rr[gs], self.n_probe, self.seg_cap, self.slots, self.stream)
+        return self.ops.group_rows(self.parts[gs], self.rr[gs], self.n_probe, self.seg_cap, self.slots, self.stream,
+                                   self.src_of_slot)
 
     def received_keys(self, i):
         """Batch i's received keys (of the last run's first step: call after a one-step run) without
@@ -469,7 +508,7 @@ class ShardedProbe:
             for i in range(first, last + 1):
                 gs, rk, rr, rc = self._recv(j0 + i)
                 with o.on(self.comm):
-                    dist.all_to_all_single(rr, self.srb[i])
+                    exchange_peers(self.srb[i], rr, self.seg_cap, self.world, self.rank, o.copy)
                 covered.append(i)
             self.stream.wait_stream(self.comm)
             gs = self._gslot(j0 + first)
@@ -566,3 +605,6 @@ class HostOpsBase:
 
     def zeros(self, n, dtype):
         return torch.zeros(n, dtype=dtype)
+
+    def copy(self, dst, src):
+        dst.copy_(src)

@@ -25,14 +25,36 @@ thread_local std::string g_err;
 
 // Phase boundary events (ccj_set_phase_events): the reference's CycleProfiler slots
 // (profiler.h:262-290) mapped onto this thread's next probe call's kernels.
+// One-shot: the probe call that sees them armed records all four — every return path,
+// the early ones too (PhaseScope) — and then clears them, so a later call can never record on
+// events the caller has since destroyed, and phases never mix two calls.
 thread_local hipEvent_t g_phase[4] = {};
 thread_local uint32_t g_n_phase = 0;
+thread_local uint32_t g_phase_next = 0;  // the next boundary this call has not recorded yet
 void phase_mark(hipStream_t s, uint32_t i) {
   if (i < g_n_phase && g_phase[i]) (void)hipEventRecord(g_phase[i], s);
+  if (i + 1 > g_phase_next) g_phase_next = i + 1;
 }
 void phase_marks(hipStream_t s, uint32_t from, uint32_t to) {
   for (uint32_t i = from; i <= to; ++i) phase_mark(s, i);
 }
+// Scope of one probe API call: on exit, the boundaries the call did not reach (an empty input, a
+// one-pass fallback, an error) are recorded at the stream's current point and the events cleared.
+// A nested probe call (ccj_probe_ordered's fallback to ccj_probe) consumes them itself.
+struct PhaseScope {
+  hipStream_t s;
+  bool outer;
+  explicit PhaseScope(hipStream_t st) : s(st), outer(g_n_phase != 0) {
+    if (outer) g_phase_next = 0;
+  }
+  ~PhaseScope() {
+    if (!outer || !g_n_phase) return;
+    for (uint32_t i = g_phase_next; i < 4; ++i) phase_mark(s, i);
+    for (auto &e : g_phase) e = nullptr;
+    g_n_phase = 0;
+    g_phase_next = 0;
+  }
+};
 
 
 int fail(int code, const std::string &msg) {
@@ -421,6 +443,7 @@ int ccj_set_phase_events(void *const *events, uint32_t n) {
   if (n > 4 || (n && !events)) return fail(CCJ_ERR_INVALID, "ccj_set_phase_events: at most 4 events");
   for (uint32_t i = 0; i < 4; ++i) g_phase[i] = i < n ? (hipEvent_t)events[i] : nullptr;
   g_n_phase = n;
+  g_phase_next = 0;
   return CCJ_OK;
 }
 
@@ -606,9 +629,17 @@ PartLayout part_layout(const ccj_table *t, uint64_t n_rows, uint32_t chunk) {
   }
   L.seg_cap = ccj::slot_seg_cap(n_rows, L.pl, chunk);
   L.ovf_base = (uint64_t)L.parts * 8 * L.seg_cap;
-  // 1/16 of the rows, at least one chunk per sub-area, and the split's 64-position sink
-  L.ovf_cap = (n_rows / 16 + 8ull * chunk + 64 + chunk - 1) / chunk * chunk;
-  L.ovf_sub = (L.ovf_cap - 64) / 8 / chunk * chunk;
+  // Per tile group (XCD) g, a sub-area of 1/16 of the most rows one group can receive — tile group
+  // g splits tiles [g n_tiles / 8, (g + 1) n_tiles / 8), so with few tiles one group may get all
+  // of them (1/8 of n / 16 each sent skewed small inputs to the exact fallback early) —
+  // at least one chunk each, then the split's 64-position sink.
+  uint64_t g_rows = 0;
+  for (const bool runs : {false, true}) {
+    const uint64_t tile = ccj::slot_split_tile_keys(L.parts, runs), n_tiles = (n_rows + tile - 1) / tile;
+    g_rows = std::max<uint64_t>(g_rows, std::min<uint64_t>(n_rows, (n_tiles + 7) / 8 * tile));
+  }
+  L.ovf_sub = (g_rows / 16 + chunk + chunk - 1) / chunk * chunk;
+  L.ovf_cap = (8 * L.ovf_sub + 64 + chunk - 1) / chunk * chunk;
   L.positions = L.ovf_base + L.ovf_cap;
   return L;
 }
@@ -637,6 +668,7 @@ size_t ccj_probe_partitioned_workspace_size(const ccj_table *t, uint64_t n_rows,
 
 int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t flags, uint32_t *out_row_map,
                           void *ws, size_t ws_bytes, ccj_stream stream) {
+  PhaseScope phase_scope((hipStream_t)stream);
   ccj::ProbeParams p;
   if (int rc = fill_probe_params(t, a, p)) return rc;
   if (t->info.kind == CCJ_TABLE_CHAIN && (a->out_pos || a->n_payload_cols))
@@ -848,6 +880,7 @@ size_t ccj_probe_ordered_workspace_size(const ccj_table *t, uint64_t n_rows, uin
 }
 
 int ccj_probe_ordered(const ccj_table *t, const ccj_probe_args *a, void *ws, size_t ws_bytes, ccj_stream stream) {
+  PhaseScope phase_scope((hipStream_t)stream);
   ccj::ProbeParams p;
   if (int rc = fill_probe_params(t, a, p)) return rc;
   if (a->n_rows == 0) return CCJ_OK;
@@ -911,6 +944,7 @@ int ccj_probe_ordered(const ccj_table *t, const ccj_probe_args *a, void *ws, siz
 }
 
 int ccj_probe(const ccj_table *t, const ccj_probe_args *a, ccj_stream stream) {
+  PhaseScope phase_scope((hipStream_t)stream);
   ccj::ProbeParams p;
   if (int rc = fill_probe_params(t, a, p)) return rc;
   if (a->n_rows == 0) return CCJ_OK;  // no chunks: nothing to launch
@@ -1009,7 +1043,7 @@ uint64_t ccj_partition_grouped_sub_cap(uint64_t n, uint32_t parts, uint32_t chun
 }
 
 int ccj_partition_by_owner_grouped(const int64_t *d_keys, uint64_t n, uint32_t parts, uint32_t row_base,
-                                   uint64_t sub_cap, int64_t *d_out_keys, uint32_t *d_out_rows,
+                                   uint64_t sub_cap, uint32_t self_last, int64_t *d_out_keys, uint32_t *d_out_rows,
                                    uint64_t *d_out_counts, uint32_t *d_status, void *d_workspace,
                                    size_t workspace_bytes, ccj_stream stream) {
   if (parts == 0 || parts > ccj::kMaxParts || (parts & (parts - 1)))
@@ -1021,7 +1055,7 @@ int ccj_partition_by_owner_grouped(const int64_t *d_keys, uint64_t n, uint32_t p
     return fail(CCJ_ERR_INVALID, "ccj_partition_by_owner_grouped: workspace too small");
   if ((uint64_t)row_base + n > (1ull << 32)) return fail(CCJ_ERR_LIMIT, "ccj_partition_by_owner_grouped: rows exceed u32");
   HIP_TRY(ccj::launch_partition_grouped(d_keys, n, parts, row_base, sub_cap, d_out_keys, d_out_rows, d_out_counts,
-                                        d_status, d_workspace, (hipStream_t)stream),
+                                        d_status, d_workspace, (hipStream_t)stream, self_last),
           "grouped partition launch");
   return CCJ_OK;
 }

@@ -240,7 +240,7 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
                                    uint32_t *out_rows, uint32_t *status, hipStream_t s,
                                    const uint32_t *counts = nullptr, uint32_t chunk = 0, uint2 *runs = nullptr,
                                    uint32_t *ovf_runs = nullptr, uint32_t row_base = 0, uint32_t shift = ~0u,
-                                   uint32_t wgs = 0, void *sink = nullptr);
+                                   uint32_t wgs = 0, void *sink = nullptr, uint32_t self_last = ~0u);
 // Bytes of device memory the split writes its inactive lanes' stores to when the overflow area
 // cannot hold them (launch_slot_split_fixed's `sink`; 8 XCD groups x 8 positions of key + row).
 constexpr size_t kSplitSinkBytes = 8 * 8 * 16;
@@ -248,7 +248,7 @@ size_t partition_grouped_workspace(uint32_t parts);
 uint64_t partition_grouped_sub_cap(uint64_t n, uint32_t parts, uint32_t chunk);
 hipError_t launch_partition_grouped(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t row_base,
                                     uint64_t sub_cap, int64_t *out_keys, uint32_t *out_rows, uint64_t *out_counts,
-                                    uint32_t *status, void *ws, hipStream_t s);
+                                    uint32_t *status, void *ws, hipStream_t s, uint32_t self_last = ~0u);
 uint32_t slot_split_tile_keys(uint32_t parts, bool runs = false);
 hipError_t launch_partition_fixed(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t row_base, uint64_t seg_cap,
                                   int64_t *out_keys, uint32_t *out_rows, uint64_t *out_counts, uint32_t *status,

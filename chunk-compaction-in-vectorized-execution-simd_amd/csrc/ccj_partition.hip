@@ -262,11 +262,12 @@ uint64_t partition_grouped_sub_cap(uint64_t n, uint32_t parts, uint32_t chunk) {
 
 static hipError_t launch_owner_split_small(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t shift,
                                           uint64_t sub_cap, uint32_t *cur, int64_t *out_keys, uint32_t *out_rows,
-                                          uint32_t *status, uint32_t row_base, void *sink, hipStream_t s);
+                                          uint32_t *status, uint32_t row_base, void *sink, hipStream_t s,
+                                          uint32_t self_last);
 
 hipError_t launch_partition_grouped(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t row_base,
                                     uint64_t sub_cap, int64_t *out_keys, uint32_t *out_rows, uint64_t *out_counts,
-                                    uint32_t *status, void *ws, hipStream_t s) {
+                                    uint32_t *status, void *ws, hipStream_t s, uint32_t self_last) {
   // the slot split's one-pass kernel with partition = the owner (top log2(parts) hash bits) and no
   // overflow area: a sub-segment that overflows drops rows and raises CCJ_FLAG_PART_OVERFLOW
   SlotPlan pl{};
@@ -286,10 +287,11 @@ hipError_t launch_partition_grouped(const int64_t *keys, uint64_t n, uint32_t pa
   hipError_t e;
   if (ccj_tune_int("CCJ_OWNER_SMALL", 1) && parts <= 64) {
     e = launch_owner_split_small(keys, n, parts, shift, sub_cap, cur, out_keys, out_rows, status, row_base,
-                                 (char *)ws + grouped_cursor_bytes(parts), s);
+                                 (char *)ws + grouped_cursor_bytes(parts), s, self_last);
   } else {
     e = launch_slot_split_fixed(keys, n, pl, sub_cap, 0, 0, 0, cur, out_keys, out_rows, status, s, nullptr, 0,
-                                nullptr, nullptr, row_base, shift, wgs, (char *)ws + grouped_cursor_bytes(parts));
+                                nullptr, nullptr, row_base, shift, wgs, (char *)ws + grouped_cursor_bytes(parts),
+                                self_last);
   }
   if (e) return e;
   hipLaunchKernelGGL(grouped_counts, dim3((parts * 8 + 255) / 256), dim3(256), 0, s, cur, parts, out_counts);
@@ -358,13 +360,22 @@ constexpr int kSplitPer = 11;  // CCJ_SPLIT_PER sweep at C2: 8-13 keys -> 6.35 6
 constexpr uint32_t kSplitParts = 1u << kSplitPartBits;
 static_assert(kSplitParts <= (uint32_t)kSplitThreads, "one partition per thread in the scan");
 
+// The owner split's partition -> slot map for the multi-GPU exchange: the rank's own partition
+// (self_last) goes to the last slot and the partitions above it move down one, so the N - 1 peer
+// segments are contiguous in rank order (one all-to-all with a zero self split) and the self
+// segment sits after them, copied locally instead of through RCCL.  self_last >= parts: identity.
+__device__ __forceinline__ uint32_t self_slot(uint32_t d, uint32_t self_last, uint32_t parts) {
+  return d == self_last ? parts - 1u : d - (d > self_last ? 1u : 0u);
+}
+
 template <bool COUNTS, int THREADS, int MAXP, int PER>
 __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys, uint64_t n, uint32_t shift,
                                                                  uint32_t parts, uint64_t n_tiles, uint32_t *cur,
                                                                  uint64_t cap, uint64_t ovf_base, uint64_t ovf_cap,
                                                                  int64_t *out_k, uint32_t *out_r, uint32_t *status,
                                                                  uint32_t ablate, const uint32_t *counts, uint32_t chunk,
-                                                                 uint2 *runs, uint32_t *ovf_runs, uint32_t row_base) {
+                                                                 uint2 *runs, uint32_t *ovf_runs, uint32_t row_base,
+                                                                 uint32_t self_last) {
   constexpr uint32_t kTileKeys = (uint32_t)THREADS * PER;
   static_assert(MAXP <= THREADS, "one partition per thread in the scan");
   __shared__ int64_t s_k[kTileKeys];
@@ -429,7 +440,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
     uint32_t dd[PER], rk[PER];
 #pragma unroll
     for (int it = 0; it < PER; ++it) {
-      dd[it] = (uint32_t)(murmurhash64((uint64_t)kk[it]) >> shift) & mask;
+      dd[it] = self_slot((uint32_t)(murmurhash64((uint64_t)kk[it]) >> shift) & mask, self_last, parts);
       rk[it] = (live >> it) & 1u ? atomicAdd(&s_hist[dd[it]], 1u) : 0u;
     }
     __syncthreads();
@@ -487,13 +498,14 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
       const uint32_t si = s_i[q], d = si >> 16;
       const uint32_t o = q - s_loc[d];
       const uint32_t lim = s_lim[d];
+      if (runs && !CCJ_ABLATED(ablate, 0x10u))
+        // the ordered probe: the row inside its tile (16 bits) at the entry's IMAGE index t0 + q,
+        // exactly as slot_split_pipe writes it (unsplit_words reads row_loc[t0 + j])
+        reinterpret_cast<uint16_t *>(out_r)[t0 + q] = (uint16_t)(si & 0xFFFFu);
       if ((o < lim || o - lim < s_olim[d]) && !CCJ_ABLATED(ablate, 0x10u)) {  // (0x10: timing only, no stores)
         const uint64_t dest = o < lim ? s_dst[d] + o : ovf_base + s_ovf[d] + (o - lim);
         out_k[dest] = k;  // plain stores: the L2 merges neighbouring runs' partial lines
-        if (runs)  // the ordered probe: the row inside its tile, 16 bits (the unsplit reads half the bytes)
-          reinterpret_cast<uint16_t *>(out_r)[dest] = (uint16_t)(si & 0xFFFFu);
-        else
-          out_r[dest] = row_base + (uint32_t)(t0 + (si & 0xFFFFu));  // (non-temporal stores measured the same)
+        if (!runs) out_r[dest] = row_base + (uint32_t)(t0 + (si & 0xFFFFu));  // (non-temporal stores measured the same)
       }
     }
     __syncthreads();
@@ -528,7 +540,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
                                                                 int64_t *out_k, uint32_t *out_r, uint32_t *status,
                                                                 const uint32_t *counts, uint32_t chunk, uint2 *runs,
                                                                 uint32_t *ovf_runs, uint32_t row_base, int64_t *sink_k,
-                                                                uint32_t *sink_r, uint32_t ablate) {
+                                                                uint32_t *sink_r, uint32_t ablate, uint32_t self_last) {
   constexpr uint32_t kTileKeys = (uint32_t)THREADS * PER;
   static_assert(MAXP <= THREADS, "one partition per thread in the scan");
   __shared__ int64_t s_k[kTileKeys];
@@ -661,13 +673,14 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
     uint32_t dr[PER];  // partition | rank in it << 10 (one register per key: no spills at 11 keys)
 #pragma unroll
     for (int it = 0; it < PER; ++it) {
-      const uint32_t d = CCJ_ABLATED(ablate, 0x2000u) ? (uint32_t)((uint64_t)kc[it] >> shift) & mask  // (timing: no hash)
-                                                      : (uint32_t)(murmurhash64((uint64_t)kc[it]) >> shift) & mask;
+      const uint32_t d0 = CCJ_ABLATED(ablate, 0x2000u) ? (uint32_t)((uint64_t)kc[it] >> shift) & mask  // (timing: no hash)
+                                                       : (uint32_t)(murmurhash64((uint64_t)kc[it]) >> shift) & mask;
       if constexpr (MAXP <= 64) {
         // few partitions (the owner split: one per rank): an LDS atomic per key would queue the
         // wave's 64 lanes on at most `parts` addresses (one address at N = 1).  Instead one ballot
         // per partition ranks the wave's keys, lane p adds partition p's wave count to s_hist[p]
         // (distinct addresses), and each lane takes its partition's base from that lane.
+        const uint32_t d = self_slot(d0, self_last, parts);  // (the owner split: own rank's segment last)
         const bool lv = (live >> it) & 1u;
         uint32_t wcnt = 0;
         uint64_t mine = 0;
@@ -682,6 +695,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
         dr[it] = d | (lv ? rk : 0u) << 10;
         if (it < kKS) store_one(it);
       } else {
+        const uint32_t d = d0;
         dr[it] = d | ((live >> it) & 1u ? atomicAdd(&s_hist[d], 1u) : 0u) << 10;
         if (it < kKS) store_one(it);
       }
@@ -771,7 +785,8 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
 // stream (a multiple of 8: one tile group per XCD).
 static hipError_t launch_owner_split_small(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t shift,
                                           uint64_t sub_cap, uint32_t *cur, int64_t *out_keys, uint32_t *out_rows,
-                                          uint32_t *status, uint32_t row_base, void *sink, hipStream_t s) {
+                                          uint32_t *status, uint32_t row_base, void *sink, hipStream_t s,
+                                          uint32_t self_last) {
   constexpr int kT = 256, kPer = 8;
   constexpr uint32_t kTile = (uint32_t)kT * kPer;
   hipError_t e = hipMemsetAsync(cur, 0, ((size_t)parts * 8 + 8) * 4, s);
@@ -786,7 +801,7 @@ static hipError_t launch_owner_split_small(const int64_t *keys, uint64_t n, uint
   uint32_t *sink_r = (uint32_t *)((char *)sink + kSplitSinkBytes / 16 * 8);
   hipLaunchKernelGGL((slot_split_pipe<false, kT, 64, kPer, false>), dim3((unsigned)grid), dim3(kT), 0, s, keys, n, shift, parts,
                      n_tiles, cur, sub_cap, (uint64_t)0, (uint64_t)0, out_keys, out_rows, status, nullptr, 0u, nullptr,
-                     nullptr, row_base, sink_k, sink_r, 0u);
+                     nullptr, row_base, sink_k, sink_r, 0u, self_last);
   return hipGetLastError();
 }
 
@@ -816,7 +831,7 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
                                    uint64_t ovf_base, uint64_t ovf_cap, uint64_t ovf_sub, uint32_t *cursors, int64_t *out_keys,
                                    uint32_t *out_rows, uint32_t *status, hipStream_t s, const uint32_t *counts,
                                    uint32_t chunk, uint2 *runs, uint32_t *ovf_runs, uint32_t row_base,
-                                   uint32_t shift, uint32_t wgs, void *sink) {
+                                   uint32_t shift, uint32_t wgs, void *sink, uint32_t self_last) {
   const uint32_t parts = 1u << (pl.lo_bits + pl.hi_bits);
   // counts: a tile's chunks (tile / chunk + 2 at most) fit one count per thread
   if (counts && (chunk == 0 || slot_split_tile_keys(parts, runs != nullptr) / chunk + 2 > (uint32_t)kSplitThreads))
@@ -855,11 +870,11 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
     if (runs)                                                                                                       \
       hipLaunchKernelGGL((slot_split_pipe<C, kSplitThreads, MAXP, P, true>), dim3(grid), dim3(kSplitThreads), 0, s,  \
                          keys, n, shift, parts, n_tiles, cursors, cap, ovf_base, oc, out_keys, out_rows, status,     \
-                         counts, chunk, runs, ovf_runs, row_base, sink_k, sink_r, ablate);                           \
+                         counts, chunk, runs, ovf_runs, row_base, sink_k, sink_r, ablate, self_last);                \
     else                                                                                                            \
       hipLaunchKernelGGL((slot_split_pipe<C, kSplitThreads, MAXP, P, false>), dim3(grid), dim3(kSplitThreads), 0, s, \
                          keys, n, shift, parts, n_tiles, cursors, cap, ovf_base, oc, out_keys, out_rows, status,     \
-                         counts, chunk, runs, ovf_runs, row_base, sink_k, sink_r, ablate);                           \
+                         counts, chunk, runs, ovf_runs, row_base, sink_k, sink_r, ablate, self_last);                \
   } while (0)
 #ifdef CCJ_TUNING
     // (tuning build: two workgroups per CU instead of one lock-stepped 1024-thread workgroup —
@@ -873,20 +888,20 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
         if (counts)
           hipLaunchKernelGGL((slot_split_pipe<true, 512, kSplitParts / 2, 10, false>), dim3(g2), dim3(512), 0, s, keys, n,
                              shift, parts, nt, cursors, cap, ovf_base, oc, out_keys, out_rows, status, counts, chunk,
-                             runs, ovf_runs, row_base, sink_k, sink_r, ablate);
+                             runs, ovf_runs, row_base, sink_k, sink_r, ablate, self_last);
         else
           hipLaunchKernelGGL((slot_split_pipe<false, 512, kSplitParts / 2, 10, false>), dim3(g2), dim3(512), 0, s, keys,
                              n, shift, parts, nt, cursors, cap, ovf_base, oc, out_keys, out_rows, status, counts, chunk,
-                             runs, ovf_runs, row_base, sink_k, sink_r, ablate);
+                             runs, ovf_runs, row_base, sink_k, sink_r, ablate, self_last);
       } else {
         if (counts)
           hipLaunchKernelGGL((slot_split_pipe<true, 1024, kSplitParts / 2, 4, false>), dim3(g2), dim3(1024), 0, s, keys,
                              n, shift, parts, nt, cursors, cap, ovf_base, oc, out_keys, out_rows, status, counts, chunk,
-                             runs, ovf_runs, row_base, sink_k, sink_r, ablate);
+                             runs, ovf_runs, row_base, sink_k, sink_r, ablate, self_last);
         else
           hipLaunchKernelGGL((slot_split_pipe<false, 1024, kSplitParts / 2, 4, false>), dim3(g2), dim3(1024), 0, s, keys,
                              n, shift, parts, nt, cursors, cap, ovf_base, oc, out_keys, out_rows, status, counts, chunk,
-                             runs, ovf_runs, row_base, sink_k, sink_r, ablate);
+                             runs, ovf_runs, row_base, sink_k, sink_r, ablate, self_last);
       }
       return hipGetLastError();
     }
@@ -910,7 +925,7 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
 #define CCJ_SPLIT_LAUNCH(C, MAXP, P)                                                                              \
   hipLaunchKernelGGL((slot_split_fixed<C, kSplitThreads, MAXP, P>), dim3(grid), dim3(kSplitThreads), 0, s, keys, n,      \
                      shift, parts, n_tiles, cursors, cap, ovf_base, ovf_sub, out_keys, out_rows, status, ablate,         \
-                     counts, chunk, runs, ovf_runs, row_base)
+                     counts, chunk, runs, ovf_runs, row_base, self_last)
   if (parts > kSplitParts / 2) {  // 1024 partitions: 10 keys per thread
     if (counts) CCJ_SPLIT_LAUNCH(true, kSplitParts, 10);
     else CCJ_SPLIT_LAUNCH(false, kSplitParts, 10);

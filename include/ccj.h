@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CCJ_ABI_VERSION 13  /* 13: ccj_compact_args.key_cols, per-XCD overflow sub-areas of the partitioned layout; 12: chaining tables built on the device (stable bucket sort), ccj_table_get_arrays; 11: the rank walk in the tuning build only; 10: CCJ_PART_ROWS with positions / payload columns; 9: CCJ_PART_SHARE, CU-masked streams; 8: CCJ_PART_RANK; 7: CCJ_PART_ROWS */
+#define CCJ_ABI_VERSION 14  /* 14: ccj_partition_by_owner_grouped's self_last (the own rank's segment last); 13: ccj_compact_args.key_cols, per-XCD overflow sub-areas of the partitioned layout; 12: chaining tables built on the device (stable bucket sort), ccj_table_get_arrays; 11: the rank walk in the tuning build only; 10: CCJ_PART_ROWS with positions / payload columns; 9: CCJ_PART_SHARE, CU-masked streams; 8: CCJ_PART_RANK; 7: CCJ_PART_ROWS */
 
 enum ccj_status {
   CCJ_OK = 0,
@@ -92,7 +92,10 @@ int ccj_abi_version(void);
  * finding every row's bucket (the split of the partitioned / ordered paths), [2] after match +
  * advance (the walk; this design fuses the two), [3] after the gather (C5 payload columns, or the
  * ordered path's unsplit + reference-order emit).  A kernel that fuses several phases records
- * their boundaries together (probe_chunks: [1], [2], [3] after its one launch). */
+ * their boundaries together (probe_chunks: [1], [2], [3] after its one launch).  One-shot: the
+ * next probe call (ccj_probe, ccj_probe_ordered, ccj_probe_partitioned) records all four on every
+ * return path — a boundary it does not reach (empty input, a one-pass route, an error) at the
+ * stream's point where it returns — and then clears them. */
 int ccj_set_phase_events(void *const *events, uint32_t n);
 /* Selects the HIP device for this thread and checks it is gfx950. */
 int ccj_device_init(int device);
@@ -396,6 +399,11 @@ int ccj_partition_by_owner_fixed(const int64_t *d_keys, uint64_t n, uint32_t par
  * [(d*G + g)*sub_cap, ... + count_{d,g}), sub-segment g filled only by the workgroups of XCD g (so
  * each is written from one L2); d_out_counts[d*G + g] gets the true counts.  Rows beyond a
  * sub-segment's sub_cap are dropped and CCJ_FLAG_PART_OVERFLOW is OR-ed into *d_status.
+ * self_last < parts: destination d's region is placed at slot s(d) instead of d, where
+ * s(self_last) = parts - 1 and s(d) = d - (d > self_last) otherwise — the N - 1 peer regions come
+ * first, in rank order (one all-to-all with a zero self split sends them), and the rank's own
+ * region is last, where a local copy moves it (d_out_counts follows the same slots).
+ * self_last >= parts: s(d) = d.
  * Workspace: ccj_partition_grouped_workspace_size(parts) bytes. */
 #define CCJ_OWNER_GROUPS 8
 size_t ccj_partition_grouped_workspace_size(uint32_t parts);
@@ -403,7 +411,7 @@ size_t ccj_partition_grouped_workspace_size(uint32_t parts);
  * group's rows / parts + 8 standard deviations + one chunk, a multiple of chunk. */
 uint64_t ccj_partition_grouped_sub_cap(uint64_t n, uint32_t parts, uint32_t chunk);
 int ccj_partition_by_owner_grouped(const int64_t *d_keys, uint64_t n, uint32_t parts, uint32_t row_base,
-                                   uint64_t sub_cap, int64_t *d_out_keys, uint32_t *d_out_rows,
+                                   uint64_t sub_cap, uint32_t self_last, int64_t *d_out_keys, uint32_t *d_out_rows,
                                    uint64_t *d_out_counts, uint32_t *d_status, void *d_workspace,
                                    size_t workspace_bytes, ccj_stream stream);
 /* Probe chunk counts for n_segs received fixed-capacity segments (seg_cap a multiple of chunk):

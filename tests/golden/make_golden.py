@@ -8,6 +8,7 @@ are data (inputs + expected outputs) and are committed so the tests never need t
 
   python tests/golden/make_golden.py          # rebuilds _ref/ref_driver if needed
   python tests/golden/make_golden.py phys     # only the trace_*_phys.npz files
+  python tests/golden/make_golden.py sums A B # only sum cases A, B (merged into known_answers.json)
 
 Outputs
   trace_<case>_<view>.npz   per-Next traces (every Next call: chunk, rc, result.sel, payload)
@@ -58,6 +59,12 @@ SUM_CASES = {
     "splitmix_lp_2048_1M_4M_r3M_cf2": ("lp", 2048, 1000000, 2, 4000000, 3000000, 42, 0, 0),
     "splitmix_chain_2048_1M_4M_r3M_cf2": ("chain", 2048, 1000000, 2, 4000000, 3000000, 42, 0, 0),
     "survey_lp_2048_64M_64M": ("lp", 2048, 67108864, 1, 67108864, 67108864, 42, 1, 0),
+    # chaining tables of 2^23 buckets (2^21 + 1 keys): large enough for ccj_probe_ordered's
+    # partitioned route (>= 2^22 buckets), so the reference's chain vectors reach it
+    "survey_chain_2048_2M_8M_r2M": ("chain", 2048, 2097153, 1, 8000000, 2097153, 42, 1, 0),
+    "survey_chain_2048_2M_8M_r20M": ("chain", 2048, 2097153, 1, 8000000, 20971530, 42, 1, 0),
+    "survey_chain_256_2M_4M_cf3": ("chain", 256, 2097153, 3, 4000000, 2097153, 42, 1, 0),
+    "splitmix_chain_1000_2M_4M_r6M_cf2": ("chain", 1000, 2097153, 2, 4000000, 6000000, 42, 0, 0),
 }
 
 # main.cpp-shaped pipeline: (kind, B, joins, cf, lhs, rhs, compact)
@@ -133,6 +140,20 @@ def make_phys():
         print("phys", name, {v: len(x) for v, x in ph.items()}, flush=True)
 
 
+def sum_case(name):
+    kind, B, n, cf, npb, rng, seed, gen, selm = SUM_CASES[name]
+    vs = ["next", "simdinone"] if n > 10_000_000 else VARIANTS
+    res = {}
+    for v in vs:
+        res[v] = parse_sum(run(["probe", kind, v, B, n, cf, npb, rng, seed, gen, selm, 0]))
+    for v in vs[1:]:
+        for k in ("matches", "l2", "survey_chk"):
+            assert res[v][k] == res[vs[0]][k], (name, v, k)
+    print("sum", name, res[vs[0]]["matches"], hex(res[vs[0]]["survey_chk"]), flush=True)
+    return {"spec": dict(kind=kind, B=B, n_build=n, cf=cf, n_probe=npb, range=rng, seed=seed, gen=gen,
+                         selmode=selm), "variants": res}
+
+
 def same(a, b):
     return all(np.array_equal(a[k], b[k]) for k in a)
 
@@ -140,6 +161,15 @@ def same(a, b):
 def main():
     if not os.path.exists(DRIVER):
         subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
+    if sys.argv[1:2] == ["sums"]:  # add / refresh only the named sum cases
+        path = os.path.join(HERE, "known_answers.json")
+        with open(path) as f:
+            answers = json.load(f)
+        for name in sys.argv[2:]:
+            answers["sum_cases"][name] = sum_case(name)
+        with open(path, "w") as f:
+            json.dump(answers, f, indent=1, sort_keys=True)
+        return 0
     make_phys()
     if sys.argv[1:] == ["phys"]:
         return 0
@@ -165,17 +195,8 @@ def main():
             entry["views"][view] = {"variants": vs, **s0}
         answers["trace_cases"][name] = entry
         print("trace", name, {v: e["matches"] for v, e in entry["views"].items()}, flush=True)
-    for name, (kind, B, n, cf, npb, rng, seed, gen, selm) in SUM_CASES.items():
-        vs = ["next", "simdinone"] if n > 10_000_000 else VARIANTS
-        res = {}
-        for v in vs:
-            res[v] = parse_sum(run(["probe", kind, v, B, n, cf, npb, rng, seed, gen, selm, 0]))
-        for v in vs[1:]:
-            for k in ("matches", "l2", "survey_chk"):
-                assert res[v][k] == res[vs[0]][k], (name, v, k)
-        answers["sum_cases"][name] = {"spec": dict(kind=kind, B=B, n_build=n, cf=cf, n_probe=npb, range=rng,
-                                                   seed=seed, gen=gen, selmode=selm), "variants": res}
-        print("sum", name, res[vs[0]]["matches"], hex(res[vs[0]]["survey_chk"]), flush=True)
+    for name in SUM_CASES:
+        answers["sum_cases"][name] = sum_case(name)
     for name, (kind, B, joins, cf, lhs, rhs, compact) in PIPE_CASES.items():
         out = run(["pipeline", kind, B, joins, cf, lhs, rhs, compact])
         head = []

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert ccj.lib().ccj_abi_version() == 13
+    assert ccj.lib().ccj_abi_version() == 14
 
 
 def test_fails_loudly_without_device():

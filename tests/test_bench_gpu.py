@@ -35,11 +35,19 @@ def test_bench_c2_with_other_paths():
     for o in paths.values():
         assert o["check"]["status_flags"] == 0 and o["check"]["l1_ok"] and o["check"]["l2_ok"]
     assert paths["ordered"]["check"]["equals_chunk_path_l3"]
+    # BASELINE configs[2] and [4] in the same line (the driver's default run measures them too)
+    ow = {o["workload"][:2]: o for o in line["other_workloads"]}
+    assert set(ow) == {"C3", "C5"}, line["other_workloads"]
+    for o in ow.values():
+        assert o["value"] > 0 and o["roofline"]["frac"] > 0
+        assert o["parity"]["status_flags"] == 0 and o["parity"]["l1_ok"] and o["parity"]["l2_ok"]
+    assert ow["C3"]["parity"]["compaction_keeps_all"] and ow["C3"]["compaction_ms"] > 0
+    assert ow["C5"]["parity"]["payload_cols_ok"]
 
 
 def test_bench_c2_tuning_build_with_rank_ab():
     """--lib tuning: the same line, with the rank walk (tuning build only) timed beside the headline."""
-    line = run_bench("--lib", "tuning")
+    line = run_bench("--lib", "tuning", "--no-other-workloads")
     par = line["parity"]
     assert par["status_flags"] == 0 and par["l1_ok"] and par["l2_ok"]
     paths = {o["path"]: o for o in line["other_paths"]}
@@ -50,7 +58,7 @@ def test_bench_c2_tuning_build_with_rank_ab():
 
 
 def test_bench_c2_ordered_headline():
-    line = run_bench("--path", "ordered", "--no-other")
+    line = run_bench("--path", "ordered", "--no-other", "--no-other-workloads")
     assert line["path"] == "ordered" and line["parity"]["l1_ok"] and line["parity"]["l2_ok"]
 
 

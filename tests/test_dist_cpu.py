@@ -113,21 +113,28 @@ def _fixed_worker(rank, world, port, cfg, q):
     sk = np.full(world * cap, -1, np.int64)
     sr = np.zeros(world * cap, np.int32)
     sc = np.bincount(owner, minlength=world).astype(np.int64)
-    for d in range(world):  # what ccj_partition_by_owner_fixed writes
+    sc = np.zeros(world, np.int64)
+    for d in range(world):  # what ccj_partition_by_owner_grouped writes with self_last = rank (one sub-segment)
         idx = np.nonzero(owner == d)[0]
-        sk[d * cap:d * cap + len(idx)] = keys[idx]
-        sr[d * cap:d * cap + len(idx)] = idx
-    rk, rr, rc = torch.empty(world * cap, dtype=torch.int64), torch.empty(world * cap, dtype=torch.int32), \
+        s = ccj_dist.slot_of(d, rank, world)
+        sk[s * cap:s * cap + len(idx)] = keys[idx]
+        sr[s * cap:s * cap + len(idx)] = idx
+        sc[s] = len(idx)
+    rk, rr, rc = torch.full((world * cap,), -5, dtype=torch.int64), torch.empty(world * cap, dtype=torch.int32), \
         torch.empty(world, dtype=torch.int64)
-    ccj_dist.exchange_fixed(torch.from_numpy(sk), torch.from_numpy(sr), torch.from_numpy(sc), rk, rr, rc)
+    ccj_dist.exchange_fixed(torch.from_numpy(sk), torch.from_numpy(sr), torch.from_numpy(sc), rk, rr, rc, world, rank,
+                            cap, 1, lambda dst, src: dst.copy_(src))
+    # the own segment was copied locally: the receive's last slot is this rank's send slot, bit for bit
+    assert np.array_equal(rk[(world - 1) * cap:].numpy(), sk[(world - 1) * cap:])
     build = O.ref_build_keys(n_build, cf)
     t = O.Table(O.LP, build[np_owner(build, world) == rank])
     m, l2 = 0, 0
-    for g in range(world):  # receive segment g came from rank g: global row = g * n_probe + local
-        n = int(rc[g])
-        seg_k = rk[g * cap:g * cap + n].numpy()
+    for s in range(world):  # receive slot s came from rank src: global row = src * n_probe + local
+        src = [d for d in range(world) if ccj_dist.slot_of(d, rank, world) == s][0]
+        n = int(rc[s])
+        seg_k = rk[s * cap:s * cap + n].numpy()
         assert (np_owner(seg_k, world) == rank).all()
-        rows = g * n_probe + rr[g * cap:g * cap + n].numpy().astype(np.int64)
+        rows = src * n_probe + rr[s * cap:s * cap + n].numpy().astype(np.int64)
         res = t.probe(seg_k, 2048, cap_factor=cf, max_rounds=4096)
         cap_o = res["cap"]
         for c in range(len(res["count"])):
@@ -145,8 +152,9 @@ def _fixed_worker(rank, world, port, cfg, q):
 
 @pytest.mark.parametrize("world", [2, 4])
 def test_fixed_capacity_exchange_gloo(world):
-    """The pipelined protocol's exchange (fixed-capacity segments, equal splits, u32 local rows,
-    source rank implied by the segment) gives the exact membership answer (L1 + L2)."""
+    """The pipelined protocol's exchange (fixed-capacity segments, equal splits to the peers, the
+    own segment copied locally, u32 local rows, source rank implied by the slot) gives the exact
+    membership answer (L1 + L2)."""
     from oracle import oracle as O
     cfg = (1 << 14, 2, 1 << 15, 3 << 13, 9)
     ctx = mp.get_context("spawn")
@@ -188,7 +196,8 @@ class HostOps:
         self.table, self.cf = O.Table(O.LP, own), cf
         return len(own)
 
-    def fixed_partitioner(self, n, world, sub_cap):
+    def fixed_partitioner(self, n, world, sub_cap, self_last):
+        import ccj_dist
         S = self.subs
 
         def run(keys, row_base, sk, sr, sc, status, stream):
@@ -198,7 +207,7 @@ class HostOps:
             for d in range(world):
                 for g in range(S):
                     idx = np.nonzero((owner == d) & (grp == g))[0]
-                    seg = d * S + g
+                    seg = ccj_dist.slot_of(d, self_last, world) * S + g  # the own rank's region last
                     sc[seg] = len(idx)
                     keep = idx[:sub_cap]
                     sk[seg * sub_cap:seg * sub_cap + len(keep)] = torch.from_numpy(k[keep])
@@ -234,9 +243,9 @@ class HostOps:
         if self.local_overflow:
             out["status"] |= 8  # CCJ_FLAG_PART_OVERFLOW
 
-    def group_rows(self, part, recv_rows, n_probe, seg_cap, slots, stream):
+    def group_rows(self, part, recv_rows, n_probe, seg_cap, slots, stream, src):
         q = np.arange(recv_rows.numel()) % slots
-        recv = (q // seg_cap) * n_probe + recv_rows.numpy().astype(np.int64)
+        recv = np.asarray(src, np.int64)[q // seg_cap] * n_probe + recv_rows.numpy().astype(np.int64)
         return recv[part["row_map"]]
 
     def checksum(self, out, chunk, row_map, stream):

@@ -103,15 +103,18 @@ def test_partition_fixed_overflow_flags_and_stays_in_bounds():
         assert (np_owner(kk[d * cap:(d + 1) * cap], parts) == d).all()
 
 
-@pytest.mark.parametrize("parts,n,base", [(1, 1000, 0), (2, 100000, 7), (8, 1234567, 1 << 20), (64, 500000, 3)])
-def test_partition_grouped_segments(parts, n, base):
+@pytest.mark.parametrize("parts,n,base,self_last", [(1, 1000, 0, -1), (2, 100000, 7, -1), (8, 1234567, 1 << 20, -1),
+                                                    (64, 500000, 3, -1), (1, 1000, 0, 0), (2, 100000, 7, 0),
+                                                    (8, 1234567, 1 << 20, 3), (8, 300000, 5, 7), (64, 500000, 3, 17)])
+def test_partition_grouped_segments(parts, n, base, self_last):
     """ccj_partition_by_owner_grouped (the one-pass split with the owner as partition): the 8
-    sub-segments of destination d hold exactly the owner-d (key, base + row) pairs between them (in
-    any order), their counts are the true counts, and nothing past a count is written."""
+    sub-segments of destination d's slot hold exactly the owner-d (key, base + row) pairs between
+    them (in any order), their counts are the true counts, and nothing past a count is written.
+    self_last = r: the own rank's region in the last slot, the peers' in rank order before it."""
     G = ccj.OWNER_GROUPS
     keys = O.uniform_keys(parts + 13, 0, n, 1 << 40)
     cap = ccj.grouped_sub_cap(n, parts, 256)
-    fp = ccj.GroupedOwnerPartitioner(n, parts, cap)
+    fp = ccj.GroupedOwnerPartitioner(n, parts, cap, self_last=self_last)
     ok = torch.full((parts * G * cap,), -7, dtype=torch.int64, device="cuda")
     orow = torch.zeros(parts * G * cap, dtype=torch.int32, device="cuda")
     cnt = torch.zeros(parts * G, dtype=torch.int64, device="cuda")
@@ -119,14 +122,16 @@ def test_partition_grouped_segments(parts, n, base):
     fp(torch.from_numpy(keys).cuda(), base, ok, orow, cnt, st)
     torch.cuda.synchronize()
     owner = np_owner(keys, parts)
-    c = cnt.cpu().numpy().reshape(parts, G)
+    slot = [d if self_last < 0 else (parts - 1 if d == self_last else d - (d > self_last)) for d in range(parts)]
+    assert sorted(slot) == list(range(parts))
+    c = cnt.cpu().numpy().reshape(parts, G)[slot]  # row d: destination d's sub-segment counts
     assert int(st.item()) == 0
     assert np.array_equal(c.sum(axis=1), np.bincount(owner, minlength=parts))
     k, r = ok.cpu().numpy(), orow.cpu().numpy()
     for d in range(parts):
         rows, ks = [], []
         for g in range(G):
-            lo = (d * G + g) * cap
+            lo = (slot[d] * G + g) * cap
             rows.append(r[lo:lo + c[d, g]].astype(np.int64) - base)
             ks.append(k[lo:lo + c[d, g]])
             assert (k[lo + c[d, g]:lo + cap] == -7).all()  # padding untouched
@@ -221,8 +226,8 @@ def test_bench_sharded_line():
     assert line["xgmi_bytes_per_step"] == 0  # one rank: nothing crosses xGMI
 
 
-@pytest.mark.parametrize("world", [2, 8])
-def test_bench_multi_rank_on_one_gpu(world):
+@pytest.mark.parametrize("world,scaling", [(2, "weak"), (8, "weak"), (2, "strong"), (8, "strong")])
+def test_bench_multi_rank_on_one_gpu(world, scaling):
     """The N > 1 HIP path as the driver's 8-GPU run takes it — bench.py --gpus N through its own
     launcher, N rank processes, DeviceOps with N owners (owner split into N destinations, the local
     table of 1/N of the build keys, received segments from N sources, the local partitioned probe) —
@@ -237,13 +242,14 @@ def test_bench_multi_rank_on_one_gpu(world):
     env["OMP_NUM_THREADS"] = "2"
     p = subprocess.run([sys.executable, "bench.py", "--gpus", str(world), "--backend", "gloo", "--same-device",
                         "--steps", "2", "--warmup", "1", "--no-cpu", "--n-build-per-gpu", str(1 << 19),
-                        "--n-probe", str(3 << 20), "--batches", "3", "--group", "2"],
+                        "--n-probe", str(3 << 20), "--batches", "3", "--group", "2", "--scaling", scaling],
                        cwd=root, capture_output=True, text=True, timeout=600, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, p.stdout
     line = json.loads(lines[0])
-    assert line["n_gpus"] == world and line["value"] > 0
+    assert line["n_gpus"] == world and line["value"] > 0 and line["scaling"] == scaling
+    assert line["config"]["n_probe_per_gpu"] == (3 << 20 if scaling == "weak" else (3 << 20) // world)
     assert line["parity"]["l1_ok"] and line["parity"]["l2_ok"], line["parity"]
     assert line["parity"]["exact_size_fallback_steps"] == 0
     assert line["xgmi_bytes_per_step"] > 0 and line["local_probe_ms"] > 0

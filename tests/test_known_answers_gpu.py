@@ -1,12 +1,14 @@
 """The reference's own answer vectors replayed on the GPU (SURVEY §4 / §8c known answers).
 
-tests/golden/known_answers.json holds 11 `sum_cases` recorded from the compiled reference
+tests/golden/known_answers.json holds 15 `sum_cases` recorded from the compiled reference
 (oracle/_ref/ref_driver: its LPHashTable / HashTable + Probe / Next loop): LP and chaining, B 256
-and 2048, cf 1/2/4, 100 % and 10 % hits, SplitMix64 and mt19937_64 probe streams, and the C2-size
+and 2048 (and 1000), cf 1/2/3/4, 100 % and 10 % hits, SplitMix64 and mt19937_64 probe streams, and the C2-size
 2^26-key LP table.  Each is replayed through the C ABI:
   - ccj_probe (probe_chunks): matches, L2, the order-sensitive L3 fold and the SURVEY checksum equal
     the reference's (L3);
-  - ccj_probe_ordered where the table has >= 2^22 slots / buckets: the same four values (L3);
+  - ccj_probe_ordered: the same four values (L3) — through its partitioned route where the table
+    has >= 2^22 slots / buckets (the C2-size LP vector and four chaining vectors of 2^23 buckets),
+    through its one-pass route below that;
   - ccj_probe_partitioned on a device-built table: CCJ_PART_ROWS where the keys are distinct
     (LP, cf 1), plain mode with the row map otherwise: matches and L2 (L1 + L2).
 And simd_micro_bench.cpp's known answer (`#tuples: 134217728` for all 8 variants at scale 0: 2^27
@@ -71,9 +73,12 @@ def test_reference_sum_vector_on_gpu(name, path):
     else:
         table = ccj.Table.reference(kind, n, cf, ccj.LAYOUT_REFERENCE)
         if path == "ordered":
-            if table.size < 1 << 22:
-                pytest.skip("ccj_probe_ordered's partitioned route needs >= 2^22 slots / buckets")
-            out = table.probe_ordered(keys, B, rounds=False)
+            # >= 2^22 slots / buckets: the partitioned route (split, L2-resident walk, unsplit,
+            # emit); below that the table is cache-resident and ccj_probe_ordered is one pass of
+            # probe_chunks — both must give the reference's L3 stream, so nothing is skipped
+            ws = table.alloc_ordered(keys.numel(), B)
+            assert (ws is not None) == (table.size >= 1 << 22)
+            out = table.probe_ordered(keys, B, rounds=False, ws=ws)
             assert not out.get("exact_retry")
         else:
             out = table.probe(keys, B, rounds=False)

@@ -277,6 +277,29 @@ def test_partitioned_probe_skew_falls_back_to_exact(distinct):
     assert ccj.result_checksum(out, 2048, row_map=out["row_map"].to(torch.int64)) == want
 
 
+@pytest.mark.parametrize("rows", [False, True])
+def test_partitioned_probe_skew_few_tiles_stays_one_pass(rows):
+    """Fewer rows than 8 split tiles: only some tile groups (XCDs) receive tiles, so each group's
+    overflow sub-area is sized from the rows one group can get, not 1/8 of the area.
+    40 % of the rows are one hot key: its run outgrows the partition's segment in every tile and
+    fits the group's sub-area — no exact-split fallback, exact L1 + L2."""
+    n_build, n_probe = 1 << 20, 30000
+    table = ccj.Table.reference(ccj.LP, n_build, 1, ccj.LAYOUT_DEVICE)
+    g = np.random.default_rng(77)
+    keys_h = g.integers(0, 2 * n_build, size=n_probe).astype(np.int64)
+    keys_h[g.random(n_probe) < 0.4] = 4242
+    keys = torch.from_numpy(keys_h).cuda()
+    out = table.probe_partitioned(keys, 2048, retry=False, rows=rows)
+    torch.cuda.synchronize()
+    assert int(out["status"].item()) == 0
+    hit = keys_h < n_build
+    r = np.nonzero(hit)[0].astype(np.uint64)
+    want = (len(r), O.l2_sum(r, keys_h[hit]))
+    got = ccj.result_checksum(out, 0) if rows else \
+        ccj.result_checksum(out, 2048, row_map=out["row_map"].to(torch.int64))
+    assert got == want
+
+
 def test_partitioned_probe_same_rows_as_chunk_probe():
     n_build, n_probe = 1 << 20, 1 << 21
     table = ccj.Table.reference(ccj.LP, n_build, 3, ccj.LAYOUT_REFERENCE)
@@ -463,6 +486,34 @@ def test_ordered_probe_chaining_equals_chunk_probe(n_build, cf, n_probe, chunk, 
     valid = np.arange(cap)[None, :] < want["count"].astype(np.int64)[:, None]
     assert np.array_equal(got["sel"].reshape(-1, cap)[valid], want["sel"].reshape(-1, cap)[valid])
     assert np.array_equal(got["payload"].reshape(-1, cap)[valid], want["payload"].reshape(-1, cap)[valid])
+
+
+@pytest.mark.parametrize("kind", ["lp", "chain"])
+@pytest.mark.parametrize("chunk,n_probe", [(1, 500), (4, 400), (7, 20), (64, 300)])
+def test_ordered_probe_small_inputs_equal_chunk_probe(kind, chunk, n_probe):
+    """Tiny chunks and few rows: the overflow area is then under 128 positions, so the ordered
+    route's split is the non-pipelined slot_split_fixed, which must leave each row's tile index
+    at its IMAGE position as the pipelined split does (it wrote it at the segment
+    destination, and the unsplit read stale workspace). L3 against ccj_probe."""
+    if kind == "lp":
+        table = ccj.Table.reference(ccj.LP, 1 << 20, 1, ccj.LAYOUT_REFERENCE)
+        keys = ccj.gen_uniform_keys(n_probe, 41 + chunk, 3 << 19)
+    else:
+        table = ccj.Table.reference(ccj.CHAIN, 1 << 21, 3, ccj.LAYOUT_REFERENCE)
+        keys = ccj.gen_uniform_keys(n_probe, 43 + chunk, (1 << 21) // 3)
+    assert table.size >= 1 << 22
+    want = host(table.probe(keys, chunk))
+    got = host(table.probe_ordered(keys, chunk))
+    assert got["status"][0] == 0 and want["status"][0] == 0 and not got.get("exact_retry")
+    assert want["count"].sum() > 0
+    assert np.array_equal(got["count"], want["count"])
+    assert np.array_equal(got["rounds"], want["rounds"])
+    assert np.array_equal(got["round_counts"], want["round_counts"])
+    cap = want["cap"]
+    valid = np.arange(cap)[None, :] < want["count"].astype(np.int64)[:, None]
+    assert np.array_equal(got["sel"].reshape(-1, cap)[valid], want["sel"].reshape(-1, cap)[valid])
+    assert np.array_equal(got["payload"].reshape(-1, cap)[valid], want["payload"].reshape(-1, cap)[valid])
+    table.free()
 
 
 def test_ordered_probe_c2_table_reference_vector():
