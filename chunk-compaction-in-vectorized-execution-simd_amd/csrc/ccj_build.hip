@@ -82,11 +82,19 @@ __global__ __launch_bounds__(256) void chain_records(const uint32_t *off, const 
     const uint64_t fp1 = len > 1 ? bucket_fp(murmurhash64((uint64_t)chain[lo + 1])) : 0u;
     rec8[b] = lo | (len & 0xFFull) << 32 | fp0 << 40 | fp1 << 52;
   }
+  // one atomic per workgroup (the grid is capped, so a few thousand): one per wave of a
+  // one-bucket-per-thread grid queued 2^21 atomics on one address (round 4: 23.8 ms for C3's table)
   for (int d = 32; d > 0; d >>= 1) {
     const uint32_t o = (uint32_t)__shfl_xor((int)best, d);
     best = o > best ? o : best;
   }
-  if ((threadIdx.x & 63u) == 0 && best) atomicMax(longest, best);
+  __shared__ uint32_t s_best[4];
+  if ((threadIdx.x & 63u) == 0) s_best[threadIdx.x >> 6] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t w = 1; w < blockDim.x / 64; ++w) best = s_best[w] > best ? s_best[w] : best;
+    if (best) atomicMax(longest, best);
+  }
 }
 
 // The bucket filter (probe_chain_filt): 2 bits per bucket, 16 buckets per word.
@@ -252,7 +260,7 @@ int build_chain_device(const int64_t *d_keys, uint64_t n, hipStream_t s, uint64_
   hipLaunchKernelGGL(chain_gather, dim3(grid_of(n_pad, 256)), dim3(256), 0, s, d_keys, idx_s.as<uint32_t>(), n, n_pad,
                      chain.as<int64_t>(), row.as<uint32_t>());
   BUILD_TRY(hipGetLastError(), "chain gather");
-  hipLaunchKernelGGL(chain_records, dim3(grid_of(n_rec8, 256)), dim3(256), 0, s, off.as<uint32_t>(),
+  hipLaunchKernelGGL(chain_records, dim3(std::min<unsigned>(grid_of(n_rec8, 256), 4096)), dim3(256), 0, s, off.as<uint32_t>(),
                      chain.as<int64_t>(), size, rec16.as<longlong2>(), rec8.as<uint64_t>(), n_rec8,
                      d_longest.as<uint32_t>());
   BUILD_TRY(hipGetLastError(), "bucket records");

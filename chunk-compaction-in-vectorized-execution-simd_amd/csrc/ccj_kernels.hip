@@ -1455,7 +1455,7 @@ __device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
   FiltQueue<WORDS> &q = s_q[wave];
-  const uint32_t x = blockIdx.x & 7u, k = blockIdx.x >> 3, K = gridDim.x >> 3;
+  const uint32_t x = blockIdx.x & 7u, k0 = blockIdx.x >> 3, K = gridDim.x >> 3;
   const uint32_t P = p.seg_parts;
   const uint32_t chunk = p.chunk;
   const uint32_t spc = (uint32_t)(p.seg_cap / chunk);  // chunks per segment
@@ -1470,15 +1470,21 @@ __device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *
   const bool rec8 = p.bucket8 != nullptr;
   const bool fm = WORDS ? p.w16 != 0u : p.first_match != 0u;  // distinct build keys
   const uint32_t stride = K * kWaves;
-  // match walk: the workgroup's units, in order — j = m * upc + kk is unit kk of its m-th chunk
-  const uint32_t n_mine = k < cpp ? (cpp - k + K - 1) / K : 0u;  // the workgroup's chunks per partition
-  const uint32_t nu = n_mine * upc;
   auto take = [&]() {  // wave-uniform: the workgroup's next unit
     uint32_t j = 0;
     if (lane == 0) j = atomicAdd(&s_s->next, 1u);
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)j);
   };
   for (uint32_t d = x * P / 8; d < (x + 1) * P / 8; ++d) {
+    // The workgroup's place among the XCD's K workgroups rotates with the partition.  With a fixed
+    // place, workgroup k took chunks k, k + K, ... of EVERY partition — the first cpp mod K
+    // workgroups one chunk more each time — so the others ran ahead by a chunk per partition and the
+    // XCD's workgroups spread over several partitions at once: their records and chains (3 MiB
+    // each) then shared the XCD's 4 MiB L2 (round 4 profile: 37 % of record / chain reads missed).
+    const uint32_t k = (k0 + d) % K;
+    // match walk: the workgroup's units, in order — j = m * upc + kk is unit kk of its m-th chunk
+    const uint32_t n_mine = k < cpp ? (cpp - k + K - 1) / K : 0u;  // the workgroup's chunks per partition
+    const uint32_t nu = n_mine * upc;
     __syncthreads();  // the previous partition's filter and chunk slots are no longer used
     for (uint32_t w = threadIdx.x * 4; w < fwords; w += NT * 4)
       *reinterpret_cast<u32x4 *>(&s_f[w]) = *reinterpret_cast<const u32x4 *>(p.filt + (uint64_t)d * fwords + w);

@@ -4,10 +4,13 @@
 // entries: every partition gets a run of exactly L entries per tile, reserved by one device atomic
 // per partition in segment (partition, g); each thread stores image entries q = it * 1024 + tid
 // (8-byte key + 4-byte row) at their run's destination.  2^30 entries per launch.
-//   runstore L off [what]     off = 0: every segment cursor starts at 0 (runs of 16 / 32 are
+//   runstore L off [what [P [G]]]  off = 0: every segment cursor starts at 0 (runs of 16 / 32 are
 //                             aligned to 128-byte key lines); off = 1: cursors start at a
 //                             per-segment offset in [1, 15] (runs never line-aligned)
-//   what = both | keys | rows
+//   runstore L off what P G pad: pad entries added to every segment's capacity (segment stride)
+//   what = both | keys | rows | read (both, plus each entry's 8-byte key read linearly from its tile);  P partitions (default 512, <= 1024);  G tile groups: 8 (a segment
+//   per partition and XCD, the split's layout: P x 8 write streams) or 1 (P streams, every XCD
+//   writing into every segment)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -23,24 +26,25 @@
     }                                                                          \
   } while (0)
 
-constexpr int T = 1024, P = 512;
+constexpr int T = 1024, PMAX = 1024;
 
-template <int WHAT>  // 0 both, 1 keys, 2 rows
+template <int WHAT>  // 0 both, 1 keys, 2 rows, 3 both + the tile's 8-byte keys read linearly (the split's loads)
 __global__ __launch_bounds__(T) void stores(int64_t *out_k, uint32_t *out_r, uint32_t *cur, uint64_t n_tiles,
-                                            uint64_t cap, uint32_t L) {
-  __shared__ uint64_t s_dst[P];
-  const uint32_t tid = threadIdx.x, g = blockIdx.x & 7u, bpg = gridDim.x >> 3;
+                                            uint64_t cap, uint32_t L, uint32_t P, uint32_t G, const int64_t *src) {
+  __shared__ uint64_t s_dst[PMAX];
+  const uint32_t tid = threadIdx.x, g = G == 8 ? blockIdx.x & 7u : 0u, bpg = G == 8 ? gridDim.x >> 3 : gridDim.x;
   const uint32_t tile = L * P;
-  const uint64_t tend = (g + 1) * n_tiles / 8;
-  for (uint64_t t = g * n_tiles / 8 + (blockIdx.x >> 3); t < tend; t += bpg) {
+  const uint64_t tend = (g + 1) * n_tiles / G;
+  for (uint64_t t = g * n_tiles / G + (G == 8 ? blockIdx.x >> 3 : blockIdx.x); t < tend; t += bpg) {
     if (tid < P) {
       const uint32_t r = atomicAdd(&cur[g * P + tid], L);
-      s_dst[tid] = ((uint64_t)tid * 8 + g) * cap + (r < cap - 64 ? r : 0u) - (uint64_t)tid * L;
+      s_dst[tid] = ((uint64_t)tid * G + g) * cap + (r < cap - 64 ? r : 0u) - (uint64_t)tid * L;
     }
     __syncthreads();
     for (uint32_t q = tid; q < tile; q += T) {
       const uint64_t dest = s_dst[q / L] + q;
-      if (WHAT != 2) out_k[dest] = (int64_t)q;
+      const int64_t v = WHAT == 3 ? __builtin_nontemporal_load(src + t * tile + q) : (int64_t)q;
+      if (WHAT != 2) out_k[dest] = v;
       if (WHAT != 1) out_r[dest] = q;
     }
     __syncthreads();
@@ -49,44 +53,55 @@ __global__ __launch_bounds__(T) void stores(int64_t *out_k, uint32_t *out_r, uin
 
 __global__ void init_cur(uint32_t *cur, uint32_t off) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < P * 8) cur[i] = off ? 1u + (i * 7u) % 15u : 0u;
+  if (i < PMAX * 8) cur[i] = off ? 1u + (i * 7u) % 15u : 0u;
 }
 
 int main(int argc, char **argv) {
   const uint32_t L = argc > 1 ? (uint32_t)atoi(argv[1]) : 22;
   const uint32_t off = argc > 2 ? (uint32_t)atoi(argv[2]) : 0;
-  const int what = argc > 3 ? (!strcmp(argv[3], "keys") ? 1 : !strcmp(argv[3], "rows") ? 2 : 0) : 0;
+  const int what = argc > 3 ? (!strcmp(argv[3], "keys") ? 1 : !strcmp(argv[3], "rows") ? 2 : !strcmp(argv[3], "read") ? 3 : 0) : 0;
+  const uint32_t P = argc > 4 ? (uint32_t)atoi(argv[4]) : 512;
+  const uint32_t G = argc > 5 && atoi(argv[5]) == 1 ? 1u : 8u;
+  const uint64_t pad = argc > 6 ? (uint64_t)atoll(argv[6]) : 0;  // entries added to every segment's capacity
+  if (P == 0 || P > (uint32_t)PMAX) return 2;
   const uint64_t n = 1ull << 30;
   const uint64_t tile = (uint64_t)L * P;
   const uint64_t n_tiles = (n + tile - 1) / tile;
-  const uint64_t cap = (uint64_t)((double)n / (8.0 * P) * 1.0625 + 8000 + 256) / 2048 * 2048 + 2048;
-  const uint64_t positions = (uint64_t)P * 8 * cap + 64;
+  const uint64_t cap = (uint64_t)((double)n / ((double)G * P) * 1.0625 + 8000 + 256) / 2048 * 2048 + 2048 + pad;
+  const uint64_t positions = (uint64_t)P * G * cap + 64;
   int64_t *k;
   uint32_t *r, *cur;
   CK(hipMalloc(&k, positions * 8));
   CK(hipMalloc(&r, positions * 4));
-  CK(hipMalloc(&cur, P * 8 * 4));
+  CK(hipMalloc(&cur, PMAX * 8 * 4));
+  int64_t *src = nullptr;
+  if (what == 3) {
+    CK(hipMalloc(&src, (n_tiles * tile) * 8));
+    CK(hipMemset(src, 3, (n_tiles * tile) * 8));
+  }
   int cus = 256;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const unsigned grid = cus / 8 * 8;
   float best = 1e30f;
   for (int rep = 0; rep < 5; ++rep) {
-    hipLaunchKernelGGL(init_cur, dim3((P * 8 + 255) / 256), dim3(256), 0, 0, cur, off);
+    hipLaunchKernelGGL(init_cur, dim3((PMAX * 8 + 255) / 256), dim3(256), 0, 0, cur, off);
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     CK(hipEventRecord(a, 0));
-    if (what == 0) hipLaunchKernelGGL(stores<0>, dim3(grid), dim3(T), 0, 0, k, r, cur, n_tiles, cap, L);
-    if (what == 1) hipLaunchKernelGGL(stores<1>, dim3(grid), dim3(T), 0, 0, k, r, cur, n_tiles, cap, L);
-    if (what == 2) hipLaunchKernelGGL(stores<2>, dim3(grid), dim3(T), 0, 0, k, r, cur, n_tiles, cap, L);
+    if (what == 0) hipLaunchKernelGGL(stores<0>, dim3(grid), dim3(T), 0, 0, k, r, cur, n_tiles, cap, L, P, G, src);
+    if (what == 1) hipLaunchKernelGGL(stores<1>, dim3(grid), dim3(T), 0, 0, k, r, cur, n_tiles, cap, L, P, G, src);
+    if (what == 2) hipLaunchKernelGGL(stores<2>, dim3(grid), dim3(T), 0, 0, k, r, cur, n_tiles, cap, L, P, G, src);
+    if (what == 3) hipLaunchKernelGGL(stores<3>, dim3(grid), dim3(T), 0, 0, k, r, cur, n_tiles, cap, L, P, G, src);
     CK(hipEventRecord(b, 0));
     CK(hipEventSynchronize(b));
     float ms = 0;
     CK(hipEventElapsedTime(&ms, a, b));
     if (rep) best = ms < best ? ms : best;
   }
-  const double bytes = (what == 0 ? 12.0 : what == 1 ? 8.0 : 4.0) * (double)n_tiles * tile;
-  printf("L %3u off %u %-4s %.3f ms  %.2f TB/s\n", L, off, what == 0 ? "both" : what == 1 ? "keys" : "rows", best,
+  const double bytes = (what == 0 ? 12.0 : what == 1 ? 8.0 : what == 2 ? 4.0 : 20.0) * (double)n_tiles * tile;
+  printf("L %3u off %u %-4s P %4u G %u pad %5lu  %.3f ms  %.2f TB/s\n", L, off,
+         what == 0 ? "both" : what == 1 ? "keys" : what == 2 ? "rows" : "read", P, G, (unsigned long)pad, best,
          bytes / (best * 1e-3) / 1e12);
   return 0;
 }
