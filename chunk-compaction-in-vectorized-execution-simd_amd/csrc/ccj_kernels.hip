@@ -1531,10 +1531,12 @@ __device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *
       unit_at(j < nu ? g : 8u, pc - g * spc, jj - m * upc, c, u0, uend);
     };
     auto load_keys = [&](uint64_t c, uint32_t u0, uint32_t uend, int64_t(&kk)[kJ]) {
+      // (timing only, tuning build: 0x10000 = keys from chunk c & 63, L2-resident lines)
+      const uint64_t kc = CCJ_ABLATED(p.ablate, 0x10000u) ? (c & 63u) : c;
 #pragma unroll
       for (int j = 0; j < (int)kJ; ++j) {
         const uint32_t i = u0 + (uint32_t)j * kWave + lane;
-        kk[j] = __builtin_nontemporal_load(p.keys + c * chunk + (i < uend ? i : u0));
+        kk[j] = __builtin_nontemporal_load(p.keys + kc * chunk + (i < uend ? i : u0));
       }
     };
     uint32_t g = 0, r = 0, j = 0, m = 0;
@@ -1564,6 +1566,10 @@ __device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *
         const bool ps = (i < uend) & ((code == 3u) | (code == filt_code_of(h)));  // (no branches)
         pass |= (ps ? 1u : 0u) << jj;
         bk[jj] = (uint32_t)h & p.mask;
+        // (timing only, tuning build: records and chains from the lower half / quarter of the
+        // partition's buckets — a smaller L2 working set, wrong results)
+        if (CCJ_ABLATED(p.ablate, 0x4000u)) bk[jj] &= ~(1u << (wb - 1u));
+        if (CCJ_ABLATED(p.ablate, 0x8000u)) bk[jj] &= ~(3u << (wb - 2u));
         kfp[jj] = ps ? bucket_fp(h) : code;  // (a rejected row keeps its code: 0 empty, else a one-key chain)
       }
       uint64_t rec[kJ];
