@@ -49,7 +49,9 @@ __global__ __launch_bounds__(256) void walk_emu(const int64_t *keys, const u32x4
   for (int j = 0; j < 8; ++j) {  // 8 rows per thread, one window per row (lane pairs)
     const uint64_t row = c * kChunk + (uint32_t)j * 256 + threadIdx.x;
     const int64_t k = __builtin_nontemporal_load(keys + row);
-    const uint32_t w = mix32((uint32_t)k ^ (uint32_t)(k >> 32)) & (kWinSlots / 4 - 1);  // 32-byte window
+    // a random 32-byte window of the partition's slice (the row index mixed in: the key column
+    // is constant here, its load only carries the walk's 8 bytes of key traffic)
+    const uint32_t w = mix32((uint32_t)row * 0x9E3779B9u ^ (uint32_t)k) & (kWinSlots / 4 - 1);
     // lanes 2q, 2q + 1 load the two 16-byte halves of lane 2q's window, then of lane 2q + 1's
     const uint32_t w0 = (uint32_t)__shfl((int)w, (int)(lane & ~1u)), w1 = (uint32_t)__shfl((int)w, (int)(lane | 1u));
     const u32x4 v0 = table[((uint64_t)part * kWinSlots / 4 + w0) * 2 + (lane & 1u)];
