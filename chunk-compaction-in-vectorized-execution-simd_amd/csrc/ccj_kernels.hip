@@ -1914,17 +1914,27 @@ __device__ __forceinline__ void wave_lds_sync() {
 template <uint32_t kWaveRows, bool HOME, typename SM>
 __device__ __forceinline__ void walk_stage(const ProbeParams &p, SM &sm, uint64_t base, uint32_t w0,
                                            uint32_t wend, uint32_t lane) {
-  int64_t v[kWaveRows / kWave];  // all loads in flight before the first LDS write
+  // all loads in flight before the first LDS write; lane L loads rows 2L, 2L + 1 of each 128-row
+  // block as one 16-byte load (half the load instructions; probe_walk2's stage, round 5)
+  typedef long long i64x2 __attribute__((ext_vector_type(2)));
+  constexpr int kH = (int)(kWaveRows / (2 * kWave));
+  static_assert(kWaveRows % (2 * kWave) == 0, "pairs of rows per lane");
+  i64x2 v[kH];
 #pragma unroll
-  for (int j = 0; j < (int)(kWaveRows / kWave); ++j) {
-    const uint32_t i = w0 + (uint32_t)j * kWave + lane;
-    v[j] = i < wend ? __builtin_nontemporal_load(p.keys + base + i) : 0;
+  for (int j = 0; j < kH; ++j) {
+    const uint32_t i = w0 + (uint32_t)j * 2u * kWave + 2u * lane;
+    v[j] = i < wend ? __builtin_nontemporal_load(reinterpret_cast<const i64x2 *>(p.keys + base + i)) : i64x2{0, 0};
+    if (i + 1 >= wend) v[j].y = 0;
   }
 #pragma unroll
-  for (int j = 0; j < (int)(kWaveRows / kWave); ++j) {
-    const uint32_t i = w0 + (uint32_t)j * kWave + lane;
-    sm.key[i] = v[j];
-    if (HOME) sm.hc[i] = (uint32_t)murmurhash64((uint64_t)v[j]) & p.mask;
+  for (int j = 0; j < kH; ++j) {
+    const uint32_t i = w0 + (uint32_t)j * 2u * kWave + 2u * lane;
+    *reinterpret_cast<i64x2 *>(&sm.key[i]) = v[j];
+    if (HOME) {
+      typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+      const u32x2 hh = {(uint32_t)murmurhash64((uint64_t)v[j].x) & p.mask, (uint32_t)murmurhash64((uint64_t)v[j].y) & p.mask};
+      *reinterpret_cast<u32x2 *>(&sm.hc[i]) = hh;
+    }
   }
   wave_lds_sync();
 }
@@ -2626,13 +2636,13 @@ __device__ __forceinline__ void stage_keys_aux(const int64_t *keys, uint32_t phy
   // the descriptor spans the chunk's live rows only: a load past them returns 0 (no access)
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<int64_t *>(keys), (short)0, (int)(phys * 8), 0x00020000);
 #pragma unroll
-  for (int j = 0; j < KJ; ++j) {
-    const uint32_t i = w0 + (uint32_t)j * kWave + lane;
+  for (int j = 0; j < KJ; ++j) {  // probe_walk2's row mapping: lane L holds rows 2L, 2L + 1 of each 128-row block
+    const uint32_t i = w0 + (uint32_t)(j >> 1) * 128u + 2u * lane + (uint32_t)(j & 1);
     k[j] = (int64_t)__builtin_amdgcn_raw_buffer_load_b64(rs, (int)(i * 8), 0, AUX);
   }
 #pragma unroll
   for (int j = 0; j < KJ; ++j)
-    if (w0 + (uint32_t)j * kWave + lane >= wend) k[j] = 0;
+    if (w0 + (uint32_t)(j >> 1) * 128u + 2u * lane + (uint32_t)(j & 1) >= wend) k[j] = 0;
 }
 #endif
 template <bool POS, int NB = 1>
@@ -2651,16 +2661,23 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
   const uint32_t w0 = wave * kWaveRows;
   const uint32_t wend = phys > w0 ? (phys - w0 < kWaveRows ? phys : w0 + kWaveRows) : w0;  // wave's rows [w0, wend)
   // stage: keys (all loads in flight first) and home slots stay in registers; the keys also go to
-  // LDS for phase B and the emit's compaction
+  // LDS for phase B and the emit's compaction.  Lane L holds rows 2L and 2L + 1 of each 128-row
+  // block (row_of(j)), so its keys arrive as 16-byte loads: half the load instructions of one
+  // key per lane and row (round 5, tools/overlap_emu.hip: the walk's pattern 6.11 -> 5.86-5.98 ms).
+  auto row_of = [&](int j) { return w0 + (uint32_t)(j >> 1) * 128u + 2u * lane + (uint32_t)(j & 1); };
   int64_t k[kJ];
   uint32_t h[kJ];
 #ifdef CCJ_TUNING
   if (p.key_aux == 0u) {
 #endif
+    typedef long long i64x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-    for (int j = 0; j < kJ; ++j) {
-      const uint32_t i = w0 + (uint32_t)j * kWave + lane;
-      k[j] = i < wend ? __builtin_nontemporal_load(p.keys + base + i) : 0;
+    for (int j = 0; j < kJ; j += 2) {
+      const uint32_t i = row_of(j);  // even: the pair (i, i + 1) lies inside the wave's 512 rows
+      const i64x2 v = i < wend ? __builtin_nontemporal_load(reinterpret_cast<const i64x2 *>(p.keys + base + i))
+                               : i64x2{0, 0};
+      k[j] = v.x;
+      k[j + 1] = i + 1 < wend ? v.y : 0;
     }
 #ifdef CCJ_TUNING
   } else {  // (tuning build only: p.key_aux = 1 + the buffer loads' cache-policy bits)
@@ -2678,7 +2695,7 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
 #endif
 #pragma unroll
   for (int j = 0; j < kJ; ++j) {
-    sm.key[w0 + (uint32_t)j * kWave + lane] = k[j];
+    sm.key[row_of(j)] = k[j];
     h[j] = (uint32_t)murmurhash64((uint64_t)k[j]) & p.mask;
   }
   CCJ_STAMP(t1);
@@ -2734,12 +2751,12 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
 #pragma unroll
   for (int j = 0; j < kJ; ++j) {
     ++steps;
-    const uint32_t i = w0 + (uint32_t)j * kWave + lane;
+    const uint32_t i = row_of(j);
     const bool valid = i < wend;
     const uint32_t s = sa[j];
     if (NB > 1) {
       if (j + 1 < kJ) {
-        issue(i + kWave < wend ? sa[j + 1] : 0u, (uint32_t)(j + 1) & 1u);
+        issue(row_of(j + 1) < wend ? sa[j + 1] : 0u, (uint32_t)(j + 1) & 1u);
         wait_vmcnt<2>();  // step j's two DMAs have landed (step j + 1's are in flight)
       } else {
         wait_vmcnt<0>();
@@ -2765,9 +2782,9 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
     int64_t bkey = 0;
     auto take = [&]() {
       if (!have && cont) {
-        const uint32_t j = (uint32_t)__builtin_ctz(cont);
+        const int j = __builtin_ctz(cont);
         cont &= cont - 1u;
-        bi = w0 + j * kWave + lane;
+        bi = row_of(j);
         bkey = sm.key[bi];
         bcur = sm.hc[bi];
         have = true;

@@ -36,7 +36,10 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
 
 constexpr uint32_t kChunk = 2048, kParts = 512, kWinSlots = 1u << 19;  // 4 MiB of 8-byte slots
 
-// walk: chunk order swizzled so that XCD x walks partitions [64x, 64x + 64) in order
+// walk: chunk order swizzled so that XCD x walks partitions [64x, 64x + 64) in order.
+// KEYS: 0 no key loads (windows only), 1 one 8-byte key per lane and row (the walk's form),
+// 2 two keys per 16-byte load (half the key load instructions, same lines)
+template <int KEYS>
 __global__ __launch_bounds__(256) void walk_emu(const int64_t *keys, const u32x4 *table, uint64_t n_chunks,
                                                 uint32_t *sink) {
   const uint64_t per = n_chunks / 8;
@@ -45,10 +48,20 @@ __global__ __launch_bounds__(256) void walk_emu(const int64_t *keys, const u32x4
   const uint32_t part = (uint32_t)(c * kParts / n_chunks);
   const uint32_t lane = threadIdx.x & 63u;
   uint32_t acc = 0;
+  int64_t kk[8];
+  if (KEYS == 2) {  // lane L loads rows 2L, 2L + 1 of each 512-row half: kk[j] for row j * 256 + tid
+    typedef long long i64x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const i64x2 v = __builtin_nontemporal_load(reinterpret_cast<const i64x2 *>(keys + c * kChunk + h * 512) + threadIdx.x);
+      kk[2 * h] = v.x;
+      kk[2 * h + 1] = v.y;
+    }
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {  // 8 rows per thread, one window per row (lane pairs)
     const uint64_t row = c * kChunk + (uint32_t)j * 256 + threadIdx.x;
-    const int64_t k = __builtin_nontemporal_load(keys + row);
+    const int64_t k = KEYS == 1 ? __builtin_nontemporal_load(keys + row) : KEYS == 2 ? kk[j] : (int64_t)row;
     // a random 32-byte window of the partition's slice (the row index mixed in: the key column
     // is constant here, its load only carries the walk's 8 bytes of key traffic)
     const uint32_t w = mix32((uint32_t)row * 0x9E3779B9u ^ (uint32_t)k) & (kWinSlots / 4 - 1);
@@ -112,8 +125,11 @@ int main(int argc, char **argv) {
   CK(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
   CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
   const uint64_t n_chunks = n / kChunk;
+  int kmode = 1;
   auto walk = [&](hipStream_t s) {
-    hipLaunchKernelGGL(walk_emu, dim3((unsigned)n_chunks), dim3(256), 0, s, keys, table, n_chunks, sink);
+    if (kmode == 0) hipLaunchKernelGGL(walk_emu<0>, dim3((unsigned)n_chunks), dim3(256), 0, s, keys, table, n_chunks, sink);
+    if (kmode == 1) hipLaunchKernelGGL(walk_emu<1>, dim3((unsigned)n_chunks), dim3(256), 0, s, keys, table, n_chunks, sink);
+    if (kmode == 2) hipLaunchKernelGGL(walk_emu<2>, dim3((unsigned)n_chunks), dim3(256), 0, s, keys, table, n_chunks, sink);
   };
   auto split = [&](hipStream_t s) {
     hipLaunchKernelGGL(init_cur, dim3(16), dim3(256), 0, s, cur);
@@ -146,6 +162,12 @@ int main(int argc, char **argv) {
     }
     return best;
   };
+  if (argc > 2) {  // overlap_emu WGS keys: the walk alone with each key-load form
+    for (kmode = 0; kmode < 3; ++kmode)
+      printf("walk alone, keys %s: %.3f ms\n", kmode == 0 ? "none" : kmode == 1 ? "8-byte loads" : "16-byte loads",
+             timed(2));
+    return 0;
+  }
   const float ts = timed(1), tw = timed(2), tb = timed(3);
   printf("split_wgs %u  split alone %.3f ms  walk alone %.3f ms  both %.3f ms  (sum %.3f, max %.3f)\n", split_wgs, ts,
          tw, tb, ts + tw, ts > tw ? ts : tw);

@@ -8,7 +8,9 @@
 //                             aligned to 128-byte key lines); off = 1: cursors start at a
 //                             per-segment offset in [1, 15] (runs never line-aligned)
 //   runstore L off what P G pad: pad entries added to every segment's capacity (segment stride)
-//   what = both | keys | rows | read (both, plus each entry's 8-byte key read linearly from its tile);  P partitions (default 512, <= 1024);  G tile groups: 8 (a segment
+//   what = both | keys | rows | read (both, plus each entry's 8-byte key read linearly from its tile,
+//   right before its store) | pref (the same with the split's schedule: the next tile's keys in
+//   flight while this tile's entries are stored; L x P must be 11264);  P partitions (default 512, <= 1024);  G tile groups: 8 (a segment
 //   per partition and XCD, the split's layout: P x 8 write streams) or 1 (P streams, every XCD
 //   writing into every segment)
 #include <hip/hip_runtime.h>
@@ -51,6 +53,42 @@ __global__ __launch_bounds__(T) void stores(int64_t *out_k, uint32_t *out_r, uin
   }
 }
 
+// pref: the split's own load schedule — the next tile's 11 keys per thread are loaded while this
+// tile's entries are stored (tiles of exactly 11 x 1024 entries: L x P = 11264)
+__global__ __launch_bounds__(T) void stores_pref(int64_t *out_k, uint32_t *out_r, uint32_t *cur, uint64_t n_tiles,
+                                                 uint64_t cap, uint32_t L, uint32_t P, uint32_t G, const int64_t *src) {
+  constexpr int PER = 11;
+  __shared__ uint64_t s_dst[PMAX];
+  const uint32_t tid = threadIdx.x, g = G == 8 ? blockIdx.x & 7u : 0u, bpg = G == 8 ? gridDim.x >> 3 : gridDim.x;
+  const uint32_t tile = L * P;  // == PER * T
+  const uint64_t tend = (g + 1) * n_tiles / G;
+  uint64_t t = g * n_tiles / G + (G == 8 ? blockIdx.x >> 3 : blockIdx.x);
+  if (t >= tend) return;
+  int64_t kc[PER], kn[PER];
+#pragma unroll
+  for (int it = 0; it < PER; ++it) kc[it] = __builtin_nontemporal_load(src + t * tile + it * T + tid);
+  for (; t < tend; t += bpg) {
+    const uint64_t tn = t + bpg < tend ? t + bpg : t;
+#pragma unroll
+    for (int it = 0; it < PER; ++it) kn[it] = __builtin_nontemporal_load(src + tn * tile + it * T + tid);
+    if (tid < P) {
+      const uint32_t r = atomicAdd(&cur[g * P + tid], L);
+      s_dst[tid] = ((uint64_t)tid * G + g) * cap + (r < cap - 64 ? r : 0u) - (uint64_t)tid * L;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      const uint32_t q = (uint32_t)it * T + tid;
+      const uint64_t dest = s_dst[q / L] + q;
+      out_k[dest] = kc[it];
+      out_r[dest] = q;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < PER; ++it) kc[it] = kn[it];
+  }
+}
+
 __global__ void init_cur(uint32_t *cur, uint32_t off) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < PMAX * 8) cur[i] = off ? 1u + (i * 7u) % 15u : 0u;
@@ -59,7 +97,8 @@ __global__ void init_cur(uint32_t *cur, uint32_t off) {
 int main(int argc, char **argv) {
   const uint32_t L = argc > 1 ? (uint32_t)atoi(argv[1]) : 22;
   const uint32_t off = argc > 2 ? (uint32_t)atoi(argv[2]) : 0;
-  const int what = argc > 3 ? (!strcmp(argv[3], "keys") ? 1 : !strcmp(argv[3], "rows") ? 2 : !strcmp(argv[3], "read") ? 3 : 0) : 0;
+  const int what = argc > 3 ? (!strcmp(argv[3], "keys") ? 1 : !strcmp(argv[3], "rows") ? 2 : !strcmp(argv[3], "read") ? 3
+                                : !strcmp(argv[3], "pref") ? 4 : 0) : 0;
   const uint32_t P = argc > 4 ? (uint32_t)atoi(argv[4]) : 512;
   const uint32_t G = argc > 5 && atoi(argv[5]) == 1 ? 1u : 8u;
   const uint64_t pad = argc > 6 ? (uint64_t)atoll(argv[6]) : 0;  // entries added to every segment's capacity
@@ -75,7 +114,8 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&r, positions * 4));
   CK(hipMalloc(&cur, PMAX * 8 * 4));
   int64_t *src = nullptr;
-  if (what == 3) {
+  if (what == 4 && L * P != 11264) return 2;
+  if (what >= 3) {
     CK(hipMalloc(&src, (n_tiles * tile) * 8));
     CK(hipMemset(src, 3, (n_tiles * tile) * 8));
   }
@@ -93,6 +133,7 @@ int main(int argc, char **argv) {
     if (what == 1) hipLaunchKernelGGL(stores<1>, dim3(grid), dim3(T), 0, 0, k, r, cur, n_tiles, cap, L, P, G, src);
     if (what == 2) hipLaunchKernelGGL(stores<2>, dim3(grid), dim3(T), 0, 0, k, r, cur, n_tiles, cap, L, P, G, src);
     if (what == 3) hipLaunchKernelGGL(stores<3>, dim3(grid), dim3(T), 0, 0, k, r, cur, n_tiles, cap, L, P, G, src);
+    if (what == 4) hipLaunchKernelGGL(stores_pref, dim3(grid), dim3(T), 0, 0, k, r, cur, n_tiles, cap, L, P, G, src);
     CK(hipEventRecord(b, 0));
     CK(hipEventSynchronize(b));
     float ms = 0;
@@ -100,8 +141,9 @@ int main(int argc, char **argv) {
     if (rep) best = ms < best ? ms : best;
   }
   const double bytes = (what == 0 ? 12.0 : what == 1 ? 8.0 : what == 2 ? 4.0 : 20.0) * (double)n_tiles * tile;
+  const char *wn[5] = {"both", "keys", "rows", "read", "pref"};
   printf("L %3u off %u %-4s P %4u G %u pad %5lu  %.3f ms  %.2f TB/s\n", L, off,
-         what == 0 ? "both" : what == 1 ? "keys" : what == 2 ? "rows" : "read", P, G, (unsigned long)pad, best,
+         wn[what], P, G, (unsigned long)pad, best,
          bytes / (best * 1e-3) / 1e12);
   return 0;
 }
