@@ -1452,7 +1452,11 @@ __device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *
                                                 FiltSlots *s_s) {
   constexpr uint32_t kJ = kFiltUnit / kWave;  // rows per lane and unit
   constexpr uint32_t kWaves = NT / kWave;
+  static_assert(kJ % 2 == 0, "pairs of rows per lane");
   const uint32_t lane = threadIdx.x & (kWave - 1);
+  // row jj of this lane inside the unit: rows 2L and 2L + 1 of each 128-row half, so the keys
+  // arrive as 16-byte loads (probe_walk2's stage, round 5)
+  auto urow = [&](int jj) { return (uint32_t)(jj >> 1) * 128u + 2u * lane + (uint32_t)(jj & 1); };
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
   FiltQueue<WORDS> &q = s_q[wave];
   const uint32_t x = blockIdx.x & 7u, k0 = blockIdx.x >> 3, K = gridDim.x >> 3;
@@ -1533,10 +1537,13 @@ __device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *
     auto load_keys = [&](uint64_t c, uint32_t u0, uint32_t uend, int64_t(&kk)[kJ]) {
       // (timing only, tuning build: 0x10000 = keys from chunk c & 63, L2-resident lines)
       const uint64_t kc = CCJ_ABLATED(p.ablate, 0x10000u) ? (c & 63u) : c;
+      typedef long long i64x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-      for (int j = 0; j < (int)kJ; ++j) {
-        const uint32_t i = u0 + (uint32_t)j * kWave + lane;
-        kk[j] = __builtin_nontemporal_load(p.keys + kc * chunk + (i < uend ? i : u0));
+      for (int j = 0; j < (int)kJ; j += 2) {
+        const uint32_t i = u0 + urow(j);  // even; row i + 1 is inside the unit's 256 positions
+        const i64x2 v = __builtin_nontemporal_load(reinterpret_cast<const i64x2 *>(p.keys + kc * chunk + (i < uend ? i : u0)));
+        kk[j] = v.x;
+        kk[j + 1] = v.y;
       }
     };
     uint32_t g = 0, r = 0, j = 0, m = 0;
@@ -1559,7 +1566,7 @@ __device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *
       uint32_t pass = 0, kfp[kJ], bk[kJ];
 #pragma unroll
       for (int jj = 0; jj < (int)kJ; ++jj) {
-        const uint32_t i = u0 + (uint32_t)jj * kWave + lane;
+        const uint32_t i = u0 + urow(jj);
         const uint64_t h = murmurhash64((uint64_t)kk[jj]);
         const uint32_t bl = (uint32_t)h & wmask;
         const uint32_t code = (s_f[bl >> 4] >> ((bl & 15u) * 2u)) & 3u;
@@ -1621,10 +1628,10 @@ __device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *
           q.cur[qi] = cur;
           q.lim[qi] = lim;
           if (WORDS) q.st[WORDS ? qi : 0] = st;
-          q.row[qi] = (uint8_t)((uint32_t)jj * kWave + lane);
+          q.row[qi] = (uint8_t)urow(jj);
         }
         if (WORDS) {
-          const uint32_t i = u0 + (uint32_t)jj * kWave + lane;
+          const uint32_t i = u0 + urow(jj);
           if (!act && i < uend) {
             const uint32_t len = lim - st;
             const uint32_t word = (pass >> jj) & 1u ? (len <= kMmRounds ? len << kMmRounds : kMmLong | len)
@@ -1655,7 +1662,7 @@ __device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *
               q.cur[e] = cur;
               q.lim[e] = lim;
               if (WORDS) q.st[WORDS ? e : 0] = st;
-              q.row[e] = (uint8_t)((uint32_t)jj * kWave + lane);
+              q.row[e] = (uint8_t)urow(jj);
             }
           }
         }
