@@ -937,11 +937,11 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
         with torch.cuda.stream(stream):
             cu_split = tuple(int(x) for x in args.cu_split.split(",")) if args.cu_split else None
             sp = ccj_dist.ShardedProbe(n_build_total, 1, n_probe, chunk, world, rank, batches=args.batches,
-                                       group=group, ops=ccj_dist.DeviceOps(cu_split=cu_split))
+                                       group=group, ops=ccj_dist.DeviceOps(cu_split=cu_split), keep_rows=True)
             keys = ccj.gen_uniform_keys(n_probe, SEED, n_build_total, first_row=rank * n_probe, stream=stream)
     else:
         sp = ccj_dist.ShardedProbe(n_build_total, 1, n_probe, chunk, world, rank, batches=args.batches, ops=ops,
-                                   group=group)
+                                   group=group, keep_rows=True)
         keys = ops.probe_keys(SEED, rank * n_probe, n_probe, n_build_total)
     o = sp.ops
     o.synchronize()

@@ -258,8 +258,12 @@ class ShardedProbe:
     """One rank's part of the multi-GPU probe of the C4 configuration."""
 
     def __init__(self, n_build_total: int, cf: int, n_probe: int, chunk: int, world: int, rank: int,
-                 stream=None, batches: int = 4, ops=None, group=GROUP):
+                 stream=None, batches: int = 4, ops=None, group=GROUP, keep_rows: bool = False):
+        """keep_rows: one send-row buffer per batch (4 B per send slot and batch: 4.3 GB per rank
+        at C4) instead of one per send slot, so that resolve_kept_groups can fetch a timed run's
+        probe rows afterwards."""
         self.ops = ops or DeviceOps()
+        self.keep_rows = keep_rows
         o = self.ops
         self.world, self.rank, self.chunk, self.n_probe = world, rank, chunk, n_probe
         # receive slot s holds source src_of_slot[s]'s segment (exchange_peers: peers, then own)
@@ -305,9 +309,9 @@ class ShardedProbe:
         self.fparts = {}
         mk = lambda dt, n: [o.zeros(n, dt) for _ in range(2)]  # noqa: E731
         self.sk, self.sc = mk(torch.int64, slots), mk(torch.int64, self.nseg)
-        # send rows: one buffer per batch (not per send slot), so a timed step's matches stay traceable
-        # to their probe rows after the step (4 B per slot: 4.3 GB per rank at C4)
-        self.srb = [o.zeros(slots, torch.int32) for _ in range(self.batches)]
+        # send rows: with keep_rows one buffer per batch, so a timed step's matches stay traceable to
+        # their probe rows after the step; otherwise one per send slot
+        self.srb = [o.zeros(slots, torch.int32) for _ in range(self.batches if self.keep_rows else 2)]
         self.rk, self.rr = mk(torch.int64, gslots), mk(torch.int32, gslots)
         self.rc = mk(torch.int64, self.group * self.nseg)
         self.cc = mk(torch.int32, gslots // self.chunk)
@@ -317,6 +321,10 @@ class ShardedProbe:
             part, out = o.alloc_group(gslots, self.chunk, self.status)
             self.parts.append(part)
             self.outs.append(out)
+
+    def _srb(self, j):
+        """Send-row buffer of run batch j (per batch with keep_rows, else per send slot j % 2)."""
+        return self.srb[j % self.batches] if self.keep_rows else self.srb[j % 2]
 
     def _batch(self, i):
         lo = i * self.bn
@@ -359,7 +367,7 @@ class ShardedProbe:
             self.fparts[n] = self.ops.fixed_partitioner(n, self.world, self.sub_cap, self.rank)
         self.pstream.wait_event(self.ev_comm[s])  # the previous all-to-all from send slot s is done
         with self._timed(self.part_events, self.pstream, timing):
-            self.fparts[n](keys[lo:lo + n], lo, self.sk[s], self.srb[j % self.batches], self.sc[s], self.status,
+            self.fparts[n](keys[lo:lo + n], lo, self.sk[s], self._srb(j), self.sc[s], self.status,
                            self.pstream)
         self.ev_part[s].record(self.pstream)
 
@@ -370,7 +378,7 @@ class ShardedProbe:
         if (j % self.batches) % self.group == 0:
             self.comm.wait_event(self.ev_probe[gs])  # the previous probe of receive group slot gs is done
         with self.ops.on(self.comm), self._timed(self.comm_events, self.comm, timing):
-            exchange_fixed(self.sk[s], self.srb[j % self.batches], self.sc[s], rk, rr, rc, self.world, self.rank,
+            exchange_fixed(self.sk[s], self._srb(j), self.sc[s], rk, rr, rc, self.world, self.rank,
                            self.seg_cap, self.subs, self.ops.copy, rows=rows)
         self.ev_comm[s].record(self.comm)
 
@@ -497,6 +505,8 @@ class ShardedProbe:
         global rows, batch indices covered).  Shows that a timed step's matches name their probe
         tuples although no row crossed during it.  Call right after run() (no verify)."""
         o = self.ops
+        if not self.keep_rows:
+            raise RuntimeError("resolve_kept_groups needs ShardedProbe(..., keep_rows=True)")
         if self.last_exact:
             raise RuntimeError("the last run fell back to the exact-size protocol: nothing kept")
         o.synchronize()

@@ -726,7 +726,12 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
     const uint32_t incl = wave_incl_scan(h);
     if (lane == 63) s_wsum[wave] = incl;
     uint32_t r = 0;
-    if (h) r = atomicAdd(&cur[(uint64_t)g * parts + opaque_v32(tid)], h);  // awaited after the stores are issued
+    if (h) {
+      if CCJ_ABLATED(ablate, 0x100000u)  // (timing: no reservation atomics — each tile an expected-size run)
+        r = (uint32_t)(((t - g * n_tiles / 8) * (kTileKeys / parts)) % (cap > 2 * kTileKeys ? cap - 2 * kTileKeys : 1));
+      else
+        r = atomicAdd(&cur[(uint64_t)g * parts + opaque_v32(tid)], h);  // awaited after the stores are issued
+    }
 #ifdef CCJ_SPLIT_STORES16
     stores16();
 #else
@@ -753,7 +758,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
     __syncthreads();
 #pragma unroll
     for (int it = 0; it < PER; ++it) {
-      if ((live >> it) & 1u) {
+      if (((live >> it) & 1u) && !CCJ_ABLATED(ablate, 0x200000u)) {  // (timing: 0x200000 no image scatter)
         const uint32_t d = dr[it] & 1023u;
         const uint32_t pos = s_loc[d] + (dr[it] >> 10);
         s_k[pos] = kc[it];
@@ -806,9 +811,29 @@ static hipError_t launch_owner_split_small(const int64_t *keys, uint64_t n, uint
   grid = grid < 8 ? 8 : grid;
   int64_t *sink_k = (int64_t *)sink;
   uint32_t *sink_r = (uint32_t *)((char *)sink + kSplitSinkBytes / 16 * 8);
+#ifdef CCJ_TUNING
+  // (A/B forms: CCJ_OWNER_FORM=1 4096-key tiles of 16 keys per thread, 2 = 512-thread workgroups)
+  const int form = ccj_tune_int("CCJ_OWNER_FORM", 0);
+  if (form == 1 || form == 2) {
+    const uint32_t tk = form == 1 ? 256u * 16u : 512u * 8u;
+    const uint64_t nt = (n + tk - 1) / tk;
+    const uint32_t pc = (uint32_t)ccj_tune_int("CCJ_OWNER_SMALL_PER_CU", form == 1 ? 3 : 2);
+    uint64_t gr = pc ? (uint64_t)stream_cus(s) * pc / 8 * 8 : (nt + 7) / 8 * 8;
+    gr = gr < 8 ? 8 : gr;
+    if (form == 1)
+      hipLaunchKernelGGL((slot_split_pipe<false, 256, 64, 16, false>), dim3((unsigned)gr), dim3(256), 0, s, keys, n, shift,
+                         parts, nt, cur, sub_cap, (uint64_t)0, (uint64_t)0, out_keys, out_rows, status, nullptr, 0u,
+                         nullptr, nullptr, row_base, sink_k, sink_r, (uint32_t)ccj_tune_int("CCJ_OWNER_ABLATE", 0), self_last);
+    else
+      hipLaunchKernelGGL((slot_split_pipe<false, 512, 64, 8, false>), dim3((unsigned)gr), dim3(512), 0, s, keys, n, shift,
+                         parts, nt, cur, sub_cap, (uint64_t)0, (uint64_t)0, out_keys, out_rows, status, nullptr, 0u,
+                         nullptr, nullptr, row_base, sink_k, sink_r, (uint32_t)ccj_tune_int("CCJ_OWNER_ABLATE", 0), self_last);
+    return hipGetLastError();
+  }
+#endif
   hipLaunchKernelGGL((slot_split_pipe<false, kT, 64, kPer, false>), dim3((unsigned)grid), dim3(kT), 0, s, keys, n, shift, parts,
                      n_tiles, cur, sub_cap, (uint64_t)0, (uint64_t)0, out_keys, out_rows, status, nullptr, 0u, nullptr,
-                     nullptr, row_base, sink_k, sink_r, 0u, self_last);
+                     nullptr, row_base, sink_k, sink_r, (uint32_t)ccj_tune_int("CCJ_OWNER_ABLATE", 0), self_last);
   return hipGetLastError();
 }
 

@@ -405,7 +405,7 @@ def _timed_resolve_worker(rank, world, port, cfg, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     n_build, cf, n_probe, rng, seed, chunk, batches, group, subs, steps = cfg
     ops = HostOps(subs=subs)
-    sp = ccj_dist.ShardedProbe(n_build, cf, n_probe, chunk, world, rank, batches=batches, ops=ops, group=group)
+    sp = ccj_dist.ShardedProbe(n_build, cf, n_probe, chunk, world, rank, batches=batches, ops=ops, group=group, keep_rows=True)
     keys = O.uniform_keys(seed, rank * n_probe, (rank + 1) * n_probe, rng)
     for rr in sp.rr:
         rr.fill_(-7)  # poisoned: a timed run moves no rows

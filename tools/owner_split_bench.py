@@ -1,6 +1,8 @@
 """Owner split alone (ON THE GPU BOX): ms per 2^25-key batch of ccj_partition_by_owner_grouped for
 1 and 8 owners, on an unmasked stream (the default half-CU grid) and on CU-masked streams of 64 / 128
-CUs (one workgroup per CU), nothing else running.  python3 tools/owner_split_bench.py [--lib tuning]"""
+CUs (one workgroup per CU), nothing else running.  python3 tools/owner_split_bench.py [--lib tuning]
+[--unmasked].  Tuning-build knobs: CCJ_OWNER_FORM (1: 4096-key tiles, 2: 512-thread workgroups),
+CCJ_OWNER_SMALL_PER_CU, CCJ_OWNER_ABLATE (0x10 no stores, 0x20 no key reads, 0x2000 no hash)."""
 import os
 import sys
 
@@ -32,15 +34,18 @@ def run(parts, stream, n=1 << 25, iters=20):
         p(keys, 0, ok, orr, oc, st, stream=stream)
     b.record(stream)
     torch.cuda.synchronize()
-    assert int(oc.sum().item()) == n and int(st.item()) == 0
+    if not os.environ.get("CCJ_OWNER_ABLATE"):  # (timing ablations write wrong outputs)
+        assert int(oc.sum().item()) == n and int(st.item()) == 0
     return a.elapsed_time(b) / iters
 
 
 def main():
     print({k: v for k, v in os.environ.items() if k.startswith("CCJ_")})
-    streams = {"unmasked (half-CU grid)": torch.cuda.Stream(),
+    streams = {"unmasked": torch.cuda.Stream(),
                "masked 64 CUs": ccj.cu_masked_stream(ccj.cu_mask_groups(set(range(24, 32)))),
                "masked 128 CUs": ccj.cu_masked_stream(ccj.cu_mask_groups(set(range(16, 32))))}
+    if "--unmasked" in sys.argv:
+        streams = {k: v for k, v in streams.items() if k.startswith("unmasked")}
     for parts in (1, 8):
         for name, s in streams.items():
             ms = run(parts, s)
