@@ -46,6 +46,17 @@ __host__ __device__ __forceinline__ uint64_t murmurhash64(uint64_t x) {
   return x;
 }
 
+// The high 32 bits of murmurhash64(x) (the last xor-shift leaves them as the second product's
+// high word, which needs three 32-bit multiplies, not four).
+__host__ __device__ __forceinline__ uint32_t murmurhash64_hi(uint64_t x) {
+  constexpr uint64_t kC = 0xd6e8feb86659fd93ULL;
+  x ^= x >> 32;
+  x *= kC;
+  x ^= x >> 32;
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return (uint32_t)(((uint64_t)lo * (uint32_t)kC) >> 32) + lo * (uint32_t)(kC >> 32) + hi * (uint32_t)kC;
+}
+
 // Fingerprint of a chain key for the 8-byte bucket records: 12 hash bits far above any bucket index.
 __host__ __device__ __forceinline__ uint32_t bucket_fp(uint64_t h) { return (uint32_t)(h >> 52); }
 // 8-byte bucket record {start | len << 32 | fp(node 0) << 40 | fp(node 1) << 52} (len < 256): the

@@ -693,8 +693,12 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
     uint32_t dr[PER];  // partition | rank in it << 10 (one register per key: no spills at 11 keys)
 #pragma unroll
     for (int it = 0; it < PER; ++it) {
+      // (the owner split's small forms — launch_owner_split_small only: shift = 64 - log2(parts) or
+      // mask 0 — need only the hash's high word: one 32-bit product fewer)
+      constexpr bool kOwnerHi = MAXP <= 64 && THREADS <= 512;
       const uint32_t d0 = CCJ_ABLATED(ablate, 0x2000u) ? (uint32_t)((uint64_t)kc[it] >> shift) & mask  // (timing: no hash)
-                                                       : (uint32_t)(murmurhash64((uint64_t)kc[it]) >> shift) & mask;
+                          : kOwnerHi ? (murmurhash64_hi((uint64_t)kc[it]) >> ((shift - 32u) & 31u)) & mask
+                                     : (uint32_t)(murmurhash64((uint64_t)kc[it]) >> shift) & mask;
       if constexpr (MAXP <= 64) {
         // few partitions (the owner split: one per rank): an LDS atomic per key would queue the
         // wave's 64 lanes on at most `parts` addresses (one address at N = 1).  Instead one ballot
@@ -702,13 +706,16 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
         // (distinct addresses), and each lane takes its partition's base from that lane.
         const uint32_t d = self_slot(d0, self_last, parts);  // (the owner split: own rank's segment last)
         const bool lv = (live >> it) & 1u;
-        uint32_t wcnt = 0;
-        uint64_t mine = 0;
-        for (uint32_t q = 0; q < parts; ++q) {
-          const uint64_t b = __ballot(lv && d == q);
-          if (lane == q) wcnt = (uint32_t)__popcll(b);
-          if (d == q) mine = b;
+        // bit-sliced: one ballot per partition-index bit; a lane's mask keeps the live lanes that
+        // agree with its partition (mine) / with partition `lane` (pm) on every bit — log2(parts)
+        // ballots instead of parts (owner split alone, 8 owners, ranking only: see DESIGN §5)
+        uint64_t mine = __ballot(lv), pm = mine;
+        for (uint32_t b = 0; (1u << b) < parts; ++b) {
+          const uint64_t bb = __ballot((d >> b) & 1u);
+          mine &= (d >> b) & 1u ? bb : ~bb;
+          pm &= (lane >> b) & 1u ? bb : ~bb;
         }
+        const uint32_t wcnt = (uint32_t)__popcll(pm);
         const uint32_t base = lane < parts && wcnt ? atomicAdd(&s_hist[lane], wcnt) : 0u;
         const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
         const uint32_t rk = (uint32_t)__shfl((int)base, (int)d) + below;
@@ -769,6 +776,13 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
     p_t0 = t0;
     have_prev = 1u;
   };
+  if CCJ_ABLATED(ablate, 0x200000u) {  // (timing, no image scatter: every image entry names partition 0,
+    // whose run bounds every store, so the stale image stays inside reserved space)
+    for (uint32_t q = tid; q < kTileKeys; q += THREADS) {
+      s_k[q] = 0;
+      s_i[q] = q & 0xFFFFu;
+    }
+  }
   int64_t kA[PER], kB[PER];
   uint32_t cA = 0, cB = 0;
   load(tile, kA, cA);

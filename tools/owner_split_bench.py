@@ -1,6 +1,6 @@
 """Owner split alone (ON THE GPU BOX): ms per 2^25-key batch of ccj_partition_by_owner_grouped for
 1 and 8 owners, on an unmasked stream (the default half-CU grid) and on CU-masked streams of 64 / 128
-CUs (one workgroup per CU), nothing else running.  python3 tools/owner_split_bench.py [--lib tuning]
+CUs (one workgroup per CU), nothing else running.  python3 tools/owner_split_bench.py [--lib tuning|PATH]
 [--unmasked].  Tuning-build knobs: CCJ_OWNER_FORM (1: 4096-key tiles, 2: 512-thread workgroups),
 CCJ_OWNER_SMALL_PER_CU, CCJ_OWNER_ABLATE (0x10 no stores, 0x20 no key reads, 0x2000 no hash)."""
 import os
@@ -12,8 +12,10 @@ import torch  # noqa: E402
 
 import ccj  # noqa: E402
 
-if "--lib" in sys.argv and sys.argv[sys.argv.index("--lib") + 1] == "tuning":
-    ccj.LIB_PATH = os.path.join(ROOT, "chunk-compaction-in-vectorized-execution-simd_amd", "libccj_tuning.so")
+if "--lib" in sys.argv:  # tuning, or the path of another build (A/B)
+    _lib = sys.argv[sys.argv.index("--lib") + 1]
+    ccj.LIB_PATH = (os.path.join(ROOT, "chunk-compaction-in-vectorized-execution-simd_amd", "libccj_tuning.so")
+                    if _lib == "tuning" else os.path.abspath(_lib))
 
 
 def run(parts, stream, n=1 << 25, iters=20):
