@@ -800,6 +800,153 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
   if (dropped && status) atomicOr(status, CCJ_FLAG_PART_OVERFLOW);
 }
 
+// owner_split_direct: the owner split (<= 64 destinations) without the workgroup's tile image.
+// Per tile:
+//   rank (one ballot per destination-index bit; the wave's running count of destination p in lane
+//   p) | [WIMG: the wave's 64 x PER keys written to its own LDS image in destination order] |
+//   barrier | one reservation atomic per destination for the workgroup's whole run, split into the
+//   waves' runs | barrier | stores
+// Without WIMG each lane stores its keys where they rank: a store instruction's 64 lanes write
+// one piece per destination (8 B x ~64 / parts).  With WIMG a wave stores its image in order:
+// whole runs of ~64 x PER / parts keys, as slot_split_pipe's image does for the workgroup — but
+// the image is the wave's own (written and read back by the same wave: no barrier guards it),
+// and two barriers per tile instead of four.  Same tiles, tile groups and segment layout as
+// slot_split_pipe's small form (partition_grouped_sub_cap sizes them); the order inside a
+// segment is free ("in any order").  Inactive lanes store to the per-XCD sink, so every store is
+// unconditional (as in the pipe).
+template <int PER, bool WIMG>
+__global__ __launch_bounds__(256) void owner_split_direct(const int64_t *keys, uint64_t n, uint32_t shift,
+                                                          uint32_t parts, uint64_t n_tiles, uint32_t *cur,
+                                                          uint64_t cap, int64_t *out_k, uint32_t *out_r,
+                                                          uint32_t *status, uint32_t row_base, int64_t *sink_k,
+                                                          uint32_t *sink_r, uint32_t self_last, uint32_t ablate) {
+  constexpr uint32_t T = 256, kTile = T * PER, kWaves = T / 64, kWaveKeys = 64 * PER;
+  __shared__ uint32_t s_cnt[kWaves][64];   // wave w's keys of destination p in this tile
+  __shared__ uint32_t s_base[kWaves][64];  // their run's first position in segment (p, g) [WIMG: - image offset]
+  __shared__ int64_t s_wk[WIMG ? kWaves : 1][WIMG ? kWaveKeys : 1];   // [WIMG] wave images: key
+  __shared__ uint32_t s_wr[WIMG ? kWaves : 1][WIMG ? kWaveKeys : 1];  // and row in the wave's block | dest << 16
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t g = blockIdx.x & 7u, bpg = gridDim.x >> 3;
+  const uint32_t mask = parts - 1;
+  const uint64_t tend = (g + 1) * n_tiles / 8;
+  uint64_t tile = g * n_tiles / 8 + (blockIdx.x >> 3);
+  if (tile >= tend) return;
+  sink_k += g * 8;
+  sink_r += g * 8;
+  // wave w takes the tile's keys [w * 64 * PER, (w + 1) * 64 * PER): key it of lane L at it * 64 + L
+  auto load = [&](uint64_t t, int64_t(&kk)[PER]) {
+    const uint64_t tt = t < tend ? t : tend - 1;  // the last prefetch re-reads a valid tile
+    const uint64_t i0 = tt * kTile + wave * kWaveKeys + lane;
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      const uint64_t i = i0 + (uint32_t)it * 64u;
+      kk[it] = __builtin_nontemporal_load(keys + (i < n ? i : 0u));
+    }
+  };
+  bool dropped = false;
+  int64_t kA[PER], kB[PER];
+  auto step = [&](uint64_t t, int64_t(&kc)[PER], int64_t(&kn)[PER]) {
+    load(t + bpg, kn);
+    const uint64_t w0 = t * kTile + wave * kWaveKeys;  // the wave's first key
+    uint32_t dr[PER];  // destination | rank in the wave's run << 8 (0xFFFFFFFF: no key)
+    uint32_t cum = 0;  // lane p < parts: the wave's keys of destination p so far
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      const bool lv = w0 + (uint32_t)it * 64u + lane < n;
+      const uint32_t d =
+          self_slot((murmurhash64_hi((uint64_t)kc[it]) >> ((shift - 32u) & 31u)) & mask, self_last, parts);
+      uint64_t mine = __ballot(lv), pm = mine;
+      for (uint32_t b = 0; (1u << b) < parts; ++b) {
+        const uint64_t bb = __ballot((d >> b) & 1u);
+        mine &= (d >> b) & 1u ? bb : ~bb;
+        pm &= (lane >> b) & 1u ? bb : ~bb;
+      }
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
+      const uint32_t pre = (uint32_t)__shfl((int)cum, (int)d);
+      dr[it] = lv ? d | (pre + below) << 8 : 0xFFFFFFFFu;
+      cum += (uint32_t)__popcll(pm);
+    }
+    const uint32_t mine_cnt = lane < parts ? cum : 0u;
+    uint32_t wloc = 0, wtot = 0;  // lane p: destination p's offset in the wave image; the image's length
+    if constexpr (WIMG) {
+      const uint32_t incl = wave_incl_scan(mine_cnt);
+      wloc = incl - mine_cnt;
+      wtot = (uint32_t)__shfl((int)incl, 63);
+#pragma unroll
+      for (int it = 0; it < PER; ++it) {
+        // (the shuffle with every lane active: a lane reading an inactive lane's value gets 0)
+        const uint32_t d = dr[it] & 63u;
+        const uint32_t q = (uint32_t)__shfl((int)wloc, (int)d) + (dr[it] >> 8);
+        if (dr[it] != 0xFFFFFFFFu) {
+          s_wk[wave][q] = kc[it];
+          s_wr[wave][q] = ((uint32_t)it * 64u + lane) | d << 16;
+        }
+      }
+    }
+    if (lane < parts) s_cnt[wave][lane] = cum;
+    __syncthreads();
+    if (tid < parts) {
+      uint32_t tot = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < kWaves; ++w) tot += s_cnt[w][tid];
+      uint32_t r = 0;
+      if (tot) {
+        if CCJ_ABLATED(ablate, 0x100000u)  // (timing: no reservation atomics)
+          r = (uint32_t)(((t - g * n_tiles / 8) * (kTile / parts)) % (cap > 2 * kTile ? cap - 2 * kTile : 1));
+        else
+          r = atomicAdd(&cur[(uint64_t)g * parts + tid], tot);
+      }
+#pragma unroll
+      for (uint32_t w = 0; w < kWaves; ++w) {
+        s_base[w][tid] = r;
+        r += s_cnt[w][tid];
+      }
+    }
+    __syncthreads();
+    if constexpr (WIMG) {
+      // lane p < parts: its run's base minus its image offset, so entry q of destination d is
+      // stored at position base_d + q (mod 2^32)
+      const uint32_t adj = lane < parts ? s_base[wave][lane] - wloc : 0u;
+#pragma unroll
+      for (int it = 0; it < PER; ++it) {
+        const uint32_t q = (uint32_t)it * 64u + lane;
+        const uint32_t e = s_wr[wave][q];
+        const uint32_t d = (e >> 16) & 63u;
+        const uint32_t base = (uint32_t)__shfl((int)adj, (int)d);  // (every lane active)
+        const uint32_t pos = q < wtot ? base + q : 0xFFFFFFFFu;
+        const bool act = pos < cap;
+        dropped |= q < wtot && !act;
+        const uint64_t dest = ((uint64_t)d * 8 + g) * cap + pos;
+        if CCJ_ABLATED(ablate, 0x10u) continue;  // (timing: no stores)
+        *(act ? out_k + dest : sink_k) = s_wk[wave][q];
+        *(act ? out_r + dest : sink_r) = row_base + (uint32_t)(w0 + (e & 0xFFFFu));
+      }
+    } else {
+#pragma unroll
+      for (int it = 0; it < PER; ++it) {
+        const uint32_t d = dr[it] & 0xFFu;
+        const uint32_t pos = dr[it] == 0xFFFFFFFFu ? 0xFFFFFFFFu : s_base[wave][d & 63u] + (dr[it] >> 8);
+        const bool act = pos < cap;
+        dropped |= dr[it] != 0xFFFFFFFFu && !act;
+        const uint64_t dest = ((uint64_t)d * 8 + g) * cap + pos;
+        if CCJ_ABLATED(ablate, 0x10u) continue;  // (timing: no stores)
+        *(act ? out_k + dest : sink_k) = kc[it];
+        *(act ? out_r + dest : sink_r) = row_base + (uint32_t)(w0 + (uint32_t)it * 64u + lane);
+      }
+    }
+  };
+  load(tile, kA);
+  for (;;) {
+    step(tile, kA, kB);
+    tile += bpg;
+    if (tile >= tend) break;
+    step(tile, kB, kA);
+    tile += bpg;
+    if (tile >= tend) break;
+  }
+  if (dropped && status) atomicOr(status, CCJ_FLAG_PART_OVERFLOW);
+}
+
 }  // namespace
 
 // The owner split in small workgroups (the multi-GPU step): slot_split_pipe with 256 threads and
@@ -809,6 +956,9 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
 // kernel trace of the one-rank rehearsal: no partition ran during any walk), while 26 KB
 // workgroups take the slots the walk's retiring workgroups free.  Persistent, 4 per CU of the
 // stream (a multiple of 8: one tile group per XCD).
+// owner_split_direct's persistent workgroups per CU (the wave-image form's occupancy: 87 VGPRs)
+constexpr uint32_t kOwnerDirectPerCu = 5;
+
 static hipError_t launch_owner_split_small(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t shift,
                                           uint64_t sub_cap, uint32_t *cur, int64_t *out_keys, uint32_t *out_rows,
                                           uint32_t *status, uint32_t row_base, void *sink, hipStream_t s,
@@ -825,6 +975,20 @@ static hipError_t launch_owner_split_small(const int64_t *keys, uint64_t n, uint
   grid = grid < 8 ? 8 : grid;
   int64_t *sink_k = (int64_t *)sink;
   uint32_t *sink_r = (uint32_t *)((char *)sink + kSplitSinkBytes / 16 * 8);
+  const int direct = ccj_tune_int("CCJ_OWNER_DIRECT", 2);  // (tuning build: 0 = slot_split_pipe's small form below,
+  if (direct) {                                            // 1 = owner_split_direct without wave images)
+    const uint32_t pc = (uint32_t)ccj_tune_int("CCJ_OWNER_DIRECT_PER_CU", kOwnerDirectPerCu);
+    uint64_t gr = pc ? (uint64_t)stream_cus(s) * pc / 8 * 8 : (n_tiles + 7) / 8 * 8;
+    gr = gr < 8 ? 8 : gr;
+    const uint32_t abl = (uint32_t)ccj_tune_int("CCJ_OWNER_ABLATE", 0);
+    if (direct == 1)
+      hipLaunchKernelGGL((owner_split_direct<kPer, false>), dim3((unsigned)gr), dim3(kT), 0, s, keys, n, shift, parts,
+                         n_tiles, cur, sub_cap, out_keys, out_rows, status, row_base, sink_k, sink_r, self_last, abl);
+    else
+      hipLaunchKernelGGL((owner_split_direct<kPer, true>), dim3((unsigned)gr), dim3(kT), 0, s, keys, n, shift, parts,
+                         n_tiles, cur, sub_cap, out_keys, out_rows, status, row_base, sink_k, sink_r, self_last, abl);
+    return hipGetLastError();
+  }
 #ifdef CCJ_TUNING
   // (A/B forms: CCJ_OWNER_FORM=1 4096-key tiles of 16 keys per thread, 2 = 512-thread workgroups)
   const int form = ccj_tune_int("CCJ_OWNER_FORM", 0);
