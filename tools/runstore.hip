@@ -10,7 +10,8 @@
 //   runstore L off what P G pad: pad entries added to every segment's capacity (segment stride)
 //   what = both | keys | rows | read (both, plus each entry's 8-byte key read linearly from its tile,
 //   right before its store) | pref (the same with the split's schedule: the next tile's keys in
-//   flight while this tile's entries are stored; L x P must be 11264);  P partitions (default 512, <= 1024);  G tile groups: 8 (a segment
+//   flight while this tile's entries are stored; L x P must be 11264) | pref16 (pref, keys loaded as
+//   16-byte pairs);  P partitions (default 512, <= 1024);  G tile groups: 8 (a segment
 //   per partition and XCD, the split's layout: P x 8 write streams) or 1 (P streams, every XCD
 //   writing into every segment)
 #include <hip/hip_runtime.h>
@@ -89,6 +90,51 @@ __global__ __launch_bounds__(T) void stores_pref(int64_t *out_k, uint32_t *out_r
   }
 }
 
+// pref16: pref with the keys loaded as 16-byte pairs (2 tid, 2 tid + 1 of each 2048-entry block, the
+// 11th key per thread as one 8-byte load); the stores as in pref (their addresses do not depend on
+// how the keys were loaded: in the split they come from the LDS image)
+__global__ __launch_bounds__(T) void stores_pref16(int64_t *out_k, uint32_t *out_r, uint32_t *cur, uint64_t n_tiles,
+                                                   uint64_t cap, uint32_t L, uint32_t P, uint32_t G, const int64_t *src) {
+  constexpr int PER = 11;
+  typedef long long i64x2 __attribute__((ext_vector_type(2)));
+  __shared__ uint64_t s_dst[PMAX];
+  const uint32_t tid = threadIdx.x, g = G == 8 ? blockIdx.x & 7u : 0u, bpg = G == 8 ? gridDim.x >> 3 : gridDim.x;
+  const uint32_t tile = L * P;  // == PER * T
+  const uint64_t tend = (g + 1) * n_tiles / G;
+  uint64_t t = g * n_tiles / G + (G == 8 ? blockIdx.x >> 3 : blockIdx.x);
+  if (t >= tend) return;
+  int64_t kc[PER], kn[PER];
+  auto load = [&](uint64_t tt, int64_t(&kk)[PER]) {
+#pragma unroll
+    for (int j = 0; j < PER / 2; ++j) {
+      const i64x2 v = __builtin_nontemporal_load(reinterpret_cast<const i64x2 *>(src + tt * tile + j * 2 * T + 2 * tid));
+      kk[2 * j] = v.x;
+      kk[2 * j + 1] = v.y;
+    }
+    kk[PER - 1] = __builtin_nontemporal_load(src + tt * tile + (PER - 1) * T + tid);
+  };
+  load(t, kc);
+  for (; t < tend; t += bpg) {
+    const uint64_t tn = t + bpg < tend ? t + bpg : t;
+    load(tn, kn);
+    if (tid < P) {
+      const uint32_t r = atomicAdd(&cur[g * P + tid], L);
+      s_dst[tid] = ((uint64_t)tid * G + g) * cap + (r < cap - 64 ? r : 0u) - (uint64_t)tid * L;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      const uint32_t q = (uint32_t)it * T + tid;
+      const uint64_t dest = s_dst[q / L] + q;
+      out_k[dest] = kc[it];
+      out_r[dest] = q;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < PER; ++it) kc[it] = kn[it];
+  }
+}
+
 __global__ void init_cur(uint32_t *cur, uint32_t off) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < PMAX * 8) cur[i] = off ? 1u + (i * 7u) % 15u : 0u;
@@ -98,7 +144,7 @@ int main(int argc, char **argv) {
   const uint32_t L = argc > 1 ? (uint32_t)atoi(argv[1]) : 22;
   const uint32_t off = argc > 2 ? (uint32_t)atoi(argv[2]) : 0;
   const int what = argc > 3 ? (!strcmp(argv[3], "keys") ? 1 : !strcmp(argv[3], "rows") ? 2 : !strcmp(argv[3], "read") ? 3
-                                : !strcmp(argv[3], "pref") ? 4 : 0) : 0;
+                                : !strcmp(argv[3], "pref") ? 4 : !strcmp(argv[3], "pref16") ? 5 : 0) : 0;
   const uint32_t P = argc > 4 ? (uint32_t)atoi(argv[4]) : 512;
   const uint32_t G = argc > 5 && atoi(argv[5]) == 1 ? 1u : 8u;
   const uint64_t pad = argc > 6 ? (uint64_t)atoll(argv[6]) : 0;  // entries added to every segment's capacity
@@ -114,7 +160,7 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&r, positions * 4));
   CK(hipMalloc(&cur, PMAX * 8 * 4));
   int64_t *src = nullptr;
-  if (what == 4 && L * P != 11264) return 2;
+  if (what >= 4 && L * P != 11264) return 2;
   if (what >= 3) {
     CK(hipMalloc(&src, (n_tiles * tile) * 8));
     CK(hipMemset(src, 3, (n_tiles * tile) * 8));
@@ -134,6 +180,7 @@ int main(int argc, char **argv) {
     if (what == 2) hipLaunchKernelGGL(stores<2>, dim3(grid), dim3(T), 0, 0, k, r, cur, n_tiles, cap, L, P, G, src);
     if (what == 3) hipLaunchKernelGGL(stores<3>, dim3(grid), dim3(T), 0, 0, k, r, cur, n_tiles, cap, L, P, G, src);
     if (what == 4) hipLaunchKernelGGL(stores_pref, dim3(grid), dim3(T), 0, 0, k, r, cur, n_tiles, cap, L, P, G, src);
+    if (what == 5) hipLaunchKernelGGL(stores_pref16, dim3(grid), dim3(T), 0, 0, k, r, cur, n_tiles, cap, L, P, G, src);
     CK(hipEventRecord(b, 0));
     CK(hipEventSynchronize(b));
     float ms = 0;
@@ -141,7 +188,7 @@ int main(int argc, char **argv) {
     if (rep) best = ms < best ? ms : best;
   }
   const double bytes = (what == 0 ? 12.0 : what == 1 ? 8.0 : what == 2 ? 4.0 : 20.0) * (double)n_tiles * tile;
-  const char *wn[5] = {"both", "keys", "rows", "read", "pref"};
+  const char *wn[6] = {"both", "keys", "rows", "read", "pref", "pr16"};
   printf("L %3u off %u %-4s P %4u G %u pad %5lu  %.3f ms  %.2f TB/s\n", L, off,
          wn[what], P, G, (unsigned long)pad, best,
          bytes / (best * 1e-3) / 1e12);
