@@ -244,12 +244,8 @@ int build_chain_device(const int64_t *d_keys, uint64_t n, hipStream_t s, uint64_
                        bid.as<uint32_t>(), idx.as<uint32_t>(), cnt.as<uint32_t>());
     BUILD_TRY(hipGetLastError(), "bucket ids");
   }
-  size_t tb = 0;
-  BUILD_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt.as<uint32_t>(), off.as<uint32_t>(), size + 1, s),
-            "scan size");
-  BUILD_TRY(scan_tmp.alloc(tb), "scan scratch");
-  BUILD_TRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp.p, tb, cnt.as<uint32_t>(), off.as<uint32_t>(), size + 1, s),
-            "offset scan");
+  BUILD_TRY(scan_tmp.alloc(scan_u64_temp_bytes(size + 1)), "scan scratch");
+  BUILD_TRY(scan_exclusive_u32(cnt.as<uint32_t>(), off.as<uint32_t>(), size + 1, nullptr, scan_tmp.p, s), "offset scan");
   if (n) {
     // stable LSD radix sort by bucket: equal buckets keep ascending tuple order (push_back order)
     const int end_bit = bits ? (int)bits : 1;

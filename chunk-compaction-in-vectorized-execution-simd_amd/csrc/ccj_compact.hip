@@ -13,7 +13,6 @@
 //   P-row u (chunk k = u/B)  -> output chunk k + #{pass-through s : E(t_s) <= k}, row u % B
 // Kernels: per-chunk segment sums -> exclusive scans (hipCUB) -> full-result E list -> one wave
 // per probe chunk copies its rows (DataChunk::Append's gather, base.cpp:15-27) -> chunk counts.
-#include <hipcub/hipcub.hpp>
 
 #include <cstdlib>
 
@@ -227,11 +226,7 @@ __global__ void chunk_counts(CompactParams p) {
   }
 }
 
-size_t scan_temp_bytes(uint64_t n) {
-  size_t bytes = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (uint64_t *)nullptr, (uint64_t *)nullptr, (int)n);
-  return (bytes + 255) & ~(size_t)255;
-}
+size_t scan_temp_bytes(uint64_t n) { return scan_u64_temp_bytes(n); }
 
 }  // namespace
 
@@ -266,8 +261,7 @@ hipError_t launch_compact(const ccj_compact_args &a, hipStream_t s) {
   p.max_full = max_bypass(a.n_chunks, a.cap, a.chunk, a.max_rounds, a.threshold);
   p.thr = a.threshold ? (a.threshold < a.chunk ? a.threshold : a.chunk) : a.chunk;
   p.fullE = (uint32_t *)take(p.max_full * 4);
-  size_t tb = scan_temp_bytes(a.n_chunks);
-  void *tmp = take(tb);
+  void *tmp = take(scan_temp_bytes(a.n_chunks));
   const unsigned g = (unsigned)((a.n_chunks + 255) / 256);
   CompactParams q = p;
   q.nonfull = nf_raw;
@@ -275,9 +269,9 @@ hipError_t launch_compact(const ccj_compact_args &a, hipStream_t s) {
   hipLaunchKernelGGL(seg_sums, dim3(g), dim3(256), 0, s, q);
   hipError_t e = hipGetLastError();
   if (e) return e;
-  e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, nf_raw, p.nonfull, (int)a.n_chunks, s);
+  e = scan_exclusive_u64(nf_raw, p.nonfull, a.n_chunks, nullptr, tmp, s);
   if (e) return e;
-  e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, f_raw, p.full, (int)a.n_chunks, s);
+  e = scan_exclusive_u64(f_raw, p.full, a.n_chunks, nullptr, tmp, s);
   if (e) return e;
   hipLaunchKernelGGL(seg_totals, dim3(1), dim3(1), 0, s, p, nf_raw + a.n_chunks - 1, f_raw + a.n_chunks - 1);
   hipLaunchKernelGGL(full_list, dim3(g), dim3(256), 0, s, p);

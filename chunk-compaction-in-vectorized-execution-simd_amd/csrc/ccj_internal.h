@@ -239,6 +239,14 @@ hipError_t launch_slot_partition(const int64_t *keys, uint64_t n, const SlotPlan
 // One-pass fixed-capacity form: segment (partition d, XCD group g) = positions [(d*8+g)*cap, +cap);
 // cursors[g*parts + d] = rows that went to it (may exceed cap: CCJ_FLAG_PART_OVERFLOW raised).
 uint64_t slot_seg_cap(uint64_t n, const SlotPlan &pl, uint32_t chunk);
+// Exclusive prefix sums of n values (ccj_scan.hip): out[i] = in[0] + ... + in[i-1] (in may be
+// out; u32 sums wrap as the values do); *total (optional, device) = the sum of all n.  tmp:
+// scan_u64_temp_bytes(n) bytes (either width).
+size_t scan_u64_temp_bytes(uint64_t n);
+hipError_t scan_exclusive_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *total, void *tmp,
+                              hipStream_t s);
+hipError_t scan_exclusive_u32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *total, void *tmp,
+                              hipStream_t s);
 // cursors[parts * 8 + g] = rows that tile group g (XCD) put in its overflow sub-area
 // [ovf_base + g * ovf_sub, + ovf_sub) (ovf_sub = 0: no overflow area); the last 64 positions of the
 // area [ovf_base, ovf_base + ovf_cap) are the pipelined form's sink.

@@ -11,7 +11,6 @@
 // Emission order is round-major, idx ascending within a round: exactly the reference's
 // result_vector order (L3).  Per-row state lives in VGPRs (key, slot/chain position, chain end);
 // active/match sets are bitmasks over the lane's R rows.
-#include <hipcub/hipcub.hpp>
 #include <cstdlib>
 #include <string>
 

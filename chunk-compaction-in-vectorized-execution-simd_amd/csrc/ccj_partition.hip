@@ -15,7 +15,6 @@
 // mbcnt), so its output is deterministic; the fixed-capacity owner split and the slot split rank
 // them with LDS atomics (grouping exact, order inside a tile's segment not), which is all the
 // probe needs — the second LSD pass still leaves every slot partition contiguous.
-#include <hipcub/hipcub.hpp>
 
 #include <cmath>
 
@@ -174,11 +173,7 @@ __global__ void part_totals(const uint64_t *cnt, const uint64_t *off, uint32_t p
   }
 }
 
-size_t scan_bytes(uint64_t n) {
-  size_t b = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (uint64_t *)nullptr, (uint64_t *)nullptr, (int)n);
-  return (b + 255) & ~(size_t)255;
-}
+size_t scan_bytes(uint64_t n) { return scan_u64_temp_bytes(n); }
 
 size_t pass_workspace(uint64_t n, uint32_t parts) {
   const uint64_t n_tiles = (n + kTile - 1) / kTile;
@@ -200,11 +195,10 @@ hipError_t split_pass(const int64_t *keys, const RowT *in_rows, uint64_t n, uint
   w += (m * 8 + 255) & ~255ull;
   uint64_t *off = (uint64_t *)w;
   w += (m * 8 + 255) & ~255ull;
-  size_t tb = scan_bytes(m);
   hipLaunchKernelGGL(part_count, dim3((unsigned)n_tiles), dim3(kTileThreads), 0, s, keys, n, parts, dg, n_tiles, cnt);
   hipError_t e = hipGetLastError();
   if (e) return e;
-  e = hipcub::DeviceScan::ExclusiveSum(w, tb, cnt, off, (int)m, s);
+  e = scan_exclusive_u64(cnt, off, m, nullptr, w, s);
   if (e) return e;
   hipLaunchKernelGGL((part_scatter<RowT, STABLE>), dim3((unsigned)n_tiles), dim3(kTileThreads), 0, s, keys, in_rows, n, parts,
                      dg, n_tiles, cnt, off, row_base, out_keys, out_rows, stride, status);

@@ -10,7 +10,6 @@
 //     join l+1 (rows packed back to back; chunk_base / out_base give each chunk its rows), or
 //   - compacted (CCJ_COMPACT_FULL): ccj_compact's closed form of NaiveCompactor::Compact + Flush.
 // The final level's output is the ResultCollector's table (main.cpp:125-128) in append order.
-#include <hipcub/hipcub.hpp>
 
 #include <memory>
 #include <vector>
@@ -175,11 +174,7 @@ __global__ __launch_bounds__(256) void dense_pack(PackParams p) {
     for (uint32_t j = lane; j < n; j += 64) p.dst[q][d0 + j] = p.src[q][s0 + j];
 }
 
-size_t scan_bytes(uint64_t n) {
-  size_t b = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (uint64_t *)nullptr, (uint64_t *)nullptr, (int)n);
-  return b;
-}
+size_t scan_bytes(uint64_t n) { return scan_u64_temp_bytes(n); }
 
 }  // namespace
 }  // namespace ccj
@@ -367,11 +362,9 @@ extern "C" int ccj_pipeline_run(ccj_pipeline *pl, const int64_t *const *d_cols, 
       hipLaunchKernelGGL(ccj::level_sizes, dim3(g), dim3(256), 0, s, p.out_count, p.out_rounds, p.out_round_counts, R,
                          in_chunks, L.rows.as<uint64_t>(), L.segs.as<uint64_t>());
       PL_TRY(hipGetLastError(), "level sizes");
-      PL_TRY(hipcub::DeviceScan::ExclusiveSum(L.scan_tmp.p, tb, L.rows.as<uint64_t>(), L.rows_pre.as<uint64_t>(),
-                                              (int)in_chunks, s),
+      PL_TRY(ccj::scan_exclusive_u64(L.rows.as<uint64_t>(), L.rows_pre.as<uint64_t>(), in_chunks, nullptr, L.scan_tmp.p, s),
              "scan");
-      PL_TRY(hipcub::DeviceScan::ExclusiveSum(L.scan_tmp.p, tb, L.segs.as<uint64_t>(), L.segs_pre.as<uint64_t>(),
-                                              (int)in_chunks, s),
+      PL_TRY(ccj::scan_exclusive_u64(L.segs.as<uint64_t>(), L.segs_pre.as<uint64_t>(), in_chunks, nullptr, L.scan_tmp.p, s),
              "scan");
       hipLaunchKernelGGL(ccj::level_totals, dim3(1), dim3(1), 0, s, L.rows.as<uint64_t>(), L.rows_pre.as<uint64_t>(),
                          L.segs.as<uint64_t>(), L.segs_pre.as<uint64_t>(), in_chunks, tot);
@@ -495,8 +488,7 @@ extern "C" int ccj_pipeline_run(ccj_pipeline *pl, const int64_t *const *d_cols, 
         hipLaunchKernelGGL(ccj::widen_counts, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in_counts, n,
                            pl->pack_w.as<uint64_t>());
         PL_TRY(hipGetLastError(), "widen");
-        PL_TRY(hipcub::DeviceScan::ExclusiveSum(pl->pack_tmp.p, tb, pl->pack_w.as<uint64_t>(),
-                                                pl->pack_pre.as<uint64_t>(), (int)n, s),
+        PL_TRY(ccj::scan_exclusive_u64(pl->pack_w.as<uint64_t>(), pl->pack_pre.as<uint64_t>(), n, nullptr, pl->pack_tmp.p, s),
                "scan");
         ccj::PackParams pp{};
         pp.n_cols = 2 * J;

@@ -49,8 +49,17 @@ def expected_compaction(ores, chunk, keys, extra, threshold=0):
                                                   (256, 20000, 3, 90000), (2048, 100000, 1, 100000),
                                                   (2048, 100000, 4, 1000000), (1000, 5000, 5, 5000)])
 def test_compact_matches_sequential_compactor(kind, chunk, n_build, cf, rng):
+    check_compaction(kind, chunk, n_build, cf, rng, 20 * chunk + chunk // 3)
+
+
+@pytest.mark.parametrize("kind", [ccj.LP, ccj.CHAIN])
+def test_compact_many_chunks(kind):
+    """4101 probe chunks: the per-chunk offset scans (csrc/ccj_scan.hip) span three 2048-chunk tiles."""
+    check_compaction(kind, 4, 512, 2, 600, 4101 * 4 - 1)
+
+
+def check_compaction(kind, chunk, n_build, cf, rng, n_probe):
     bkeys = ref_keys(n_build, cf)
-    n_probe = 20 * chunk + chunk // 3
     keys = O.uniform_keys(5 + chunk, 0, n_probe, rng)
     extra = [O.uniform_keys(77, 0, n_probe, 1 << 40), np.arange(n_probe, dtype=np.int64) * 3 + 1]
     table = ccj.Table.from_host(kind, bkeys)
