@@ -365,7 +365,9 @@ def bench_c3(args, dev, stream):
                                        "carried join-key column filled from the payload, key_cols)")
     phases["kernels"]["compaction_gather"] = "ccj_compact with the key column gathered by sel (DataChunk::Append's form)"
     if part_mode:
-        phases["kernels"]["match_tuples_and_advance_pointers"] = "probe_chain_win<3> (bucket records, 2-key windows)"
+        phases["kernels"]["match_tuples_and_advance_pointers"] = (
+            "probe_chain_filt (the partition's 2-bit bucket filter in LDS, 8-byte fingerprinted bucket records; "
+            "probe_chain_win<3> for the overflow area's chunks)")
         phases["kernels"]["gather_tuples"] = "— (the walk writes each match's payload)"
     if part_mode or args.path == "ordered":
         if int(out["status"].item()) & ccj.FLAG_PART_OVERFLOW:
@@ -445,8 +447,8 @@ def bench_c3(args, dev, stream):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": c3_traffic,
                      "traffic_GBps": c3_traffic / (probe_ms * 1e-3) / 1e9 if c3_traffic else None,
-                     "kernel": ("ccj_probe_partitioned (bucket-range split + probe_chain_win<3>)" if part_mode
-                                else "ccj_probe_ordered (bucket split with runs + chain_words<3> + unsplit_words + "
+                     "kernel": ("ccj_probe_partitioned (bucket-range split + probe_chain_filt)" if part_mode
+                                else "ccj_probe_ordered (bucket split with runs + chain_words_filt + unsplit_words + "
                                      "emit_ordered<CHAIN>)" if args.path == "ordered"
                                 else "probe_chunks<CHAIN,2>"),
                      "kernel_ms": probe_ms, "alg_bytes_per_tuple": alg, "chain_keys_per_tuple": n_bar,
