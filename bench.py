@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--group", type=int, default=None,
                     help="N > 1: received batches per local probe (each local probe sweeps the whole table); "
                          "default ccj_dist.GROUP")
+    ap.add_argument("--part-share", default="auto", choices=["auto", "on", "off"],
+                    help="N > 1 step: the local probe's split on 3/4 of the CUs (room for RCCL's kernels); "
+                         "auto = on when there are peers to exchange with (N > 1)")
     ap.add_argument("--cu-split", default=None,
                     help="N > 1: 'P,Q' = groups of 8 CUs (of 32) for the local probe's and the owner split's "
                          "streams (the rest stay free for RCCL); '0,0' = unmasked; default ccj_dist.CU_SPLIT")
@@ -935,11 +938,14 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
     chunk = args.chunk
     group = args.group or ccj_dist.GROUP
     t0 = time.perf_counter()
+    # the local split leaves CUs to the peers' RCCL kernels; with no peers (N = 1) there are none
+    part_share = world > 1 if args.part_share == "auto" else args.part_share == "on"
     if ops is None:
         with torch.cuda.stream(stream):
             cu_split = tuple(int(x) for x in args.cu_split.split(",")) if args.cu_split else None
             sp = ccj_dist.ShardedProbe(n_build_total, 1, n_probe, chunk, world, rank, batches=args.batches,
-                                       group=group, ops=ccj_dist.DeviceOps(cu_split=cu_split), keep_rows=True)
+                                       group=group, keep_rows=True,
+                                       ops=ccj_dist.DeviceOps(cu_split=cu_split, share=part_share))
             keys = ccj.gen_uniform_keys(n_probe, SEED, n_build_total, first_row=rank * n_probe, stream=stream)
     else:
         sp = ccj_dist.ShardedProbe(n_build_total, 1, n_probe, chunk, world, rank, batches=args.batches, ops=ops,
@@ -1042,6 +1048,8 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
             "local_probe_ms": probe_ms,
             "local_probe_alone_ms": probe_alone,
             "local_probe_alone_rows": sp.group * sp.slots,
+            "local_split_share": ("3/4 of the CUs (room for the peers' RCCL kernels)" if part_share
+                                  else "all CUs (no peers: N = 1)") if ops is None else None,
             "exchange": ("key-only all-to-all in timed steps (8 B per tuple + segment counts); each sender keeps its "
                          "rows per batch, so the held groups' matches are resolved to global rows after timing "
                          "(parity.timed_step_rows_resolved)"),

@@ -136,11 +136,14 @@ CU_SPLIT = (0, 0)
 class DeviceOps:
     """The HIP kernels (libccj.so) and torch.cuda streams/events one rank's step runs on."""
 
-    def __init__(self, cu_split=None):
+    def __init__(self, cu_split=None, share=True):
+        """share: the local probe's split on 3/4 of the CUs (CCJ_PART_SHARE), leaving the rest to
+        the exchange's RCCL kernels and the next owner splits."""
         import ccj
         self.ccj = ccj
         self.device = torch.device("cuda", torch.cuda.current_device())
         self.cu_split = tuple(CU_SPLIT if cu_split is None else cu_split)
+        self.share = share
 
     # streams and events
     def stream(self, role=None):
@@ -222,7 +225,7 @@ class DeviceOps:
         rows = int(self.table.max_dup) <= 1 and out["cap"] == chunk
         part["rows_mode"] = rows
         self.table.probe_partitioned(keys, chunk, counts=counts, out=out, part=part, stream=stream, retry=False,
-                                     share=True, rows=rows)
+                                     share=self.share, rows=rows)
 
     def group_rows(self, part, recv_rows, n_probe, seg_cap, slots, stream, src):
         """Global probe row of every position of a group's partitioned layout (gap positions hold
