@@ -70,9 +70,9 @@ def parse():
     ap.add_argument("--group", type=int, default=None,
                     help="N > 1: received batches per local probe (each local probe sweeps the whole table); "
                          "default ccj_dist.GROUP")
-    ap.add_argument("--part-share", default="auto", choices=["auto", "on", "off"],
-                    help="N > 1 step: the local probe's split on 3/4 of the CUs (room for RCCL's kernels); "
-                         "auto = on when there are peers to exchange with (N > 1)")
+    ap.add_argument("--part-share", default="on", choices=["on", "off"],
+                    help="N > 1 step: the local probe's split on 3/4 of the CUs (room for the exchange's RCCL "
+                         "kernels and the next owner splits)")
     ap.add_argument("--cu-split", default=None,
                     help="N > 1: 'P,Q' = groups of 8 CUs (of 32) for the local probe's and the owner split's "
                          "streams (the rest stay free for RCCL); '0,0' = unmasked; default ccj_dist.CU_SPLIT")
@@ -938,8 +938,10 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
     chunk = args.chunk
     group = args.group or ccj_dist.GROUP
     t0 = time.perf_counter()
-    # the local split leaves CUs to the peers' RCCL kernels; with no peers (N = 1) there are none
-    part_share = world > 1 if args.part_share == "auto" else args.part_share == "on"
+    # the local split leaves CUs to the exchange's RCCL kernels and the next owner splits (one-rank
+    # rehearsal, profiles/r5_ab_part_share.log: 19.95 ms per step with the share, 20.8 without —
+    # the owner splits' busy time 10.3 -> 13.5 ms — although the probe alone is 14.75 -> 12.9 ms)
+    part_share = args.part_share != "off"
     if ops is None:
         with torch.cuda.stream(stream):
             cu_split = tuple(int(x) for x in args.cu_split.split(",")) if args.cu_split else None
@@ -1006,6 +1008,9 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
     # on the device, the slowest rank's — its own time beside the busy time shared with the other
     # two streams (the local probe against the single-GPU probe of the same table)
     probe_alone = slowest(sp.probe_alone_ms()) if not exact_fallback else None
+    # the same group on the whole grid: the local probe's kernels without the CU share
+    probe_alone_full = (slowest(sp.probe_alone_ms(share=False)) if not exact_fallback and part_share and ops is None
+                        else None)
     # verification (untimed): global L1 / L2 against the exact membership answer
     m, l2 = sp.step(keys, rank * n_probe, verify=True)
     examined, received = 0, 0
@@ -1048,8 +1053,9 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
             "local_probe_ms": probe_ms,
             "local_probe_alone_ms": probe_alone,
             "local_probe_alone_rows": sp.group * sp.slots,
-            "local_split_share": ("3/4 of the CUs (room for the peers' RCCL kernels)" if part_share
-                                  else "all CUs (no peers: N = 1)") if ops is None else None,
+            "local_split_share": ("3/4 of the CUs (room for the exchange and the next owner splits)" if part_share
+                                  else "all CUs") if ops is None else None,
+            "local_probe_alone_full_grid_ms": probe_alone_full,
             "exchange": ("key-only all-to-all in timed steps (8 B per tuple + segment counts); each sender keeps its "
                          "rows per batch, so the held groups' matches are resolved to global rows after timing "
                          "(parity.timed_step_rows_resolved)"),

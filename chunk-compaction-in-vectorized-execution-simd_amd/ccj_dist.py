@@ -530,13 +530,22 @@ class ShardedProbe:
         o.synchronize()
         return m, l2, covered
 
-    def probe_alone_ms(self, reps: int = 3) -> float:
+    def probe_alone_ms(self, reps: int = 3, share=None) -> float:
         """After a run: the run's last group probed again with nothing else on the device (every
         stream drained first) — the local probe's own time, beside `local_probe_ms`, which is its
-        busy time while the partition and exchange streams share the GPU.  Min over `reps`."""
+        busy time while the partition and exchange streams share the GPU.  Min over `reps`.
+        share (DeviceOps only): override the ops' CU share for these probes (False: the whole grid,
+        the kernels' own speed without the room the step leaves to the exchange and owner splits)."""
         o = self.ops
         if self.last_exact:
             raise RuntimeError("the last run fell back to the exact-size protocol")
+        if share is not None and hasattr(o, "share"):
+            saved = o.share
+            o.share = share
+            try:
+                return self.probe_alone_ms(reps)
+            finally:
+                o.share = saved
         o.synchronize()
         g = self.n_groups - 1
         first, _ = self._group_range(g)
