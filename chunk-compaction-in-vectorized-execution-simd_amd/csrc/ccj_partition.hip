@@ -797,18 +797,18 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
 // owner_split_direct: the owner split (<= 64 destinations) without the workgroup's tile image.
 // Per tile:
 //   rank (one ballot per destination-index bit; the wave's running count of destination p in lane
-//   p) | [WIMG: the wave's 64 x PER keys written to its own LDS image in destination order] |
-//   barrier | one reservation atomic per destination for the workgroup's whole run, split into the
-//   waves' runs | barrier | stores
-// Without WIMG each lane stores its keys where they rank: a store instruction's 64 lanes write
-// one piece per destination (8 B x ~64 / parts).  With WIMG a wave stores its image in order:
-// whole runs of ~64 x PER / parts keys, as slot_split_pipe's image does for the workgroup — but
-// the image is the wave's own (written and read back by the same wave: no barrier guards it),
-// and two barriers per tile instead of four.  Same tiles, tile groups and segment layout as
+//   p) | the wave's 64 x PER keys written to its own LDS image in destination order | barrier |
+//   one reservation atomic per destination for the workgroup's whole run, split into the waves'
+//   runs | barrier | each wave stores its image in order
+// A wave's image holds whole runs of ~64 x PER / parts keys, as slot_split_pipe's image does for
+// the workgroup — but it is the wave's own (written and read back by the same wave: no barrier
+// guards it), and there are two barriers per tile instead of four.  (Round 5: lanes storing their
+// keys where they rank, with no image — 8-key pieces per store instruction — measured slower,
+// 0.182-0.197 against 0.165 ms per 2^25 keys.)  Same tiles, tile groups and segment layout as
 // slot_split_pipe's small form (partition_grouped_sub_cap sizes them); the order inside a
 // segment is free ("in any order").  Inactive lanes store to the per-XCD sink, so every store is
 // unconditional (as in the pipe).
-template <int PER, bool WIMG>
+template <int PER>
 __global__ __launch_bounds__(256) void owner_split_direct(const int64_t *keys, uint64_t n, uint32_t shift,
                                                           uint32_t parts, uint64_t n_tiles, uint32_t *cur,
                                                           uint64_t cap, int64_t *out_k, uint32_t *out_r,
@@ -816,9 +816,9 @@ __global__ __launch_bounds__(256) void owner_split_direct(const int64_t *keys, u
                                                           uint32_t *sink_r, uint32_t self_last, uint32_t ablate) {
   constexpr uint32_t T = 256, kTile = T * PER, kWaves = T / 64, kWaveKeys = 64 * PER;
   __shared__ uint32_t s_cnt[kWaves][64];   // wave w's keys of destination p in this tile
-  __shared__ uint32_t s_base[kWaves][64];  // their run's first position in segment (p, g) [WIMG: - image offset]
-  __shared__ int64_t s_wk[WIMG ? kWaves : 1][WIMG ? kWaveKeys : 1];   // [WIMG] wave images: key
-  __shared__ uint32_t s_wr[WIMG ? kWaves : 1][WIMG ? kWaveKeys : 1];  // and row in the wave's block | dest << 16
+  __shared__ uint32_t s_base[kWaves][64];  // their run's first position in segment (p, g)
+  __shared__ int64_t s_wk[kWaves][kWaveKeys];   // the waves' images: key
+  __shared__ uint32_t s_wr[kWaves][kWaveKeys];  // and row in the wave's block | destination << 16
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint32_t g = blockIdx.x & 7u, bpg = gridDim.x >> 3;
   const uint32_t mask = parts - 1;
@@ -860,21 +860,18 @@ __global__ __launch_bounds__(256) void owner_split_direct(const int64_t *keys, u
       dr[it] = lv ? d | (pre + below) << 8 : 0xFFFFFFFFu;
       cum += (uint32_t)__popcll(pm);
     }
+    // lane p: destination p's offset in the wave image (wloc); the image's length (wtot)
     const uint32_t mine_cnt = lane < parts ? cum : 0u;
-    uint32_t wloc = 0, wtot = 0;  // lane p: destination p's offset in the wave image; the image's length
-    if constexpr (WIMG) {
-      const uint32_t incl = wave_incl_scan(mine_cnt);
-      wloc = incl - mine_cnt;
-      wtot = (uint32_t)__shfl((int)incl, 63);
+    const uint32_t incl = wave_incl_scan(mine_cnt);
+    const uint32_t wloc = incl - mine_cnt, wtot = (uint32_t)__shfl((int)incl, 63);
 #pragma unroll
-      for (int it = 0; it < PER; ++it) {
-        // (the shuffle with every lane active: a lane reading an inactive lane's value gets 0)
-        const uint32_t d = dr[it] & 63u;
-        const uint32_t q = (uint32_t)__shfl((int)wloc, (int)d) + (dr[it] >> 8);
-        if (dr[it] != 0xFFFFFFFFu) {
-          s_wk[wave][q] = kc[it];
-          s_wr[wave][q] = ((uint32_t)it * 64u + lane) | d << 16;
-        }
+    for (int it = 0; it < PER; ++it) {
+      // (the shuffle with every lane active: a lane reading an inactive lane's value gets 0)
+      const uint32_t d = dr[it] & 63u;
+      const uint32_t q = (uint32_t)__shfl((int)wloc, (int)d) + (dr[it] >> 8);
+      if (dr[it] != 0xFFFFFFFFu) {
+        s_wk[wave][q] = kc[it];
+        s_wr[wave][q] = ((uint32_t)it * 64u + lane) | d << 16;
       }
     }
     if (lane < parts) s_cnt[wave][lane] = cum;
@@ -897,36 +894,22 @@ __global__ __launch_bounds__(256) void owner_split_direct(const int64_t *keys, u
       }
     }
     __syncthreads();
-    if constexpr (WIMG) {
-      // lane p < parts: its run's base minus its image offset, so entry q of destination d is
-      // stored at position base_d + q (mod 2^32)
-      const uint32_t adj = lane < parts ? s_base[wave][lane] - wloc : 0u;
+    // lane p < parts: its run's base minus its image offset, so entry q of destination d is stored
+    // at position base_d + q (mod 2^32)
+    const uint32_t adj = lane < parts ? s_base[wave][lane] - wloc : 0u;
 #pragma unroll
-      for (int it = 0; it < PER; ++it) {
-        const uint32_t q = (uint32_t)it * 64u + lane;
-        const uint32_t e = s_wr[wave][q];
-        const uint32_t d = (e >> 16) & 63u;
-        const uint32_t base = (uint32_t)__shfl((int)adj, (int)d);  // (every lane active)
-        const uint32_t pos = q < wtot ? base + q : 0xFFFFFFFFu;
-        const bool act = pos < cap;
-        dropped |= q < wtot && !act;
-        const uint64_t dest = ((uint64_t)d * 8 + g) * cap + pos;
-        if CCJ_ABLATED(ablate, 0x10u) continue;  // (timing: no stores)
-        *(act ? out_k + dest : sink_k) = s_wk[wave][q];
-        *(act ? out_r + dest : sink_r) = row_base + (uint32_t)(w0 + (e & 0xFFFFu));
-      }
-    } else {
-#pragma unroll
-      for (int it = 0; it < PER; ++it) {
-        const uint32_t d = dr[it] & 0xFFu;
-        const uint32_t pos = dr[it] == 0xFFFFFFFFu ? 0xFFFFFFFFu : s_base[wave][d & 63u] + (dr[it] >> 8);
-        const bool act = pos < cap;
-        dropped |= dr[it] != 0xFFFFFFFFu && !act;
-        const uint64_t dest = ((uint64_t)d * 8 + g) * cap + pos;
-        if CCJ_ABLATED(ablate, 0x10u) continue;  // (timing: no stores)
-        *(act ? out_k + dest : sink_k) = kc[it];
-        *(act ? out_r + dest : sink_r) = row_base + (uint32_t)(w0 + (uint32_t)it * 64u + lane);
-      }
+    for (int it = 0; it < PER; ++it) {
+      const uint32_t q = (uint32_t)it * 64u + lane;
+      const uint32_t e = s_wr[wave][q];
+      const uint32_t d = (e >> 16) & 63u;
+      const uint32_t base = (uint32_t)__shfl((int)adj, (int)d);  // (every lane active)
+      const uint32_t pos = q < wtot ? base + q : 0xFFFFFFFFu;
+      const bool act = pos < cap;
+      dropped |= q < wtot && !act;
+      const uint64_t dest = ((uint64_t)d * 8 + g) * cap + pos;
+      if CCJ_ABLATED(ablate, 0x10u) continue;  // (timing: no stores)
+      *(act ? out_k + dest : sink_k) = s_wk[wave][q];
+      *(act ? out_r + dest : sink_r) = row_base + (uint32_t)(w0 + (e & 0xFFFFu));
     }
   };
   load(tile, kA);
@@ -943,14 +926,15 @@ __global__ __launch_bounds__(256) void owner_split_direct(const int64_t *keys, u
 
 }  // namespace
 
-// The owner split in small workgroups (the multi-GPU step): slot_split_pipe with 256 threads and
-// 2048-key tiles (~26 KB of LDS) instead of one 1024-thread, 149 KB workgroup per CU.  The step
-// runs it beside the local probe: a workgroup that needs a whole CU's LDS waits until no walk
-// workgroup is left on some CU, i.e. until the walk's ~3·10^5 workgroups have drained (round-3
-// kernel trace of the one-rank rehearsal: no partition ran during any walk), while 26 KB
-// workgroups take the slots the walk's retiring workgroups free.  Persistent, 4 per CU of the
-// stream (a multiple of 8: one tile group per XCD).
-// owner_split_direct's persistent workgroups per CU (the wave-image form's occupancy: 87 VGPRs)
+// The owner split (the multi-GPU step) in small workgroups: 256 threads and 2048-key tiles (~26 KB
+// of LDS) instead of one 1024-thread, 149 KB workgroup per CU.  The step runs it beside the local
+// probe: a workgroup that needs a whole CU's LDS waits until no walk workgroup is left on some CU,
+// i.e. until the walk's ~3·10^5 workgroups have drained (round-3 kernel trace of the one-rank
+// rehearsal: no partition ran during any walk), while 26 KB workgroups take the slots the walk's
+// retiring workgroups free.  Persistent, kOwnerDirectPerCu per CU of the stream (a multiple of 8:
+// one tile group per XCD; 87 VGPRs: 5 waves per SIMD).  owner_split_direct since round 5 (DESIGN
+// §3.6: 0.177 -> 0.165 ms per 2^25 keys at 8 owners); the tuning build's CCJ_OWNER_DIRECT=0 runs
+// round 4's form, slot_split_pipe's ballot-ranked small instantiation, for A/B.
 constexpr uint32_t kOwnerDirectPerCu = 5;
 
 static hipError_t launch_owner_split_small(const int64_t *keys, uint64_t n, uint32_t parts, uint32_t shift,
@@ -962,50 +946,20 @@ static hipError_t launch_owner_split_small(const int64_t *keys, uint64_t n, uint
   hipError_t e = hipMemsetAsync(cur, 0, ((size_t)parts * 8 + 8) * 4, s);
   if (e || n == 0) return e;
   const uint64_t n_tiles = (n + kTile - 1) / kTile;
-  // per_cu = 0: one workgroup per tile (not persistent), so that workgroups dispatched late —
-  // behind another stream's kernel — do not each carry a fixed share of the tiles
-  const uint32_t per_cu = (uint32_t)ccj_tune_int("CCJ_OWNER_SMALL_PER_CU", 4);
-  uint64_t grid = per_cu ? (uint64_t)stream_cus(s) * per_cu / 8 * 8 : (n_tiles + 7) / 8 * 8;
-  grid = grid < 8 ? 8 : grid;
   int64_t *sink_k = (int64_t *)sink;
   uint32_t *sink_r = (uint32_t *)((char *)sink + kSplitSinkBytes / 16 * 8);
-  const int direct = ccj_tune_int("CCJ_OWNER_DIRECT", 2);  // (tuning build: 0 = slot_split_pipe's small form below,
-  if (direct) {                                            // 1 = owner_split_direct without wave images)
-    const uint32_t pc = (uint32_t)ccj_tune_int("CCJ_OWNER_DIRECT_PER_CU", kOwnerDirectPerCu);
-    uint64_t gr = pc ? (uint64_t)stream_cus(s) * pc / 8 * 8 : (n_tiles + 7) / 8 * 8;
-    gr = gr < 8 ? 8 : gr;
-    const uint32_t abl = (uint32_t)ccj_tune_int("CCJ_OWNER_ABLATE", 0);
-    if (direct == 1)
-      hipLaunchKernelGGL((owner_split_direct<kPer, false>), dim3((unsigned)gr), dim3(kT), 0, s, keys, n, shift, parts,
-                         n_tiles, cur, sub_cap, out_keys, out_rows, status, row_base, sink_k, sink_r, self_last, abl);
-    else
-      hipLaunchKernelGGL((owner_split_direct<kPer, true>), dim3((unsigned)gr), dim3(kT), 0, s, keys, n, shift, parts,
-                         n_tiles, cur, sub_cap, out_keys, out_rows, status, row_base, sink_k, sink_r, self_last, abl);
-    return hipGetLastError();
-  }
-#ifdef CCJ_TUNING
-  // (A/B forms: CCJ_OWNER_FORM=1 4096-key tiles of 16 keys per thread, 2 = 512-thread workgroups)
-  const int form = ccj_tune_int("CCJ_OWNER_FORM", 0);
-  if (form == 1 || form == 2) {
-    const uint32_t tk = form == 1 ? 256u * 16u : 512u * 8u;
-    const uint64_t nt = (n + tk - 1) / tk;
-    const uint32_t pc = (uint32_t)ccj_tune_int("CCJ_OWNER_SMALL_PER_CU", form == 1 ? 3 : 2);
-    uint64_t gr = pc ? (uint64_t)stream_cus(s) * pc / 8 * 8 : (nt + 7) / 8 * 8;
-    gr = gr < 8 ? 8 : gr;
-    if (form == 1)
-      hipLaunchKernelGGL((slot_split_pipe<false, 256, 64, 16, false>), dim3((unsigned)gr), dim3(256), 0, s, keys, n, shift,
-                         parts, nt, cur, sub_cap, (uint64_t)0, (uint64_t)0, out_keys, out_rows, status, nullptr, 0u,
-                         nullptr, nullptr, row_base, sink_k, sink_r, (uint32_t)ccj_tune_int("CCJ_OWNER_ABLATE", 0), self_last);
-    else
-      hipLaunchKernelGGL((slot_split_pipe<false, 512, 64, 8, false>), dim3((unsigned)gr), dim3(512), 0, s, keys, n, shift,
-                         parts, nt, cur, sub_cap, (uint64_t)0, (uint64_t)0, out_keys, out_rows, status, nullptr, 0u,
-                         nullptr, nullptr, row_base, sink_k, sink_r, (uint32_t)ccj_tune_int("CCJ_OWNER_ABLATE", 0), self_last);
-    return hipGetLastError();
-  }
-#endif
-  hipLaunchKernelGGL((slot_split_pipe<false, kT, 64, kPer, false>), dim3((unsigned)grid), dim3(kT), 0, s, keys, n, shift, parts,
-                     n_tiles, cur, sub_cap, (uint64_t)0, (uint64_t)0, out_keys, out_rows, status, nullptr, 0u, nullptr,
-                     nullptr, row_base, sink_k, sink_r, (uint32_t)ccj_tune_int("CCJ_OWNER_ABLATE", 0), self_last);
+  const uint32_t abl = (uint32_t)ccj_tune_int("CCJ_OWNER_ABLATE", 0);  // (timing ablations, tuning build)
+  // per_cu = 0: one workgroup per tile (not persistent)
+  const uint32_t per_cu = (uint32_t)ccj_tune_int("CCJ_OWNER_PER_CU", kOwnerDirectPerCu);
+  uint64_t grid = per_cu ? (uint64_t)stream_cus(s) * per_cu / 8 * 8 : (n_tiles + 7) / 8 * 8;
+  grid = grid < 8 ? 8 : grid;
+  if (ccj_tune_int("CCJ_OWNER_DIRECT", 1))
+    hipLaunchKernelGGL(owner_split_direct<kPer>, dim3((unsigned)grid), dim3(kT), 0, s, keys, n, shift, parts, n_tiles,
+                       cur, sub_cap, out_keys, out_rows, status, row_base, sink_k, sink_r, self_last, abl);
+  else
+    hipLaunchKernelGGL((slot_split_pipe<false, kT, 64, kPer, false>), dim3((unsigned)grid), dim3(kT), 0, s, keys, n,
+                       shift, parts, n_tiles, cur, sub_cap, (uint64_t)0, (uint64_t)0, out_keys, out_rows, status,
+                       nullptr, 0u, nullptr, nullptr, row_base, sink_k, sink_r, abl, self_last);
   return hipGetLastError();
 }
 

@@ -1,8 +1,10 @@
 """Owner split alone (ON THE GPU BOX): ms per 2^25-key batch of ccj_partition_by_owner_grouped for
 1 and 8 owners, on an unmasked stream (the default half-CU grid) and on CU-masked streams of 64 / 128
 CUs (one workgroup per CU), nothing else running.  python3 tools/owner_split_bench.py [--lib tuning|PATH]
-[--unmasked].  Tuning-build knobs: CCJ_OWNER_FORM (1: 4096-key tiles, 2: 512-thread workgroups),
-CCJ_OWNER_SMALL_PER_CU, CCJ_OWNER_ABLATE (0x10 no stores, 0x20 no key reads, 0x2000 no hash)."""
+[--unmasked].  Tuning-build knobs: CCJ_OWNER_DIRECT=0 (round 4's slot_split_pipe form),
+CCJ_OWNER_PER_CU (persistent workgroups per CU; 0: one per tile), CCJ_OWNER_ABLATE (0x10 no stores,
+0x20 no key reads, 0x2000 no hash, 0x100000 no reservation atomics, 0x200000 no image scatter;
+the last two in the round-4 form)."""
 import os
 import sys
 
