@@ -2453,6 +2453,36 @@ __device__ __forceinline__ void walk_emit_pos(const ProbeParams &p, SM &sm, uint
   emit_wg_stores<2, kWave * NW>(p, sm, obase, tot, true);
   if (threadIdx.x == 0) sm.total = tot;
 }
+// The ordered walks' output (MM): every row's round word at its position, coalesced (16-bit words,
+// 8 per lane as one 16-byte store, for full 512-row waves of chunks that are multiples of 8).
+template <uint32_t kWaveRows, typename SM>
+__device__ __forceinline__ void walk_words_out(const ProbeParams &p, SM &sm, uint64_t base, uint32_t w0,
+                                               uint32_t wend, uint32_t lane) {
+  if (p.w16 && kWaveRows == 8 * kWave && w0 + kWaveRows <= p.chunk && (p.chunk & 7u) == 0u) {
+    const uint32_t i0 = w0 + 8 * lane;
+    uint32_t h[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      h[t] = (uint32_t)round_word16(sm.hc[i0 + 2 * t]) | (uint32_t)round_word16(sm.hc[i0 + 2 * t + 1]) << 16;
+    const u32x4 v = {h[0], h[1], h[2], h[3]};
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>((uint16_t *)p.out_w + base + i0));
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < (int)(kWaveRows / kWave); ++j) {
+    const uint32_t i = w0 + (uint32_t)j * kWave + lane;
+    if (i < wend) {
+      if (p.w16) __builtin_nontemporal_store(round_word16(sm.hc[i]), (uint16_t *)p.out_w + base + i);
+      else __builtin_nontemporal_store(sm.hc[i], p.out_w + base + i);
+    }
+  }
+}
+// A row's round word (MM): the rounds it matched in (bits < kMmRounds) and its run's length r, or
+// kMmLong | r for runs longer than kMmRounds
+__device__ __forceinline__ uint32_t mm_word(uint32_t mask, uint32_t r) {
+  return r <= kMmRounds ? (mask & ((1u << kMmRounds) - 1u)) | r << kMmRounds : kMmLong | r;
+}
+
 template <int NB, bool MM = false, bool POS = false, int NW = 4>
 __global__ __launch_bounds__(kWave * NW) void probe_walk1(ProbeParams p) {
   constexpr uint32_t kWaveRows = kMaxChunk / NW;  // rows per wave
@@ -2547,7 +2577,7 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk1(ProbeParams p) {
       if (ee || (!MM && p.first_match && hits)) {
         const uint32_t r = r0[b] + f;  // occupied slots walked = the reference's rounds (run end)
         lane_rounds = r > lane_rounds ? r : lane_rounds;
-        if (MM) cnt[b] = r <= kMmRounds ? (cnt[b] & ((1u << kMmRounds) - 1u)) | r << kMmRounds : kMmLong | r;
+        if (MM) cnt[b] = mm_word(cnt[b], r);
         if (CCJ_ABLATED(p.ablate, 0x200u)) cnt[b] = 1;  // (timing only: the emit path of the real data)
         // POS (tables of <= 2^31 slots): bit 31 = matched, the low bits its slot
         sm.hc[row[b]] = POS ? (cnt[b] ? mpos[b] | 0x80000000u : 0u) : cnt[b];
@@ -2588,24 +2618,7 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk1(ProbeParams p) {
   }
   __syncthreads();
   if (MM) {  // the rows' round words, coalesced at their positions (probe_walk's MM tail)
-    if (p.w16 && kWaveRows == 8 * kWave && w0 + kWaveRows <= p.chunk && (p.chunk & 7u) == 0u) {
-      const uint32_t i0 = w0 + 8 * lane;
-      uint32_t h[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-        h[t] = (uint32_t)round_word16(sm.hc[i0 + 2 * t]) | (uint32_t)round_word16(sm.hc[i0 + 2 * t + 1]) << 16;
-      const u32x4 v = {h[0], h[1], h[2], h[3]};
-      __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>((uint16_t *)p.out_w + base + i0));
-      return;
-    }
-#pragma unroll
-    for (int j = 0; j < (int)(kWaveRows / kWave); ++j) {
-      const uint32_t i = w0 + (uint32_t)j * kWave + lane;
-      if (i < wend) {
-        if (p.w16) __builtin_nontemporal_store(round_word16(sm.hc[i]), (uint16_t *)p.out_w + base + i);
-        else __builtin_nontemporal_store(sm.hc[i], p.out_w + base + i);
-      }
-    }
+    walk_words_out<kWaveRows>(p, sm, base, w0, wend, lane);
     return;
   }
   if (POS) {  // CCJ_PART_ROWS with match positions (C5): sel and payload are the split's
@@ -2651,6 +2664,9 @@ __device__ __forceinline__ void stage_keys_aux(const int64_t *keys, uint32_t phy
     if (w0 + (uint32_t)(j >> 1) * 128u + 2u * lane + (uint32_t)(j & 1) >= wend) k[j] = 0;
 }
 #endif
+// (Round 5: an MM form for the ordered route — every row walking its whole run, phase A's
+// continuing rows keeping their first window's hits — measured slower than probe_walk1<MM>: 7.75
+// against 7.49 ms, same box; the ~16 % of rows that go on are walked lane by lane in phase B.)
 template <bool POS, int NB = 1>
 __global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
   constexpr int NW = 4;
@@ -2747,6 +2763,7 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
   auto result = [&](uint32_t cur, uint32_t hits) {
     return POS ? (hits ? (cur + (uint32_t)__builtin_ctz(hits)) | 0x80000000u : 0u) : (hits ? 1u : 0u);
   };
+
   // phase A: every row's first window (NB = 2: step j + 1's windows are fetched while step j's
   // are checked)
   uint32_t cont = 0;
