@@ -617,7 +617,7 @@ struct PartLayout {
   uint32_t parts;
   uint64_t seg_cap, positions;
   uint64_t ovf_base, ovf_cap;  // overflow area after the segments (runs that do not fit: key skew)
-  uint64_t ovf_sub;            // its 8 per-XCD sub-areas (a multiple of chunk each; the last 64 positions: the sink)
+  uint64_t ovf_sub;            // its kOvfSubs sub-areas (kOvfPerGroup per XCD; a multiple of chunk each; the last 64 positions: the sink)
 };
 PartLayout part_layout(const ccj_table *t, uint64_t n_rows, uint32_t chunk) {
   PartLayout L{};
@@ -638,8 +638,8 @@ PartLayout part_layout(const ccj_table *t, uint64_t n_rows, uint32_t chunk) {
     const uint64_t tile = ccj::slot_split_tile_keys(L.parts, runs), n_tiles = (n_rows + tile - 1) / tile;
     g_rows = std::max<uint64_t>(g_rows, std::min<uint64_t>(n_rows, (n_tiles + 7) / 8 * tile));
   }
-  L.ovf_sub = (g_rows / 16 + chunk + chunk - 1) / chunk * chunk;
-  L.ovf_cap = (8 * L.ovf_sub + 64 + chunk - 1) / chunk * chunk;
+  L.ovf_sub = (g_rows / 16 / ccj::kOvfPerGroup + chunk + chunk - 1) / chunk * chunk;
+  L.ovf_cap = (ccj::kOvfSubs * L.ovf_sub + 64 + chunk - 1) / chunk * chunk;
   L.positions = L.ovf_base + L.ovf_cap;
   return L;
 }
@@ -655,7 +655,7 @@ size_t ccj_probe_partitioned_workspace_size(const ccj_table *t, uint64_t n_rows,
   if (!t) return 0;
   const PartLayout L = part_layout(t, n_rows, chunk);
   // partitioned keys (positions) + the fixed split's cursors, or the exact split's pass scratch
-  const size_t fixed = align256(((uint64_t)L.parts * 8 + 8) * 4);
+  const size_t fixed = align256(ccj::split_cursor_count(L.parts) * 4);
   const size_t exact = ccj::slot_partition_workspace(n_rows, L.pl);
   // + the rank walk's per-block hit masks, hit counts and partition counters
 #ifdef CCJ_RANK_WALK
@@ -779,7 +779,7 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
                     a->chunk % ccj::kRankChunkMultiple == 0 && ((flags & CCJ_PART_RANK) || ccj_tune_int("CCJ_RANK", 0));
   if (rank) {
     const ccj::RankIndex ix{t->d_occ, t->d_pre, t->d_ckeys, t->rank_wbits};
-    const size_t fixed = align256(((uint64_t)L.parts * 8 + 8) * 4);
+    const size_t fixed = align256(ccj::split_cursor_count(L.parts) * 4);
     const size_t exact_ws = ccj::slot_partition_workspace(a->n_rows, L.pl);
     void *rws = (char *)rest + align256(fixed > exact_ws ? fixed : exact_ws);
     HIP_TRY(ccj::launch_probe_rank(p, ix, rws, s), "rank walk launch");
@@ -864,7 +864,7 @@ OrderedLayout ordered_layout(const ccj_table *t, uint64_t n_rows, uint32_t chunk
   O.row_map = take(O.L.positions * 4);
   O.w_pos = take(O.L.positions * 4);
   O.w_row = take(n_rows * 4);
-  O.cursors = take(((uint64_t)O.L.parts * 8 + 8) * 4);
+  O.cursors = take(ccj::split_cursor_count(O.L.parts) * 4);
   O.runs = take(O.n_tiles * O.L.parts * 8);
   O.ovf_runs = take(O.n_tiles * O.L.parts * 4);
   O.total = off;

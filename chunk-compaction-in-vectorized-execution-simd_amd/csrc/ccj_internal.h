@@ -117,7 +117,7 @@ struct ProbeParams {
   uint64_t seg_cap;
   // overflow area [ovf_base, n_rows): runs that did not fit their segment (key skew), in 8
   // sub-areas of ovf_sub positions (a multiple of chunk), one per tile group g (XCD) with fill
-  // level seg_count[seg_parts * 8 + g].  0 = no overflow area.
+  // level seg_count[ovf_cursor_index(seg_parts, k)] (k < kOvfSubs).  0 = no overflow area.
   uint64_t ovf_base;
   uint64_t ovf_sub;
   uint64_t swz_chunks;   // chunks dealt to XCDs in contiguous ranges (0: all); the overflow area's
@@ -227,6 +227,20 @@ size_t partition_workspace(uint64_t n, uint32_t parts);
 // split's runs grow with fewer partitions, the walk's L2 reuse shrinks with bigger windows.
 constexpr uint32_t kWindowBits = 19;
 constexpr uint32_t kSplitPartBits = 10;  // at most 1024 partitions (larger tables: larger windows)
+// The fixed-capacity split's overflow area (key skew): kOvfSubs sub-areas, kOvfPerGroup per tile
+// group (XCD), each with its own cursor on its own 128-byte line, so that the Zipf-hot partitions'
+// overflow reservations of one XCD's workgroups do not all queue on one address (a partition's
+// run takes sub-area (partition + workgroup) mod kOvfPerGroup of its group: balanced fills).
+constexpr uint32_t kOvfPerGroup = 4;
+constexpr uint32_t kOvfSubs = 8 * kOvfPerGroup;
+constexpr uint32_t kOvfCurStride = 32;  // u32 cursors between two overflow cursors
+// cursors of the fixed-capacity split: parts * 8 segment cursors, then the overflow cursors
+__host__ __device__ constexpr uint64_t split_cursor_count(uint32_t parts) {
+  return (uint64_t)parts * 8 + (uint64_t)kOvfSubs * kOvfCurStride;
+}
+__host__ __device__ constexpr uint64_t ovf_cursor_index(uint32_t parts, uint32_t sub) {
+  return (uint64_t)parts * 8 + (uint64_t)sub * kOvfCurStride;
+}
 struct SlotPlan {
   uint32_t window_bits, lo_bits, hi_bits;
 };
@@ -247,9 +261,10 @@ hipError_t scan_exclusive_u64(const uint64_t *in, uint64_t *out, uint64_t n, uin
                               hipStream_t s);
 hipError_t scan_exclusive_u32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *total, void *tmp,
                               hipStream_t s);
-// cursors[parts * 8 + g] = rows that tile group g (XCD) put in its overflow sub-area
-// [ovf_base + g * ovf_sub, + ovf_sub) (ovf_sub = 0: no overflow area); the last 64 positions of the
-// area [ovf_base, ovf_base + ovf_cap) are the pipelined form's sink.
+// cursors[ovf_cursor_index(parts, k)] = rows put in overflow sub-area k < kOvfSubs (tile group
+// k / kOvfPerGroup) = [ovf_base + k * ovf_sub, + ovf_sub) (ovf_sub = 0: no overflow area); the last
+// 64 positions of the area [ovf_base, ovf_base + ovf_cap) are the pipelined form's sink; cursors
+// holds split_cursor_count(parts) entries.
 // counts: live rows per input chunk.  runs (optional; the ordered probe): per (tile, partition)
 // {segment position of the run, segment length | overflow-area length << 16}; ovf_runs: the
 // overflow-area position where that length is non-zero.  Tiles are slot_split_tile_keys(parts, runs) keys.

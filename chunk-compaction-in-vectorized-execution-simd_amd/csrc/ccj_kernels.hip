@@ -540,10 +540,10 @@ __device__ __forceinline__ uint32_t flat_phys(const ProbeParams &p, uint64_t bas
   const uint64_t rem = p.n_rows - base;
   uint32_t phys = rem < p.chunk ? (uint32_t)rem : p.chunk;
   if (p.seg_count && p.ovf_base && base >= p.ovf_base) {  // the overflow area's chunks
-    const uint64_t sub = p.ovf_sub ? (base - p.ovf_base) / p.ovf_sub : 8u;  // its group's sub-area
-    uint64_t live = sub < 8u ? p.seg_count[(uint64_t)p.seg_parts * 8 + sub] : 0u;
+    const uint64_t sub = p.ovf_sub ? (base - p.ovf_base) / p.ovf_sub : kOvfSubs;  // its sub-area
+    uint64_t live = sub < kOvfSubs ? p.seg_count[ovf_cursor_index(p.seg_parts, (uint32_t)sub)] : 0u;
     live = live < p.ovf_sub ? live : p.ovf_sub;
-    const uint64_t off = sub < 8u ? base - p.ovf_base - sub * p.ovf_sub : 0u;
+    const uint64_t off = sub < kOvfSubs ? base - p.ovf_base - sub * p.ovf_sub : 0u;
     phys = live > off ? (live - off < phys ? (uint32_t)(live - off) : phys) : 0u;
   } else if (p.counts && !p.seg_count) {  // identity layout of a column with per-chunk live counts
     const uint32_t cn = p.counts[base / p.chunk];

@@ -242,7 +242,7 @@ __global__ void grouped_counts(const uint32_t *cur, uint32_t parts, uint64_t *ou
 }  // namespace
 
 // cursors, then the pipelined split's sink
-static size_t grouped_cursor_bytes(uint32_t parts) { return (((size_t)parts * 8 + 8) * 4 + 255) & ~(size_t)255; }
+static size_t grouped_cursor_bytes(uint32_t parts) { return (split_cursor_count(parts) * 4 + 255) & ~(size_t)255; }
 size_t partition_grouped_workspace(uint32_t parts) { return grouped_cursor_bytes(parts) + kSplitSinkBytes; }
 
 uint64_t partition_grouped_sub_cap(uint64_t n, uint32_t parts, uint32_t chunk) {
@@ -467,12 +467,15 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
       s_dst[tid] = seg * cap + r;
       s_lim[tid] = lim;
       uint32_t olim = 0, r2 = 0;
-      if (lim < h) {  // the rest of the run goes to the shared overflow area (key skew)
+      if (lim < h) {  // the rest of the run goes to one of group g's overflow sub-areas (key skew)
         const uint32_t extra = h - lim;
-        r2 = atomicAdd(&cur[(uint64_t)parts * 8 + g], extra);  // group g's overflow sub-area
-        olim = r2 >= ovf_cap ? 0u : (uint32_t)(ovf_cap - r2 < extra ? ovf_cap - r2 : extra);
+        if (ovf_cap) {
+          const uint32_t sub = g * kOvfPerGroup + (tid + (blockIdx.x >> 3)) % kOvfPerGroup;
+          r2 = atomicAdd(&cur[ovf_cursor_index(parts, sub)], extra);
+          olim = r2 >= ovf_cap ? 0u : (uint32_t)(ovf_cap - r2 < extra ? ovf_cap - r2 : extra);
+          r2 += sub * (uint32_t)ovf_cap;
+        }
         dropped |= olim < extra;
-        r2 += g * (uint32_t)ovf_cap;
       }
       s_ovf[tid] = r2;
       s_olim[tid] = olim;
@@ -649,12 +652,15 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
     const uint64_t seg = (uint64_t)ptid * 8 + g;
     const uint32_t lim = r >= cap ? 0u : (uint32_t)(cap - r < h ? cap - r : h);
     uint32_t olim = 0, r2 = 0;
-    if (lim < h) {  // the rest of the run goes to group g's overflow sub-area (key skew)
+    if (lim < h) {  // the rest of the run goes to one of group g's overflow sub-areas (key skew)
       const uint32_t extra = h - lim;
-      r2 = atomicAdd(&cur[(uint64_t)parts * 8 + g], extra);
-      olim = r2 >= ovf_cap ? 0u : (uint32_t)(ovf_cap - r2 < extra ? ovf_cap - r2 : extra);
+      if (ovf_cap) {
+        const uint32_t sub = g * kOvfPerGroup + (ptid + (blockIdx.x >> 3)) % kOvfPerGroup;
+        r2 = atomicAdd(&cur[ovf_cursor_index(parts, sub)], extra);
+        olim = r2 >= ovf_cap ? 0u : (uint32_t)(ovf_cap - r2 < extra ? ovf_cap - r2 : extra);
+        r2 += sub * (uint32_t)ovf_cap;  // (the sub-area's place in the overflow area)
+      }
       dropped |= olim < extra;
-      r2 += g * (uint32_t)ovf_cap;  // (the sub-area's place in the overflow area)
     }
     const uint64_t dadj = seg * cap + r - loc;  // mod 2^64: + the image index gives the dest
     s_rec[ptid] = make_uint4((uint32_t)dadj, (uint32_t)(dadj >> 32), loc + lim, loc + lim + olim);
@@ -943,7 +949,7 @@ static hipError_t launch_owner_split_small(const int64_t *keys, uint64_t n, uint
                                           uint32_t self_last) {
   constexpr int kT = 256, kPer = 8;
   constexpr uint32_t kTile = (uint32_t)kT * kPer;
-  hipError_t e = hipMemsetAsync(cur, 0, ((size_t)parts * 8 + 8) * 4, s);
+  hipError_t e = hipMemsetAsync(cur, 0, split_cursor_count(parts) * 4, s);
   if (e || n == 0) return e;
   const uint64_t n_tiles = (n + kTile - 1) / kTile;
   int64_t *sink_k = (int64_t *)sink;
@@ -994,7 +1000,7 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
   // counts: a tile's chunks (tile / chunk + 2 at most) fit one count per thread
   if (counts && (chunk == 0 || slot_split_tile_keys(parts, runs != nullptr) / chunk + 2 > (uint32_t)kSplitThreads))
     return hipErrorInvalidValue;
-  hipError_t e = hipMemsetAsync(cursors, 0, ((size_t)parts * 8 + 8) * 4, s);
+  hipError_t e = hipMemsetAsync(cursors, 0, split_cursor_count(parts) * 4, s);
   if (e || n == 0) return e;
   // One persistent 1024-thread workgroup per CU (<= 149 KB of LDS), a multiple of 8 (one tile group
   // per XCD).  Two 512-thread workgroups per CU on 6144-key tiles (same run length at 512
@@ -1019,7 +1025,7 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
   // the pipelined form needs a sink for its inactive lanes' stores: 64 positions of the overflow
   // area (8 per XCD group), or the caller's kSplitSinkBytes
   if ((ovf_cap >= 128 || sink) && ccj_tune_int("CCJ_SPLIT_PIPE", 1)) {
-    // (the 8 overflow sub-areas of ovf_sub positions end at least 64 positions before the area's end)
+    // (the kOvfSubs overflow sub-areas of ovf_sub positions end at least 64 positions before the area's end)
     const uint64_t oc = ovf_sub;
     int64_t *sink_k = sink ? (int64_t *)sink : out_keys + ovf_base + ovf_cap - 64;
     uint32_t *sink_r = sink ? (uint32_t *)((char *)sink + kSplitSinkBytes / 16 * 8) : out_rows + ovf_base + ovf_cap - 64;

@@ -1,5 +1,8 @@
-# round 5 call AD: C2 at 2 / 4 / 8 MiB table windows (1024 / 512 / 256 partitions; tuning build,
-# CCJ_WINDOW_BITS), interleaved 2x; then the ordered tests on the product (walk_words_out refactor)
+# round 5 call AE: the split's overflow area in 4 sub-areas per XCD group, each with its own cursor
+# line — partitioned / C3 / ordered / multi-GPU / known-answer tests, then C3 and C2 against the
+# one-cursor-per-group build (interleaved)
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && \
-bash tools/gpu_ab.sh r5wb c2 2 tuning:CCJ_WINDOW_BITS=18 tuning tuning:CCJ_WINDOW_BITS=20 > gpurun_out/r5wb_ab.log 2>&1 && \
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_probe_gpu.py -k "ordered" > gpurun_out/r5ad_tests.log 2>&1
+timeout -k 10 1000 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_probe_gpu.py tests/test_c3_gpu.py \
+  tests/test_dist_gpu.py tests/test_known_answers_gpu.py tests/test_c5_gpu.py > gpurun_out/r5ae_tests.log 2>&1 && \
+bash tools/gpu_ab.sh r5ovc c3 3 product tools/abx/libccj_s1.so > gpurun_out/r5ovc_ab.log 2>&1 && \
+bash tools/gpu_ab.sh r5ovc2 c2 2 product tools/abx/libccj_s1.so > gpurun_out/r5ovc2_ab.log 2>&1
