@@ -234,12 +234,21 @@ constexpr uint32_t kSplitPartBits = 10;  // at most 1024 partitions (larger tabl
 constexpr uint32_t kOvfPerGroup = 4;
 constexpr uint32_t kOvfSubs = 8 * kOvfPerGroup;
 constexpr uint32_t kOvfCurStride = 32;  // u32 cursors between two overflow cursors
+// Segment cursors: segment (partition d, tile group g) counts at seg_cursor_index(parts, g, d),
+// group-major, kSegCurStride u32 apart.
+#ifndef CCJ_SEG_CUR_STRIDE
+#define CCJ_SEG_CUR_STRIDE 1
+#endif
+constexpr uint32_t kSegCurStride = CCJ_SEG_CUR_STRIDE;
+__host__ __device__ constexpr uint64_t seg_cursor_index(uint32_t parts, uint32_t g, uint32_t d) {
+  return ((uint64_t)g * parts + d) * kSegCurStride;
+}
 // cursors of the fixed-capacity split: parts * 8 segment cursors, then the overflow cursors
 __host__ __device__ constexpr uint64_t split_cursor_count(uint32_t parts) {
-  return (uint64_t)parts * 8 + (uint64_t)kOvfSubs * kOvfCurStride;
+  return (uint64_t)parts * 8 * kSegCurStride + (uint64_t)kOvfSubs * kOvfCurStride;
 }
 __host__ __device__ constexpr uint64_t ovf_cursor_index(uint32_t parts, uint32_t sub) {
-  return (uint64_t)parts * 8 + (uint64_t)sub * kOvfCurStride;
+  return (uint64_t)parts * 8 * kSegCurStride + (uint64_t)sub * kOvfCurStride;
 }
 struct SlotPlan {
   uint32_t window_bits, lo_bits, hi_bits;

@@ -551,7 +551,7 @@ __device__ __forceinline__ uint32_t flat_phys(const ProbeParams &p, uint64_t bas
   } else if (p.seg_count) {
     const uint64_t seg = base / p.seg_cap;
     const uint64_t off = base - seg * p.seg_cap;
-    uint64_t live = p.seg_count[(seg & 7) * p.seg_parts + (seg >> 3)];
+    uint64_t live = p.seg_count[seg_cursor_index(p.seg_parts, (uint32_t)(seg & 7), (uint32_t)(seg >> 3))];
     live = live < p.seg_cap ? live : p.seg_cap;
     phys = live > off ? (live - off < phys ? (uint32_t)(live - off) : phys) : 0u;
   }
@@ -1501,11 +1501,11 @@ __device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *
     }
     __syncthreads();
     // a unit (wave-uniform, scalar): chunk c, rows [u0, uend) of it (uend <= u0: nothing live), and
-    // (match walk) the workgroup's chunk ordinal m.  Segment d * 8 + g holds seg_count[g * P + d] rows.
+    // (match walk) the workgroup's chunk ordinal m.  Segment d * 8 + g holds seg_count[seg_cursor_index(P, g, d)] rows.
     auto unit_at = [&](uint32_t g, uint32_t ci, uint32_t kk, uint64_t &c, uint32_t &u0, uint32_t &uend) {
       c = (uint64_t)(d * 8u + g) * spc + ci;
       u0 = kk * kFiltUnit;
-      const uint64_t fill = p.seg_count[g < 8u ? g * P + d : 0u];
+      const uint64_t fill = p.seg_count[g < 8u ? seg_cursor_index(P, g, d) : 0u];
       uint64_t live = g < 8u ? fill : 0u;
       live = live < p.seg_cap ? live : p.seg_cap;
       const uint64_t off = (uint64_t)ci * chunk;

@@ -237,7 +237,7 @@ namespace {
 // cursors[g * parts + d] (u32, group-major) -> counts[d * 8 + g] (u64, destination-major)
 __global__ void grouped_counts(const uint32_t *cur, uint32_t parts, uint64_t *out) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < parts * 8) out[i] = cur[(i % 8) * parts + i / 8];
+  if (i < parts * 8) out[i] = cur[seg_cursor_index(parts, i % 8, i / 8)];
 }
 }  // namespace
 
@@ -442,7 +442,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
     const uint32_t h = tid < parts ? s_hist[tid] : 0u;
     uint32_t incl = wave_incl_scan(h);
     if (lane == 63) s_wsum[wave] = incl;
-    uint32_t r = h && !CCJ_ABLATED(ablate, 0x40u) ? atomicAdd(&cur[(uint64_t)g * parts + tid], h) : 0u;  // flies during the image build
+    uint32_t r = h && !CCJ_ABLATED(ablate, 0x40u) ? atomicAdd(&cur[seg_cursor_index(parts, g, tid)], h) : 0u;  // flies during the image build
     // (timing only, 0xC0: no reservation atomics, runs at their expected offsets: 9.5 ms, not less —
     // the atomics keep one segment's runs written close together in time, so its L2 merges them)
     if CCJ_ABLATED(ablate, 0x80u) r = (uint32_t)(((tile - g * n_tiles / 8) * (kTileKeys / parts)) % cap);
@@ -737,7 +737,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
       if CCJ_ABLATED(ablate, 0x100000u)  // (timing: no reservation atomics — each tile an expected-size run)
         r = (uint32_t)(((t - g * n_tiles / 8) * (kTileKeys / parts)) % (cap > 2 * kTileKeys ? cap - 2 * kTileKeys : 1));
       else
-        r = atomicAdd(&cur[(uint64_t)g * parts + opaque_v32(tid)], h);  // awaited after the stores are issued
+        r = atomicAdd(&cur[seg_cursor_index(parts, g, opaque_v32(tid))], h);  // awaited after the stores are issued
     }
 #ifdef CCJ_SPLIT_STORES16
     stores16();
@@ -891,7 +891,7 @@ __global__ __launch_bounds__(256) void owner_split_direct(const int64_t *keys, u
         if CCJ_ABLATED(ablate, 0x100000u)  // (timing: no reservation atomics)
           r = (uint32_t)(((t - g * n_tiles / 8) * (kTile / parts)) % (cap > 2 * kTile ? cap - 2 * kTile : 1));
         else
-          r = atomicAdd(&cur[(uint64_t)g * parts + tid], tot);
+          r = atomicAdd(&cur[seg_cursor_index(parts, g, tid)], tot);
       }
 #pragma unroll
       for (uint32_t w = 0; w < kWaves; ++w) {

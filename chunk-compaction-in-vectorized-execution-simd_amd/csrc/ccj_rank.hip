@@ -59,7 +59,7 @@ struct RankParams {
   const int64_t *ckeys;
   uint32_t mask, wbits, parts;
   uint64_t seg_cap;
-  const uint32_t *seg_count;  // the split's cursors: seg_count[g * parts + d]
+  const uint32_t *seg_count;  // the split's cursors: seg_count[seg_cursor_index(parts, g, d)]
   uint32_t *ctr;              // per-partition block counters (zeroed before the launch)
   uint64_t *hit_words;        // 8 per 512-row block of the segment area
   uint32_t *blk_hits;         // per block
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(kWave * kRankWaves) void probe_rank(RankParams q) {
       uint32_t acc = 0;
       sm.nblk[0] = 0;
       for (uint32_t g = 0; g < 8; ++g) {
-        uint64_t live = q.seg_count[(uint64_t)g * q.parts + d];
+        uint64_t live = q.seg_count[seg_cursor_index(q.parts, g, d)];
         live = live < q.seg_cap ? live : q.seg_cap;
         sm.live[g] = (uint32_t)live;
         acc += (uint32_t)((live + kRankBlock - 1) / kRankBlock);
@@ -344,7 +344,7 @@ __global__ __launch_bounds__(256) void rank_finish(FinishParams f) {
   const uint64_t base = c * f.chunk;
   const uint64_t seg = base / f.seg_cap;
   const uint64_t soff = base - seg * f.seg_cap;
-  uint64_t live = f.seg_count[(seg & 7) * f.parts + (seg >> 3)];
+  uint64_t live = f.seg_count[seg_cursor_index(f.parts, (uint32_t)(seg & 7), (uint32_t)(seg >> 3))];
   live = live < f.seg_cap ? live : f.seg_cap;
   const uint32_t phys = live > soff ? (live - soff < f.chunk ? (uint32_t)(live - soff) : f.chunk) : 0u;
   const uint64_t blk0 = base / kRankBlock;
