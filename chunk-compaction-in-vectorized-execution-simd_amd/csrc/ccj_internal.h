@@ -235,20 +235,20 @@ constexpr uint32_t kOvfPerGroup = 4;
 constexpr uint32_t kOvfSubs = 8 * kOvfPerGroup;
 constexpr uint32_t kOvfCurStride = 32;  // u32 cursors between two overflow cursors
 // Segment cursors: segment (partition d, tile group g) counts at seg_cursor_index(parts, g, d),
-// group-major, kSegCurStride u32 apart.
-#ifndef CCJ_SEG_CUR_STRIDE
-#define CCJ_SEG_CUR_STRIDE 1
-#endif
-constexpr uint32_t kSegCurStride = CCJ_SEG_CUR_STRIDE;
+// group-major, each tile group's cursors starting on their own 128-byte line: with few partitions
+// (the owner split: one per rank) the XCDs' reservations then never share a line — at one owner
+// 0.218 -> 0.145 ms per 2^25 keys (profiles/r5_ab_cursor_lines.log).  Packed within a group: one
+// cursor per line instead measured slower for the slot split's 512 partitions (4.85 -> 5.13 ms at
+// C2: a wave's 64 reservations then touch 64 lines instead of 2).
 __host__ __device__ constexpr uint64_t seg_cursor_index(uint32_t parts, uint32_t g, uint32_t d) {
-  return ((uint64_t)g * parts + d) * kSegCurStride;
+  return (uint64_t)g * (parts > 32u ? parts : 32u) + d;
 }
-// cursors of the fixed-capacity split: parts * 8 segment cursors, then the overflow cursors
+// cursors of the fixed-capacity split: 8 groups of segment cursors, then the overflow cursors
 __host__ __device__ constexpr uint64_t split_cursor_count(uint32_t parts) {
-  return (uint64_t)parts * 8 * kSegCurStride + (uint64_t)kOvfSubs * kOvfCurStride;
+  return 8ull * (parts > 32u ? parts : 32u) + (uint64_t)kOvfSubs * kOvfCurStride;
 }
 __host__ __device__ constexpr uint64_t ovf_cursor_index(uint32_t parts, uint32_t sub) {
-  return (uint64_t)parts * 8 * kSegCurStride + (uint64_t)sub * kOvfCurStride;
+  return 8ull * (parts > 32u ? parts : 32u) + (uint64_t)sub * kOvfCurStride;
 }
 struct SlotPlan {
   uint32_t window_bits, lo_bits, hi_bits;

@@ -1,8 +1,10 @@
-# round 5 call AE: the split's overflow area in 4 sub-areas per XCD group, each with its own cursor
-# line — partitioned / C3 / ordered / multi-GPU / known-answer tests, then C3 and C2 against the
-# one-cursor-per-group build (interleaved)
+# round 5 call AG: each tile group's segment cursors on their own 128-byte line (few partitions) —
+# multi-GPU / partitioned tests, the owner split alone against the packed build, the rehearsal line
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && \
-timeout -k 10 1000 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_probe_gpu.py tests/test_c3_gpu.py \
-  tests/test_dist_gpu.py tests/test_known_answers_gpu.py tests/test_c5_gpu.py > gpurun_out/r5ae_tests.log 2>&1 && \
-bash tools/gpu_ab.sh r5ovc c3 3 product tools/abx/libccj_s1.so > gpurun_out/r5ovc_ab.log 2>&1 && \
-bash tools/gpu_ab.sh r5ovc2 c2 2 product tools/abx/libccj_s1.so > gpurun_out/r5ovc2_ab.log 2>&1
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_dist_gpu.py tests/test_probe_gpu.py -k "dist or partition or sharded or owner or grouped or segment" > gpurun_out/r5ag_tests.log 2>&1 && \
+o=gpurun_out/r5ag_owner.log && : > $o && \
+for i in 1 2; do
+  echo "== product $i" >> $o && timeout -k 10 120 python3 -u tools/owner_split_bench.py --unmasked >> $o 2>&1 && \
+  echo "== packed $i" >> $o && timeout -k 10 120 python3 -u tools/owner_split_bench.py --lib tools/abx/libccj_packed.so --unmasked >> $o 2>&1 || exit 1
+done && \
+timeout -k 10 300 python -u bench.py --gpus 1 --sharded --group 32 --no-cpu > gpurun_out/r5ag_sharded_g32.log 2> gpurun_out/r5ag_sharded_g32.err
