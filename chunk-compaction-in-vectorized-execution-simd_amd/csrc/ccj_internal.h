@@ -240,15 +240,18 @@ constexpr uint32_t kOvfCurStride = 32;  // u32 cursors between two overflow curs
 // 0.218 -> 0.145 ms per 2^25 keys (profiles/r5_ab_cursor_lines.log).  Packed within a group: one
 // cursor per line instead measured slower for the slot split's 512 partitions (4.85 -> 5.13 ms at
 // C2: a wave's 64 reservations then touch 64 lines instead of 2).
+// (Spreading the cursors 4 or 8 u32 apart inside a group measured slower too at C2: split 4.85
+// -> 5.01 / 4.93 ms, profiles/r5_ab_cursor_spread.log.)
+__host__ __device__ constexpr uint64_t seg_group_stride(uint32_t parts) { return parts > 32u ? parts : 32u; }
 __host__ __device__ constexpr uint64_t seg_cursor_index(uint32_t parts, uint32_t g, uint32_t d) {
-  return (uint64_t)g * (parts > 32u ? parts : 32u) + d;
+  return (uint64_t)g * seg_group_stride(parts) + d;
 }
 // cursors of the fixed-capacity split: 8 groups of segment cursors, then the overflow cursors
 __host__ __device__ constexpr uint64_t split_cursor_count(uint32_t parts) {
-  return 8ull * (parts > 32u ? parts : 32u) + (uint64_t)kOvfSubs * kOvfCurStride;
+  return 8ull * seg_group_stride(parts) + (uint64_t)kOvfSubs * kOvfCurStride;
 }
 __host__ __device__ constexpr uint64_t ovf_cursor_index(uint32_t parts, uint32_t sub) {
-  return 8ull * (parts > 32u ? parts : 32u) + (uint64_t)sub * kOvfCurStride;
+  return 8ull * seg_group_stride(parts) + (uint64_t)sub * kOvfCurStride;
 }
 struct SlotPlan {
   uint32_t window_bits, lo_bits, hi_bits;
