@@ -638,7 +638,10 @@ PartLayout part_layout(const ccj_table *t, uint64_t n_rows, uint32_t chunk) {
     const uint64_t tile = ccj::slot_split_tile_keys(L.parts, runs), n_tiles = (n_rows + tile - 1) / tile;
     g_rows = std::max<uint64_t>(g_rows, std::min<uint64_t>(n_rows, (n_tiles + 7) / 8 * tile));
   }
-  L.ovf_sub = (g_rows / 16 / ccj::kOvfPerGroup + chunk + chunk - 1) / chunk * chunk;
+  // (a group's 1/16 + one chunk, shared by its kOvfPerGroup sub-areas, each a whole number of
+  // chunks: the area stays the size it had with one sub-area per group, which ccj_pipeline_run's
+  // route gate — positions <= 4/3 of the rows — depends on)
+  L.ovf_sub = ((g_rows / 16 + chunk) / ccj::kOvfPerGroup + chunk - 1) / chunk * chunk;
   L.ovf_cap = (ccj::kOvfSubs * L.ovf_sub + 64 + chunk - 1) / chunk * chunk;
   L.positions = L.ovf_base + L.ovf_cap;
   return L;
