@@ -617,7 +617,8 @@ struct PartLayout {
   uint32_t parts;
   uint64_t seg_cap, positions;
   uint64_t ovf_base, ovf_cap;  // overflow area after the segments (runs that do not fit: key skew)
-  uint64_t ovf_sub;            // its kOvfSubs sub-areas (kOvfPerGroup per XCD; a multiple of chunk each; the last 64 positions: the sink)
+  uint64_t ovf_sub;            // its 8 x ovf_per_group sub-areas (a multiple of chunk each; the last 64 positions: the sink)
+  uint32_t ovf_per_group;      // overflow sub-areas (cursors) per XCD group: 1 or kOvfPerGroup
 };
 PartLayout part_layout(const ccj_table *t, uint64_t n_rows, uint32_t chunk) {
   PartLayout L{};
@@ -638,11 +639,14 @@ PartLayout part_layout(const ccj_table *t, uint64_t n_rows, uint32_t chunk) {
     const uint64_t tile = ccj::slot_split_tile_keys(L.parts, runs), n_tiles = (n_rows + tile - 1) / tile;
     g_rows = std::max<uint64_t>(g_rows, std::min<uint64_t>(n_rows, (n_tiles + 7) / 8 * tile));
   }
-  // (a group's 1/16 + one chunk, shared by its kOvfPerGroup sub-areas, each a whole number of
-  // chunks: the area stays the size it had with one sub-area per group, which ccj_pipeline_run's
-  // route gate — positions <= 4/3 of the rows — depends on)
-  L.ovf_sub = ((g_rows / 16 + chunk) / ccj::kOvfPerGroup + chunk - 1) / chunk * chunk;
-  L.ovf_cap = (ccj::kOvfSubs * L.ovf_sub + 64 + chunk - 1) / chunk * chunk;
+  // A group's room, 1/16 of its rows + one chunk, split over kOvfPerGroup sub-areas (cursors) only
+  // where each can hold a whole tile (one partition's run of a skewed tile may need it); the area
+  // keeps its size either way (ccj_pipeline_run's route gate, positions <= 4/3 of the rows,
+  // depends on it).
+  const uint64_t room = g_rows / 16 + chunk;
+  L.ovf_per_group = room / ccj::kOvfPerGroup >= ccj::slot_split_tile_keys(L.parts) ? ccj::kOvfPerGroup : 1u;
+  L.ovf_sub = (room / L.ovf_per_group + chunk - 1) / chunk * chunk;
+  L.ovf_cap = (8 * L.ovf_per_group * L.ovf_sub + 64 + chunk - 1) / chunk * chunk;
   L.positions = L.ovf_base + L.ovf_cap;
   return L;
 }
@@ -730,7 +734,7 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
     const uint32_t share = (flags & CCJ_PART_SHARE) ? std::max<uint32_t>(8u, ccj::stream_cus(s) * 3 / 4 / 8 * 8) : 0u;
     HIP_TRY(ccj::launch_slot_split_fixed(a->keys, a->n_rows, L.pl, L.seg_cap, L.ovf_base, L.ovf_cap, L.ovf_sub, cursors, pkeys,
                                          out_row_map, a->status, s, a->counts, a->chunk, nullptr, nullptr, 0, ~0u,
-                                         share),
+                                         share, nullptr, ~0u, L.ovf_per_group),
             "slot split");
     p.seg_count = cursors;
     p.counts = nullptr;  // the input's chunk counts were applied by the split
@@ -909,7 +913,8 @@ int ccj_probe_ordered(const ccj_table *t, const ccj_probe_args *a, void *ws, siz
   phase_mark(s, 0);
   // 1. one-pass slot split of the live rows, recording where every tile's runs went
   HIP_TRY(ccj::launch_slot_split_fixed(a->keys, a->n_rows, L.pl, L.seg_cap, L.ovf_base, L.ovf_cap, L.ovf_sub, cursors, pkeys,
-                                       row_map, a->status, s, a->counts, a->chunk, runs, ovf_runs),
+                                       row_map, a->status, s, a->counts, a->chunk, runs, ovf_runs, 0, ~0u, 0, nullptr,
+                                       ~0u, L.ovf_per_group),
           "slot split");
   phase_mark(s, 1);
   // 2. walk with the table window L2-resident: every row's Next-round word at its position

@@ -227,10 +227,11 @@ size_t partition_workspace(uint64_t n, uint32_t parts);
 // split's runs grow with fewer partitions, the walk's L2 reuse shrinks with bigger windows.
 constexpr uint32_t kWindowBits = 19;
 constexpr uint32_t kSplitPartBits = 10;  // at most 1024 partitions (larger tables: larger windows)
-// The fixed-capacity split's overflow area (key skew): kOvfSubs sub-areas, kOvfPerGroup per tile
-// group (XCD), each with its own cursor on its own 128-byte line, so that the Zipf-hot partitions'
+// The fixed-capacity split's overflow area (key skew): up to kOvfPerGroup sub-areas per tile group
+// (XCD), each with its own cursor on its own 128-byte line, so that the Zipf-hot partitions'
 // overflow reservations of one XCD's workgroups do not all queue on one address (a partition's
-// run takes sub-area (partition + workgroup) mod kOvfPerGroup of its group: balanced fills).
+// run takes sub-area (partition + workgroup) mod the group's count: balanced fills).  The layout
+// (part_layout) splits a group's room only when each part can still hold a whole tile's run.
 constexpr uint32_t kOvfPerGroup = 4;
 constexpr uint32_t kOvfSubs = 8 * kOvfPerGroup;
 constexpr uint32_t kOvfCurStride = 32;  // u32 cursors between two overflow cursors
@@ -286,7 +287,8 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
                                    uint32_t *out_rows, uint32_t *status, hipStream_t s,
                                    const uint32_t *counts = nullptr, uint32_t chunk = 0, uint2 *runs = nullptr,
                                    uint32_t *ovf_runs = nullptr, uint32_t row_base = 0, uint32_t shift = ~0u,
-                                   uint32_t wgs = 0, void *sink = nullptr, uint32_t self_last = ~0u);
+                                   uint32_t wgs = 0, void *sink = nullptr, uint32_t self_last = ~0u,
+                                   uint32_t ovf_per_group = 1);
 // Bytes of device memory the split writes its inactive lanes' stores to when the overflow area
 // cannot hold them (launch_slot_split_fixed's `sink`; 8 XCD groups x 8 positions of key + row).
 constexpr size_t kSplitSinkBytes = 8 * 8 * 16;

@@ -369,7 +369,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
                                                                  int64_t *out_k, uint32_t *out_r, uint32_t *status,
                                                                  uint32_t ablate, const uint32_t *counts, uint32_t chunk,
                                                                  uint2 *runs, uint32_t *ovf_runs, uint32_t row_base,
-                                                                 uint32_t self_last) {
+                                                                 uint32_t self_last, uint32_t ovf_pg) {
   constexpr uint32_t kTileKeys = (uint32_t)THREADS * PER;
   static_assert(MAXP <= THREADS, "one partition per thread in the scan");
   __shared__ int64_t s_k[kTileKeys];
@@ -470,7 +470,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_fixed(const int64_t *keys,
       if (lim < h) {  // the rest of the run goes to one of group g's overflow sub-areas (key skew)
         const uint32_t extra = h - lim;
         if (ovf_cap) {
-          const uint32_t sub = g * kOvfPerGroup + (tid + (blockIdx.x >> 3)) % kOvfPerGroup;
+          const uint32_t sub = g * ovf_pg + (tid + (blockIdx.x >> 3)) % ovf_pg;
           r2 = atomicAdd(&cur[ovf_cursor_index(parts, sub)], extra);
           olim = r2 >= ovf_cap ? 0u : (uint32_t)(ovf_cap - r2 < extra ? ovf_cap - r2 : extra);
           r2 += sub * (uint32_t)ovf_cap;
@@ -537,7 +537,8 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
                                                                 int64_t *out_k, uint32_t *out_r, uint32_t *status,
                                                                 const uint32_t *counts, uint32_t chunk, uint2 *runs,
                                                                 uint32_t *ovf_runs, uint32_t row_base, int64_t *sink_k,
-                                                                uint32_t *sink_r, uint32_t ablate, uint32_t self_last) {
+                                                                uint32_t *sink_r, uint32_t ablate, uint32_t self_last,
+                                                                uint32_t ovf_pg) {
   constexpr uint32_t kTileKeys = (uint32_t)THREADS * PER;
   static_assert(MAXP <= THREADS, "one partition per thread in the scan");
   __shared__ int64_t s_k[kTileKeys];
@@ -655,7 +656,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
     if (lim < h) {  // the rest of the run goes to one of group g's overflow sub-areas (key skew)
       const uint32_t extra = h - lim;
       if (ovf_cap) {
-        const uint32_t sub = g * kOvfPerGroup + (ptid + (blockIdx.x >> 3)) % kOvfPerGroup;
+        const uint32_t sub = g * ovf_pg + (ptid + (blockIdx.x >> 3)) % ovf_pg;
         r2 = atomicAdd(&cur[ovf_cursor_index(parts, sub)], extra);
         olim = r2 >= ovf_cap ? 0u : (uint32_t)(ovf_cap - r2 < extra ? ovf_cap - r2 : extra);
         r2 += sub * (uint32_t)ovf_cap;  // (the sub-area's place in the overflow area)
@@ -965,7 +966,7 @@ static hipError_t launch_owner_split_small(const int64_t *keys, uint64_t n, uint
   else
     hipLaunchKernelGGL((slot_split_pipe<false, kT, 64, kPer, false>), dim3((unsigned)grid), dim3(kT), 0, s, keys, n,
                        shift, parts, n_tiles, cur, sub_cap, (uint64_t)0, (uint64_t)0, out_keys, out_rows, status,
-                       nullptr, 0u, nullptr, nullptr, row_base, sink_k, sink_r, abl, self_last);
+                       nullptr, 0u, nullptr, nullptr, row_base, sink_k, sink_r, abl, self_last, 1u);
   return hipGetLastError();
 }
 
@@ -995,7 +996,8 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
                                    uint64_t ovf_base, uint64_t ovf_cap, uint64_t ovf_sub, uint32_t *cursors, int64_t *out_keys,
                                    uint32_t *out_rows, uint32_t *status, hipStream_t s, const uint32_t *counts,
                                    uint32_t chunk, uint2 *runs, uint32_t *ovf_runs, uint32_t row_base,
-                                   uint32_t shift, uint32_t wgs, void *sink, uint32_t self_last) {
+                                   uint32_t shift, uint32_t wgs, void *sink, uint32_t self_last, uint32_t ovf_per_group) {
+  const uint32_t ovf_pg = ovf_per_group ? ovf_per_group : 1u;
   const uint32_t parts = 1u << (pl.lo_bits + pl.hi_bits);
   // counts: a tile's chunks (tile / chunk + 2 at most) fit one count per thread
   if (counts && (chunk == 0 || slot_split_tile_keys(parts, runs != nullptr) / chunk + 2 > (uint32_t)kSplitThreads))
@@ -1034,11 +1036,11 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
     if (runs)                                                                                                       \
       hipLaunchKernelGGL((slot_split_pipe<C, kSplitThreads, MAXP, P, true>), dim3(grid), dim3(kSplitThreads), 0, s,  \
                          keys, n, shift, parts, n_tiles, cursors, cap, ovf_base, oc, out_keys, out_rows, status,     \
-                         counts, chunk, runs, ovf_runs, row_base, sink_k, sink_r, ablate, self_last);                \
+                         counts, chunk, runs, ovf_runs, row_base, sink_k, sink_r, ablate, self_last, ovf_pg);                \
     else                                                                                                            \
       hipLaunchKernelGGL((slot_split_pipe<C, kSplitThreads, MAXP, P, false>), dim3(grid), dim3(kSplitThreads), 0, s, \
                          keys, n, shift, parts, n_tiles, cursors, cap, ovf_base, oc, out_keys, out_rows, status,     \
-                         counts, chunk, runs, ovf_runs, row_base, sink_k, sink_r, ablate, self_last);                \
+                         counts, chunk, runs, ovf_runs, row_base, sink_k, sink_r, ablate, self_last, ovf_pg);                \
   } while (0)
 #ifdef CCJ_TUNING
     // (tuning build: two workgroups per CU instead of one lock-stepped 1024-thread workgroup —
@@ -1052,20 +1054,20 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
         if (counts)
           hipLaunchKernelGGL((slot_split_pipe<true, 512, kSplitParts / 2, 10, false>), dim3(g2), dim3(512), 0, s, keys, n,
                              shift, parts, nt, cursors, cap, ovf_base, oc, out_keys, out_rows, status, counts, chunk,
-                             runs, ovf_runs, row_base, sink_k, sink_r, ablate, self_last);
+                             runs, ovf_runs, row_base, sink_k, sink_r, ablate, self_last, ovf_pg);
         else
           hipLaunchKernelGGL((slot_split_pipe<false, 512, kSplitParts / 2, 10, false>), dim3(g2), dim3(512), 0, s, keys,
                              n, shift, parts, nt, cursors, cap, ovf_base, oc, out_keys, out_rows, status, counts, chunk,
-                             runs, ovf_runs, row_base, sink_k, sink_r, ablate, self_last);
+                             runs, ovf_runs, row_base, sink_k, sink_r, ablate, self_last, ovf_pg);
       } else {
         if (counts)
           hipLaunchKernelGGL((slot_split_pipe<true, 1024, kSplitParts / 2, 4, false>), dim3(g2), dim3(1024), 0, s, keys,
                              n, shift, parts, nt, cursors, cap, ovf_base, oc, out_keys, out_rows, status, counts, chunk,
-                             runs, ovf_runs, row_base, sink_k, sink_r, ablate, self_last);
+                             runs, ovf_runs, row_base, sink_k, sink_r, ablate, self_last, ovf_pg);
         else
           hipLaunchKernelGGL((slot_split_pipe<false, 1024, kSplitParts / 2, 4, false>), dim3(g2), dim3(1024), 0, s, keys,
                              n, shift, parts, nt, cursors, cap, ovf_base, oc, out_keys, out_rows, status, counts, chunk,
-                             runs, ovf_runs, row_base, sink_k, sink_r, ablate, self_last);
+                             runs, ovf_runs, row_base, sink_k, sink_r, ablate, self_last, ovf_pg);
       }
       return hipGetLastError();
     }
@@ -1089,7 +1091,7 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
 #define CCJ_SPLIT_LAUNCH(C, MAXP, P)                                                                              \
   hipLaunchKernelGGL((slot_split_fixed<C, kSplitThreads, MAXP, P>), dim3(grid), dim3(kSplitThreads), 0, s, keys, n,      \
                      shift, parts, n_tiles, cursors, cap, ovf_base, ovf_sub, out_keys, out_rows, status, ablate,         \
-                     counts, chunk, runs, ovf_runs, row_base, self_last)
+                     counts, chunk, runs, ovf_runs, row_base, self_last, ovf_pg)
   if (parts > kSplitParts / 2) {  // 1024 partitions: 10 keys per thread
     if (counts) CCJ_SPLIT_LAUNCH(true, kSplitParts, 10);
     else CCJ_SPLIT_LAUNCH(false, kSplitParts, 10);
