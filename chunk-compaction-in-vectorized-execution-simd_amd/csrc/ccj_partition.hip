@@ -17,6 +17,7 @@
 // probe needs — the second LSD pass still leaves every slot partition contiguous.
 
 #include <cmath>
+#include <type_traits>
 
 #include "ccj_internal.h"
 #include "ccj_tuning.h"
@@ -350,7 +351,19 @@ SlotPlan slot_plan(uint64_t table_size, int kind) {
 // (only heavy key skew does this; cap leaves 8 standard deviations of room).
 namespace {
 constexpr int kSplitThreads = 1024;
-constexpr int kSplitPer = 11;  // CCJ_SPLIT_PER sweep at C2: 8-13 keys -> 6.35 6.12 5.98 5.90 6.34 7.11 ms
+#ifndef CCJ_SPLIT_PER_KEYS
+#define CCJ_SPLIT_PER_KEYS 11
+#endif
+#ifndef CCJ_SPLIT_NARROW
+#define CCJ_SPLIT_NARROW 0
+#endif
+// keys per thread of the pipelined split (CCJ_SPLIT_PER sweep at C2, round 1's fixed form: 8-13 keys
+// -> 6.35 6.12 5.98 5.90 6.34 7.11 ms); the fixed form (slot_split_fixed) keeps 11
+constexpr int kSplitPer = CCJ_SPLIT_PER_KEYS;
+constexpr int kSplitPerFixed = 11;
+// CCJ_SPLIT_NARROW: the pipelined split's image holds each entry's tile row in 16 bits and the
+// stores re-derive its partition from the key (one hash more per key, 2 bytes less LDS per key)
+constexpr bool kSplitNarrow = CCJ_SPLIT_NARROW != 0;
 constexpr uint32_t kSplitParts = 1u << kSplitPartBits;
 static_assert(kSplitParts <= (uint32_t)kSplitThreads, "one partition per thread in the scan");
 
@@ -541,8 +554,10 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
                                                                 uint32_t ovf_pg) {
   constexpr uint32_t kTileKeys = (uint32_t)THREADS * PER;
   static_assert(MAXP <= THREADS, "one partition per thread in the scan");
+  static_assert(kTileKeys <= 65536u, "tile rows in 16 bits");
+  using ImgT = typename std::conditional<kSplitNarrow, uint16_t, uint32_t>::type;
   __shared__ int64_t s_k[kTileKeys];
-  __shared__ uint32_t s_i[kTileKeys];  // tile-local row | partition << 16
+  __shared__ ImgT s_i[kTileKeys];  // tile-local row | partition << 16 (narrow: the row only)
   __shared__ uint32_t s_hist[MAXP], s_loc[MAXP];
   // per partition, for the stores: {dest - image index (u64), segment end, overflow end} (image
   // indices) and the overflow area's dest - image index: two LDS reads per stored key
@@ -556,6 +571,16 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
   const uint64_t tend = (g + 1) * n_tiles / 8;
   uint64_t tile = g * n_tiles / 8 + (blockIdx.x >> 3);
   if (tile >= tend) return;
+  // a key's destination partition (the owner split's small forms — launch_owner_split_small only:
+  // shift = 64 - log2(parts) or mask 0 — need only the hash's high word: one 32-bit product fewer)
+  auto dest_of = [&](int64_t k) -> uint32_t {
+    constexpr bool kOwnerHi = MAXP <= 64 && THREADS <= 512;
+    const uint32_t d0 = CCJ_ABLATED(ablate, 0x2000u) ? (uint32_t)((uint64_t)k >> shift) & mask  // (timing: no hash)
+                        : kOwnerHi ? (murmurhash64_hi((uint64_t)k) >> ((shift - 32u) & 31u)) & mask
+                                   : (uint32_t)(murmurhash64((uint64_t)k) >> shift) & mask;
+    if constexpr (MAXP <= 64) return self_slot(d0, self_last, parts);  // (the owner split: own rank's segment last)
+    else return d0;
+  };
   sink_k += g * 8;  // inactive lanes store here (8 positions per XCD group)
   sink_r += g * 8;
   if (tid < MAXP) s_hist[tid] = 0;
@@ -581,7 +606,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
     {
       const uint32_t q = (uint32_t)it * THREADS + tid;
       const int64_t k = s_k[q];
-      const uint32_t si = s_i[q], d = (si >> 16) & (uint32_t)(MAXP - 1);
+      const uint32_t si = s_i[q], d = kSplitNarrow ? dest_of(k) : (si >> 16) & (uint32_t)(MAXP - 1);
       const uint4 rc = s_rec[d];
       const uint64_t oadj = s_oadj[d];
       const bool act = have_prev && q < p_tl && q < rc.w;
@@ -694,18 +719,12 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
     uint32_t dr[PER];  // partition | rank in it << 10 (one register per key: no spills at 11 keys)
 #pragma unroll
     for (int it = 0; it < PER; ++it) {
-      // (the owner split's small forms — launch_owner_split_small only: shift = 64 - log2(parts) or
-      // mask 0 — need only the hash's high word: one 32-bit product fewer)
-      constexpr bool kOwnerHi = MAXP <= 64 && THREADS <= 512;
-      const uint32_t d0 = CCJ_ABLATED(ablate, 0x2000u) ? (uint32_t)((uint64_t)kc[it] >> shift) & mask  // (timing: no hash)
-                          : kOwnerHi ? (murmurhash64_hi((uint64_t)kc[it]) >> ((shift - 32u) & 31u)) & mask
-                                     : (uint32_t)(murmurhash64((uint64_t)kc[it]) >> shift) & mask;
+      const uint32_t d = dest_of(kc[it]);
       if constexpr (MAXP <= 64) {
         // few partitions (the owner split: one per rank): an LDS atomic per key would queue the
         // wave's 64 lanes on at most `parts` addresses (one address at N = 1).  Instead one ballot
         // per partition ranks the wave's keys, lane p adds partition p's wave count to s_hist[p]
         // (distinct addresses), and each lane takes its partition's base from that lane.
-        const uint32_t d = self_slot(d0, self_last, parts);  // (the owner split: own rank's segment last)
         const bool lv = (live >> it) & 1u;
         // bit-sliced: one ballot per partition-index bit; a lane's mask keeps the live lanes that
         // agree with its partition (mine) / with partition `lane` (pm) on every bit — log2(parts)
@@ -723,7 +742,6 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
         dr[it] = d | (lv ? rk : 0u) << 10;
         if (it < kKS) store_one(it);
       } else {
-        const uint32_t d = d0;
         dr[it] = d | ((live >> it) & 1u ? atomicAdd(&s_hist[d], 1u) : 0u) << 10;
         if (it < kKS) store_one(it);
       }
@@ -770,7 +788,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
         const uint32_t d = dr[it] & 1023u;
         const uint32_t pos = s_loc[d] + (dr[it] >> 10);
         s_k[pos] = kc[it];
-        s_i[pos] = ((uint32_t)it * THREADS + tid) | d << 16;
+        s_i[pos] = (ImgT)(((uint32_t)it * THREADS + tid) | (kSplitNarrow ? 0u : d << 16));
       }
     }
     p_tl = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tot);
@@ -781,7 +799,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
     // whose run bounds every store, so the stale image stays inside reserved space)
     for (uint32_t q = tid; q < kTileKeys; q += THREADS) {
       s_k[q] = 0;
-      s_i[q] = q & 0xFFFFu;
+      s_i[q] = (ImgT)(q & 0xFFFFu);
     }
   }
   int64_t kA[PER], kB[PER];
@@ -1088,9 +1106,12 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
 #undef CCJ_PIPE_LAUNCH
     return hipGetLastError();
   }
+  // the fixed form: at most kSplitPerFixed keys per thread (its LDS holds 32-bit rows), own tile count
+  const int fper = per < kSplitPerFixed ? per : kSplitPerFixed;
+  const uint64_t f_tiles = (n + (uint64_t)kSplitThreads * fper - 1) / ((uint64_t)kSplitThreads * fper);
 #define CCJ_SPLIT_LAUNCH(C, MAXP, P)                                                                              \
   hipLaunchKernelGGL((slot_split_fixed<C, kSplitThreads, MAXP, P>), dim3(grid), dim3(kSplitThreads), 0, s, keys, n,      \
-                     shift, parts, n_tiles, cursors, cap, ovf_base, ovf_sub, out_keys, out_rows, status, ablate,         \
+                     shift, parts, f_tiles, cursors, cap, ovf_base, ovf_sub, out_keys, out_rows, status, ablate,         \
                      counts, chunk, runs, ovf_runs, row_base, self_last, ovf_pg)
   if (parts > kSplitParts / 2) {  // 1024 partitions: 10 keys per thread
     if (counts) CCJ_SPLIT_LAUNCH(true, kSplitParts, 10);
@@ -1099,8 +1120,8 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
     if (counts) CCJ_SPLIT_LAUNCH(true, kSplitParts / 2, 10);
     else CCJ_SPLIT_LAUNCH(false, kSplitParts / 2, 10);
   } else {
-    if (counts) CCJ_SPLIT_LAUNCH(true, kSplitParts / 2, kSplitPer);
-    else CCJ_SPLIT_LAUNCH(false, kSplitParts / 2, kSplitPer);
+    if (counts) CCJ_SPLIT_LAUNCH(true, kSplitParts / 2, kSplitPerFixed);
+    else CCJ_SPLIT_LAUNCH(false, kSplitParts / 2, kSplitPerFixed);
   }
 #undef CCJ_SPLIT_LAUNCH
   return hipGetLastError();

@@ -2,7 +2,7 @@
 # tools/gpu_ab.sh TAG WORKLOAD REPS VARIANT... — same-box A/B, run ON THE GPU BOX (via gpurun).
 # Replaces round 4's one-off tools/gpu_r4_*.sh scripts.  Each VARIANT is LIB or LIB:ENV=V[,ENV=V]:
 # LIB = "product", "tuning" or a library path (a build of libccj with one change, e.g.
-# tools/ab/libccj_<name>.so), ENV the tuning build's environment overrides for that run.  The variants run interleaved REPS times; one
+# tools/abx/libccj_<name>.so, a git-ignored directory that travels to the box), ENV the tuning build's environment overrides for that run.  The variants run interleaved REPS times; one
 # summary line per run goes to gpurun_out/TAG_all.log:
 #   WORKLOAD c2 | c2ord | c3 | c5: bench.py's line — ms per step and the phases (split / walk / gather)
 #   WORKLOAD c3split:              tools/exp_split_c3.py's split + walk lines
