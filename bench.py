@@ -277,7 +277,7 @@ def phase_report(pev, path, c5=False):
     t = [p.ms() for p in pev]
     mean = [sum(x[i] for x in t) / len(t) for i in range(3)]
     k = PHASE_KERNELS.get(path, ("?", "?", "?"))
-    gather_k = "gather_payload_quad (8 payload columns)" if c5 else k[2]
+    gather_k = "gather_payload_cols<8> (8 payload columns, stores transposed through LDS)" if c5 else k[2]
     return {"schema": "reference CycleProfiler phases (profiler.h:262-290)",
             "hash_find_bucket_ms": mean[0], "match_tuples_and_advance_pointers_ms": mean[1],
             "gather_tuples_ms": mean[2],
@@ -887,11 +887,11 @@ def bench_single(args, dev, stream):
                          # measured DRAM bytes (whole 128-B lines per random slot read) per second
                          "traffic_GBps": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
                          "kernel": (("ccj_probe_partitioned, CCJ_PART_ROWS (slot_split_pipe writing keys + rows, "
-                                     "probe_walk2<POS> writing match positions, gather_payload_quad)") if c5 and
+                                     "probe_walk2<POS> writing match positions, gather_payload_cols<8>)") if c5 and
                                     args.path == "partitioned" and rows_mode else
                                     ("ccj_probe_partitioned (slot_split_pipe + probe_win<3> with positions + "
-                                     "gather_payload_quad)") if c5 and args.path == "partitioned" else
-                                    "probe_chunks<LP,2> + gather_payload_quad" if c5 else PATH_KERNELS[args.path]),
+                                     "gather_payload_cols<8>)") if c5 and args.path == "partitioned" else
+                                    "probe_chunks<LP,2> + gather_payload_cols<8>" if c5 else PATH_KERNELS[args.path]),
                          "kernel_ms": kern_ms, "rocprof_kernels_ms": kernels_ms,
                          "alg_bytes_per_tuple": alg_bytes_per_tuple, "s_bar": s_bar, "m_bar": m_bar,
                          # the same step on the bytes its walk reads: slot words through the first

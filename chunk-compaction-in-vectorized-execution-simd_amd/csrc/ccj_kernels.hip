@@ -3232,6 +3232,7 @@ struct GatherParams {
   uint32_t stride;
   int64_t *cols[CCJ_MAX_PAYLOAD_COLS];
   uint32_t shift;  // timing only (tuning build, CCJ_GATHER_SHIFT): row = position >> shift
+  uint32_t mask;   // timing only (tuning build, CCJ_GATHER_MASK): row = (position >> shift) & mask
   uint32_t ablate; // timing only (tuning build, CCJ_GATHER_ABLATE): 1 = no column stores
 };
 
@@ -3298,7 +3299,7 @@ __global__ __launch_bounds__(256) void gather_payload_quad(GatherParams g) {
     longlong2 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      v[u] = reinterpret_cast<const longlong2 *>(g.pay + (uint64_t)(ps[u] >> g.shift) * g.stride)[q];
+      v[u] = reinterpret_cast<const longlong2 *>(g.pay + (uint64_t)((ps[u] >> g.shift) & g.mask) * g.stride)[q];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t j = base + u * 64 + r0;
@@ -3310,13 +3311,83 @@ __global__ __launch_bounds__(256) void gather_payload_quad(GatherParams g) {
   }
 }
 
+// 8 columns, the stores transposed through LDS: per step of 64 x U rows the quads load rows as in
+// gather_payload_quad and drop them into a column-major LDS tile (8 x 64U int64; U = 8: 32 KiB);
+// each wave then stores 1 KiB of ONE column per instruction (16 bytes = two rows per lane) instead
+// of four columns' 128-byte pieces of 8 bytes per lane.  The stores alone (rows from one line,
+// timing only) take 14.0 ms per C5 step against the quad form's 19.2; the row reads alone 15.1
+// against 17.1 (profiles/r5_ab_gather_cols.log).
+template <int U>
+__global__ __launch_bounds__(256) void gather_payload_cols(GatherParams g) {
+  constexpr uint32_t kStep = 64 * U;  // rows per step
+  typedef long long i64x2 __attribute__((ext_vector_type(2)));
+  __shared__ int64_t *s_cols[CCJ_MAX_PAYLOAD_COLS];
+  __shared__ int64_t s_t[8][kStep];
+  if (threadIdx.x < CCJ_MAX_PAYLOAD_COLS) s_cols[threadIdx.x] = g.cols[threadIdx.x];
+  const uint64_t c = blockIdx.x;
+  const uint64_t ob = g.out_base ? g.out_base[c] : c * g.cap;
+  const uint32_t n = g.count[c];
+  const uint32_t q = threadIdx.x & 3u, r0 = threadIdx.x >> 2;
+  // software pipeline: step i's tile is stored while step i + 1's rows and step i + 2's positions
+  // are in flight (loads issued before the stores, so no wait on a load drains them)
+  uint32_t ps[U];
+  i64x2 v[U];
+  auto load_pos = [&](uint32_t b) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t j = b + u * 64 + r0;
+      ps[u] = g.pos[ob + (j < n ? j : 0u)];
+    }
+  };
+  auto load_rows = [&]() {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = reinterpret_cast<const i64x2 *>(g.pay + (uint64_t)((ps[u] >> g.shift) & g.mask) * g.stride)[q];
+  };
+  if (n == 0) return;
+  load_pos(0);
+  load_rows();
+  if (kStep < n) load_pos(kStep);
+  for (uint32_t base = 0; base < n; base += kStep) {
+    __syncthreads();  // the previous tile is stored (and s_cols is set)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      s_t[2 * q][u * 64 + r0] = v[u].x;
+      s_t[2 * q + 1][u * 64 + r0] = v[u].y;
+    }
+    __syncthreads();
+    if (base + kStep < n) load_rows();
+    if (base + 2 * kStep < n) load_pos(base + 2 * kStep);
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t rows = n - base < kStep ? n - base : kStep;
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      // 8 columns x kStep rows = 4U 16-byte pieces per thread; a wave's 64 lanes: 1 KiB of one column
+      const uint32_t idx = (uint32_t)k * 256u + threadIdx.x, col = idx / (kStep / 2), pr = (idx % (kStep / 2)) * 2u;
+      const i64x2 x = *reinterpret_cast<const i64x2 *>(&s_t[col][pr]);
+      int64_t *dst = s_cols[col] + ob + base + pr;
+      if (CCJ_ABLATED(g.ablate, 1u) && (x.x ^ x.y) != 0x5A5A5A5A5A5A5A5All) continue;
+      if (pr + 1 < rows) __builtin_nontemporal_store(x, reinterpret_cast<i64x2 *>(dst));
+      else if (pr < rows) __builtin_nontemporal_store((int64_t)x.x, dst);
+    }
+  }
+}
+
 template <int NP>
 hipError_t launch_gather_np(const GatherParams &g, uint64_t n_chunks, hipStream_t s) {
   const bool vec = (g.stride % 2 == 0) && ((uintptr_t)g.pay % 16 == 0);
   // 8 columns: 2 / 4 / 8 rows in flight per lane group 26.9 ms each at C5, the walk's XCD order
   // 27.0, plain instead of non-temporal stores 27.8-28.9 (profiles/r1g_*)
   // (row pieces by LDS-DMA instead: 42.2-42.5 ms per C5 step against 42.2-42.3, round 3)
-  if (NP == 8 && vec) hipLaunchKernelGGL((gather_payload_quad<4>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
+  // 8 columns: the transposed stores (gather_payload_cols<8>: C5 gather 26.7-27.0 -> 25.6-25.7 ms,
+  // 256-row steps 26.9-28.4, 1024-row steps 27.0, profiles/r5_ab_gather_cols.log) where every
+  // column's rows are 16-byte aligned (no packed pipeline outputs: out_base == nullptr, cap even,
+  // columns 16-byte aligned); the tuning build's CCJ_GATHER_T=0 runs the quad form for A/B
+  bool cols16 = NP == 8 && (g.out_base == nullptr && g.cap % 2 == 0);
+  for (int q = 0; q < NP; ++q) cols16 = cols16 && (uintptr_t)g.cols[q] % 16 == 0;
+  if (NP == 8 && vec && cols16 && ccj_tune_int("CCJ_GATHER_T", 1))
+    hipLaunchKernelGGL(gather_payload_cols<8>, dim3((unsigned)n_chunks), dim3(256), 0, s, g);
+  else if (NP == 8 && vec) hipLaunchKernelGGL((gather_payload_quad<4>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
   else if (vec) hipLaunchKernelGGL((gather_payload<NP, true>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
   else hipLaunchKernelGGL((gather_payload<NP, false>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
   return hipGetLastError();
@@ -3333,6 +3404,7 @@ hipError_t launch_gather_payload(const ProbeParams &p, const uint32_t *pos, hipS
   g.stride = p.pay_stride;
   for (uint32_t q = 0; q < p.n_pay; ++q) g.cols[q] = p.out_cols[q];
   g.shift = (uint32_t)ccj_tune_int("CCJ_GATHER_SHIFT", 0);
+  g.mask = (uint32_t)ccj_tune_int("CCJ_GATHER_MASK", -1);
   g.ablate = (uint32_t)ccj_tune_int("CCJ_GATHER_ABLATE", 0);
   switch (p.n_pay) {
     case 1: return launch_gather_np<1>(g, p.n_chunks, s);

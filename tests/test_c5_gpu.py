@@ -116,14 +116,17 @@ def test_c5_partitioned(cf):
 
 
 @pytest.mark.parametrize("chunk,n_probe,spread", [(2048, 1 << 20, 8), (2048, (1 << 20) + 777, 0), (1000, 1 << 20, 8),
-                                                  (1022, 300001, 8), (2048, 1 << 20, 1)])
+                                                  (1022, 300001, 8), (2048, 1 << 20, 1), (1001, 300001, 8),
+                                                  (2048, 3 * 2048 + 5, 0)])
 def test_c5_partitioned_rows(chunk, n_probe, spread):
     """C5 under CCJ_PART_ROWS (distinct build keys, the bench's C5 route): the split writes every
     position's row and key into the outputs, probe_walk1<POS> leaves each match's table position at
     its output slot (all-matched chunks) or compacts the chunk (chunks with a miss), the gather reads
     them.  spread: probe keys from [0, n_build + n_build / spread) (0: every probe hits; 1: half
     miss).  sel is the original row; every gathered row belongs to the build tuple with the row's
-    key, the payload column holds the key, and the count is exact."""
+    key, the payload column holds the key, and the count is exact.  Even chunks take the gather
+    with stores transposed through LDS (gather_payload_cols, 512-row steps: 1000 / 1022 / 3 x 2048
+    + 5 end in partial steps and odd row counts), an odd chunk (1001) the quad form."""
     n_build = 1 << 18
     bkeys = ref_keys(n_build, 1)
     pay = payload_rows(n_build)
