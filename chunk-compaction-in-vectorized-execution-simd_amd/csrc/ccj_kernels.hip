@@ -3316,14 +3316,16 @@ __global__ __launch_bounds__(256) void gather_payload_quad(GatherParams g) {
 // each wave then stores 1 KiB of ONE column per instruction (16 bytes = two rows per lane) instead
 // of four columns' 128-byte pieces of 8 bytes per lane.  The stores alone (rows from one line,
 // timing only) take 14.0 ms per C5 step against the quad form's 19.2; the row reads alone 15.1
-// against 17.1 (profiles/r5_ab_gather_cols.log).
+// against 17.1 (profiles/r5_ab_gather_cols.log).  The column pointers come from the kernel
+// arguments (the store pass's column is its unrolled index), so the LDS tile is the workgroup's
+// only LDS — 32 KiB, five workgroups per CU instead of four with a pointer table beside it: same
+// box, gather 26.7-27.2 (four) -> 25.2-25.6 ms (profiles/r5_ab_gather_cols_5wg.log).
 template <int U>
 __global__ __launch_bounds__(256) void gather_payload_cols(GatherParams g) {
   constexpr uint32_t kStep = 64 * U;  // rows per step
   typedef long long i64x2 __attribute__((ext_vector_type(2)));
-  __shared__ int64_t *s_cols[CCJ_MAX_PAYLOAD_COLS];
-  __shared__ int64_t s_t[8][kStep];
-  if (threadIdx.x < CCJ_MAX_PAYLOAD_COLS) s_cols[threadIdx.x] = g.cols[threadIdx.x];
+  static_assert(kStep / 2 == 256, "one column per thread-wide store pass (the column index is k)");
+  __shared__ int64_t s_t[8][kStep];  // exactly 32 KiB: five workgroups per CU
   const uint64_t c = blockIdx.x;
   const uint64_t ob = g.out_base ? g.out_base[c] : c * g.cap;
   const uint32_t n = g.count[c];
@@ -3349,7 +3351,7 @@ __global__ __launch_bounds__(256) void gather_payload_cols(GatherParams g) {
   load_rows();
   if (kStep < n) load_pos(kStep);
   for (uint32_t base = 0; base < n; base += kStep) {
-    __syncthreads();  // the previous tile is stored (and s_cols is set)
+    __syncthreads();  // the previous tile is stored
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       s_t[2 * q][u * 64 + r0] = v[u].x;
@@ -3363,9 +3365,9 @@ __global__ __launch_bounds__(256) void gather_payload_cols(GatherParams g) {
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       // 8 columns x kStep rows = 4U 16-byte pieces per thread; a wave's 64 lanes: 1 KiB of one column
-      const uint32_t idx = (uint32_t)k * 256u + threadIdx.x, col = idx / (kStep / 2), pr = (idx % (kStep / 2)) * 2u;
-      const i64x2 x = *reinterpret_cast<const i64x2 *>(&s_t[col][pr]);
-      int64_t *dst = s_cols[col] + ob + base + pr;
+      const uint32_t pr = threadIdx.x * 2u;  // piece k * 256 + tid: column k, rows 2 tid, 2 tid + 1
+      const i64x2 x = *reinterpret_cast<const i64x2 *>(&s_t[k][pr]);
+      int64_t *dst = g.cols[k] + ob + base + pr;
       if (CCJ_ABLATED(g.ablate, 1u) && (x.x ^ x.y) != 0x5A5A5A5A5A5A5A5All) continue;
       if (pr + 1 < rows) __builtin_nontemporal_store(x, reinterpret_cast<i64x2 *>(dst));
       else if (pr < rows) __builtin_nontemporal_store((int64_t)x.x, dst);
@@ -3379,8 +3381,8 @@ hipError_t launch_gather_np(const GatherParams &g, uint64_t n_chunks, hipStream_
   // 8 columns: 2 / 4 / 8 rows in flight per lane group 26.9 ms each at C5, the walk's XCD order
   // 27.0, plain instead of non-temporal stores 27.8-28.9 (profiles/r1g_*)
   // (row pieces by LDS-DMA instead: 42.2-42.5 ms per C5 step against 42.2-42.3, round 3)
-  // 8 columns: the transposed stores (gather_payload_cols<8>: C5 gather 26.7-27.0 -> 25.6-25.7 ms,
-  // 256-row steps 26.9-28.4, 1024-row steps 27.0, profiles/r5_ab_gather_cols.log) where every
+  // 8 columns: the transposed stores (gather_payload_cols<8>: C5 gather 26.7-27.0 -> 25.2-25.6 ms,
+  // 256-row steps 26.9-28.4, 1024-row steps 27.0, profiles/r5_ab_gather_cols*.log) where every
   // column's rows are 16-byte aligned (no packed pipeline outputs: out_base == nullptr, cap even,
   // columns 16-byte aligned); the tuning build's CCJ_GATHER_T=0 runs the quad form for A/B
   bool cols16 = NP == 8 && (g.out_base == nullptr && g.cap % 2 == 0);

@@ -1,6 +1,4 @@
-# round 5 call AT: gather_payload_cols<8> as the product's 8-column gather — the payload tests
-# (C5, probe, bench), then the C5 profile (kernel trace + counters) of the product
+# round 5 call AV: C5 gather forms on one box — product (cols, 5 WG/CU), the previous cols build
+# (4 WG/CU), the quad form (tuning build, CCJ_GATHER_T=0)
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && \
-timeout -k 10 600 python -u -m pytest tests/test_c5_gpu.py tests/test_probe_gpu.py tests/test_bench_gpu.py -m gpu -x -q \
-  --timeout 300 --timeout-method thread > gpurun_out/r5at_tests.log 2>&1 && \
-bash tools/profile_round.sh r5h c5 > gpurun_out/r5at_prof.log 2>&1
+bash tools/gpu_ab.sh r5av c5 3 product tools/abx/libccj_gcols_lds.so tuning:CCJ_GATHER_T=0 tuning > gpurun_out/r5av_ab.log 2>&1
