@@ -3324,8 +3324,8 @@ template <int U>
 __global__ __launch_bounds__(256) void gather_payload_cols(GatherParams g) {
   constexpr uint32_t kStep = 64 * U;  // rows per step
   typedef long long i64x2 __attribute__((ext_vector_type(2)));
-  static_assert(kStep / 2 == 256, "one column per thread-wide store pass (the column index is k)");
-  __shared__ int64_t s_t[8][kStep];  // exactly 32 KiB: five workgroups per CU
+  static_assert(kStep / 2 % 64 == 0, "a wave's 64 store pieces lie in one column");
+  __shared__ int64_t s_t[8][kStep];  // U = 8: exactly 32 KiB, five workgroups per CU
   const uint64_t c = blockIdx.x;
   const uint64_t ob = g.out_base ? g.out_base[c] : c * g.cap;
   const uint32_t n = g.count[c];
@@ -3365,9 +3365,15 @@ __global__ __launch_bounds__(256) void gather_payload_cols(GatherParams g) {
 #pragma unroll
     for (int k = 0; k < U; ++k) {
       // 8 columns x kStep rows = 4U 16-byte pieces per thread; a wave's 64 lanes: 1 KiB of one column
-      const uint32_t pr = threadIdx.x * 2u;  // piece k * 256 + tid: column k, rows 2 tid, 2 tid + 1
-      const i64x2 x = *reinterpret_cast<const i64x2 *>(&s_t[k][pr]);
-      int64_t *dst = g.cols[k] + ob + base + pr;
+      // piece k * 256 + tid: column (k * 256 + tid) / (kStep / 2) — k itself at U = 8 — rows pr, pr + 1
+      const uint32_t idx = (uint32_t)k * 256u + threadIdx.x;
+      const uint32_t col = kStep / 2 == 256 ? (uint32_t)k : (uint32_t)__builtin_amdgcn_readfirstlane((int)(idx / (kStep / 2)));
+      const uint32_t pr = (idx % (kStep / 2)) * 2u;
+      const i64x2 x = *reinterpret_cast<const i64x2 *>(&s_t[col][pr]);
+      int64_t *cp = g.cols[0];
+#pragma unroll
+      for (int cc = 1; cc < 8; ++cc) cp = col == (uint32_t)cc ? g.cols[cc] : cp;  // (wave-uniform select)
+      int64_t *dst = cp + ob + base + pr;
       if (CCJ_ABLATED(g.ablate, 1u) && (x.x ^ x.y) != 0x5A5A5A5A5A5A5A5All) continue;
       if (pr + 1 < rows) __builtin_nontemporal_store(x, reinterpret_cast<i64x2 *>(dst));
       else if (pr < rows) __builtin_nontemporal_store((int64_t)x.x, dst);
@@ -3387,8 +3393,15 @@ hipError_t launch_gather_np(const GatherParams &g, uint64_t n_chunks, hipStream_
   // columns 16-byte aligned); the tuning build's CCJ_GATHER_T=0 runs the quad form for A/B
   bool cols16 = NP == 8 && (g.out_base == nullptr && g.cap % 2 == 0);
   for (int q = 0; q < NP; ++q) cols16 = cols16 && (uintptr_t)g.cols[q] % 16 == 0;
-  if (NP == 8 && vec && cols16 && ccj_tune_int("CCJ_GATHER_T", 1))
+  if (NP == 8 && vec && cols16 && ccj_tune_int("CCJ_GATHER_T", 1)) {
+#ifdef CCJ_TUNING
+    const int gu = ccj_tune_int("CCJ_GATHER_U", 8);  // (tuning build: 384- / 256-row steps, 24 / 16 KiB tiles)
+    if (gu == 6) hipLaunchKernelGGL(gather_payload_cols<6>, dim3((unsigned)n_chunks), dim3(256), 0, s, g);
+    else if (gu == 4) hipLaunchKernelGGL(gather_payload_cols<4>, dim3((unsigned)n_chunks), dim3(256), 0, s, g);
+    else
+#endif
     hipLaunchKernelGGL(gather_payload_cols<8>, dim3((unsigned)n_chunks), dim3(256), 0, s, g);
+  }
   else if (NP == 8 && vec) hipLaunchKernelGGL((gather_payload_quad<4>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
   else if (vec) hipLaunchKernelGGL((gather_payload<NP, true>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
   else hipLaunchKernelGGL((gather_payload<NP, false>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
