@@ -3332,19 +3332,26 @@ __global__ __launch_bounds__(256) void gather_payload_cols(GatherParams g) {
   const uint32_t q = threadIdx.x & 3u, r0 = threadIdx.x >> 2;
   // software pipeline: step i's tile is stored while step i + 1's rows and step i + 2's positions
   // are in flight (loads issued before the stores, so no wait on a load drains them)
-  uint32_t ps[U];
+  // positions: each lane loads its own (U / 4 loads of 64 distinct positions per wave) and the
+  // quads take theirs by ds_bpermute — 4x fewer position-load instructions than a load per quad
+  // lane: same box, 3 x interleaved, gather 25.55-25.58 -> 25.37-25.39 ms (profiles/r5_ab_gather_pos.log)
+  static_assert(U % 4 == 0, "U / 4 position loads per lane");
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  uint32_t pl[U / 4];
   i64x2 v[U];
   auto load_pos = [&](uint32_t b) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t j = b + u * 64 + r0;
-      ps[u] = g.pos[ob + (j < n ? j : 0u)];
+    for (int h = 0; h < U / 4; ++h) {  // row (4h + lane / 16) * 64 + 16 wave + lane % 16 of the step
+      const uint32_t j = b + (uint32_t)(4 * h + (lane >> 4)) * 64u + wave * 16u + (lane & 15u);
+      pl[h] = g.pos[ob + (j < n ? j : 0u)];
     }
   };
   auto load_rows = [&]() {
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = reinterpret_cast<const i64x2 *>(g.pay + (uint64_t)((ps[u] >> g.shift) & g.mask) * g.stride)[q];
+    for (int u = 0; u < U; ++u) {
+      const uint32_t pu = (uint32_t)__shfl((int)pl[u / 4], (int)(((u & 3) << 4) | (lane >> 2)));
+      v[u] = reinterpret_cast<const i64x2 *>(g.pay + (uint64_t)((pu >> g.shift) & g.mask) * g.stride)[q];
+    }
   };
   if (n == 0) return;
   load_pos(0);
@@ -3395,9 +3402,10 @@ hipError_t launch_gather_np(const GatherParams &g, uint64_t n_chunks, hipStream_
   for (int q = 0; q < NP; ++q) cols16 = cols16 && (uintptr_t)g.cols[q] % 16 == 0;
   if (NP == 8 && vec && cols16 && ccj_tune_int("CCJ_GATHER_T", 1)) {
 #ifdef CCJ_TUNING
-    const int gu = ccj_tune_int("CCJ_GATHER_U", 8);  // (tuning build: 384- / 256-row steps, 24 / 16 KiB tiles)
-    if (gu == 6) hipLaunchKernelGGL(gather_payload_cols<6>, dim3((unsigned)n_chunks), dim3(256), 0, s, g);
-    else if (gu == 4) hipLaunchKernelGGL(gather_payload_cols<4>, dim3((unsigned)n_chunks), dim3(256), 0, s, g);
+    // (tuning build: 256-row steps, 16 KiB tiles; 384-row steps measured 26.6 ms before the per-lane
+    // position loads, which need U a multiple of 4)
+    if (ccj_tune_int("CCJ_GATHER_U", 8) == 4)
+      hipLaunchKernelGGL(gather_payload_cols<4>, dim3((unsigned)n_chunks), dim3(256), 0, s, g);
     else
 #endif
     hipLaunchKernelGGL(gather_payload_cols<8>, dim3((unsigned)n_chunks), dim3(256), 0, s, g);
