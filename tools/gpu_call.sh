@@ -1,6 +1,6 @@
-# round 5 call BA: gather_payload_cols<8> with per-lane position loads shared to the quads by
-# ds_bpermute (U / 4 = 2 position loads per wave and step instead of 8) against the product; C5 tests
+# round 5 call BB: round-end checks on the final tree — the whole GPU suite, smoke, and the driver's
+# bench command (python3 bench.py --gpus 1 --steps 20 --warmup 5)
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && \
-bash tools/gpu_ab.sh r5ba c5 3 product tools/abx/libccj_gpos.so > gpurun_out/r5ba_ab.log 2>&1 && \
-CCJ_LIB_PATH=tools/abx/libccj_gpos.so timeout -k 10 300 \
-  python -u -m pytest tests/test_c5_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r5ba_tests.log 2>&1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r5bb_gputest.log 2>&1 && \
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r5bb_smoke.log 2>&1 && \
+timeout -k 10 500 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r5bb_bench.log 2> gpurun_out/r5bb_bench.err
