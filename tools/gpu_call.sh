@@ -1,6 +1,3 @@
-# round 5 call BB: round-end checks on the final tree — the whole GPU suite, smoke, and the driver's
-# bench command (python3 bench.py --gpus 1 --steps 20 --warmup 5)
+# round 5 call BC: the C5 profile (kernel trace + counters) of the final tree (per-lane position loads)
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && \
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r5bb_gputest.log 2>&1 && \
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r5bb_smoke.log 2>&1 && \
-timeout -k 10 500 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r5bb_bench.log 2> gpurun_out/r5bb_bench.err
+bash tools/profile_round.sh r5j c5 > gpurun_out/r5bc_prof.log 2>&1
