@@ -1,4 +1,3 @@
-# round 5 call BD: gather_payload_cols' column stores plain instead of non-temporal (tuning build,
-# CCJ_GATHER_ABLATE=2)
+# round 5 call BE: the C2 headline profile (kernel trace + counters) of the final tree
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && \
-bash tools/gpu_ab.sh r5bd c5 3 tuning tuning:CCJ_GATHER_ABLATE=2 > gpurun_out/r5bd_ab.log 2>&1
+bash tools/profile_round.sh r5k c2 > gpurun_out/r5be_prof.log 2>&1
