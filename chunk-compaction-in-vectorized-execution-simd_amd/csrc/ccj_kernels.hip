@@ -3359,10 +3359,14 @@ __global__ __launch_bounds__(256) void gather_payload_cols(GatherParams g) {
   if (kStep < n) load_pos(kStep);
   for (uint32_t base = 0; base < n; base += kStep) {
     __syncthreads();  // the previous tile is stored
+    // the tile's rows XOR-swizzled by 8 x (column / 2): the four quad lanes' columns (2q, 2q + 1) sit
+    // 4 KiB apart, i.e. on the same banks, so without it every 8-byte write is a 4-way conflict
+    // (60 % of the LDS cycles, profiles/r5u3_c5_units.json); same box, gather 25.39 / 26.87 / 26.83 ->
+    // 25.33 / 25.33 / 25.33 ms (profiles/r5_ab_gather_swizzle.log)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      s_t[2 * q][u * 64 + r0] = v[u].x;
-      s_t[2 * q + 1][u * 64 + r0] = v[u].y;
+      s_t[2 * q][(u * 64 + r0) ^ (8u * q)] = v[u].x;
+      s_t[2 * q + 1][(u * 64 + r0) ^ (8u * q)] = v[u].y;
     }
     __syncthreads();
     if (base + kStep < n) load_rows();
@@ -3376,7 +3380,7 @@ __global__ __launch_bounds__(256) void gather_payload_cols(GatherParams g) {
       const uint32_t idx = (uint32_t)k * 256u + threadIdx.x;
       const uint32_t col = kStep / 2 == 256 ? (uint32_t)k : (uint32_t)__builtin_amdgcn_readfirstlane((int)(idx / (kStep / 2)));
       const uint32_t pr = (idx % (kStep / 2)) * 2u;
-      const i64x2 x = *reinterpret_cast<const i64x2 *>(&s_t[col][pr]);
+      const i64x2 x = *reinterpret_cast<const i64x2 *>(&s_t[col][pr ^ (8u * (col >> 1))]);
       int64_t *cp = g.cols[0];
 #pragma unroll
       for (int cc = 1; cc < 8; ++cc) cp = col == (uint32_t)cc ? g.cols[cc] : cp;  // (wave-uniform select)

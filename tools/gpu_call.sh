@@ -1,3 +1,6 @@
-# round 5 call BF: per-unit counters of the final C5 gather (gather_payload_cols) — which unit holds it now
+# round 5 call BG: gather_payload_cols with its LDS tile XOR-swizzled (conflict-free 8-byte writes)
+# against the product; C5 tests on it
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && \
-PMC_KERNEL="gather_payload_cols" bash tools/unit_pass.sh r5u3_c5 --workload c5 > gpurun_out/r5bf_c5.log 2>&1
+bash tools/gpu_ab.sh r5bg c5 3 product tools/abx/libccj_gswz.so > gpurun_out/r5bg_ab.log 2>&1 && \
+CCJ_LIB_PATH=tools/abx/libccj_gswz.so timeout -k 10 300 \
+  python -u -m pytest tests/test_c5_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r5bg_tests.log 2>&1
