@@ -1,6 +1,6 @@
-# round 5 call BG: gather_payload_cols with its LDS tile XOR-swizzled (conflict-free 8-byte writes)
-# against the product; C5 tests on it
+# round 5 call BH: round-end checks on the final tree — the whole GPU suite, smoke, and the driver's
+# bench command (python3 bench.py --gpus 1 --steps 20 --warmup 5)
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && \
-bash tools/gpu_ab.sh r5bg c5 3 product tools/abx/libccj_gswz.so > gpurun_out/r5bg_ab.log 2>&1 && \
-CCJ_LIB_PATH=tools/abx/libccj_gswz.so timeout -k 10 300 \
-  python -u -m pytest tests/test_c5_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r5bg_tests.log 2>&1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r5bh_gputest.log 2>&1 && \
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r5bh_smoke.log 2>&1 && \
+timeout -k 10 500 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r5bh_bench.log 2> gpurun_out/r5bh_bench.err
