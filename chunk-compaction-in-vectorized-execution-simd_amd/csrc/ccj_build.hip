@@ -4,22 +4,23 @@
 // bucket h(k_t) & mask (:29-35), so a chain lists its keys in generator order.  The CSR form of
 // that is a STABLE counting sort of the tuples by bucket:
 //   1. bucket ids b_t = murmurhash64(k_t) & mask and a histogram of them (one atomic per tuple);
-//   2. off = exclusive scan of the histogram (hipCUB) — the chain ranges, off[size] = n;
-//   3. (b_t, t) sorted by b_t with a stable LSD radix sort over the log2(size) bucket bits
-//      (hipCUB/rocPRIM), so equal buckets keep ascending t: position j of the chain array holds
-//      tuple idx[j] — exactly the std::list order;
+//   2. off = exclusive scan of the histogram (ccj_scan.hip) — the chain ranges, off[size] = n;
+//   3. (b_t, t) sorted by b_t with the hand-written stable LSD radix sort (ccj_sort.hip) over the
+//      log2(size) bucket bits, so equal buckets keep ascending t: position j of the chain array
+//      holds tuple idx[j] — exactly the std::list order;
 //   4. chain[j] = k_idx[j], row[j] = idx[j] (padded to a multiple of 4 with -1 / kNoRow: the probes
 //      read aligned 4-key windows);
 //   5. per bucket the 16-byte record {start | len << 32, first key} and the 8-byte record
 //      {start | len << 32 | fp(node 0) << 40 | fp(node 1) << 52} (kept when the longest chain is
 //      < 255), plus the longest chain (max_rounds);
 //   6. max_dup (largest multiplicity of one key, which sizes every probe output): known from the
-//      generator for reference builds; otherwise from a sorted copy of the keys — the largest L
-//      with some i such that sorted[i] == sorted[i + L - 1], found by doubling then bisection.
+//      generator for reference builds; otherwise from a copy of the keys sorted by the same radix
+//      sort (as 64-bit patterns: equal keys adjacent) — the largest L with some i such that
+//      sorted[i] == sorted[i + L - 1], found by doubling then bisection.
 // Every array is byte-identical to the host build (ccj_api.hip build_chain_host, kept for
 // ccj_table_build_from_host); tests/test_build_gpu.py compares them.  Build time is untimed, as in
 // the reference (main.cpp:62-68 builds before the timer at :92-94).
-#include <hipcub/hipcub.hpp>
+#include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <memory>
@@ -155,22 +156,24 @@ int hip_err(hipError_t e, const char *what) {
     if (e_ != hipSuccess) return hip_err(e_, what); \
   } while (0)
 
-// Largest multiplicity of one key among d_keys[0, n): sort a copy, then find the largest L with
+// Largest multiplicity of one key among d_keys[0, n): radix-sort a copy, then find the largest L with
 // a run of L equal keys (doubling, then bisection; one pass for distinct keys).
 int max_multiplicity(const int64_t *d_keys, uint64_t n, hipStream_t s, uint64_t *out) {
   *out = n ? 1 : 0;
   if (n < 2) return CCJ_OK;
-  DevBuf sorted, tmp, flag;
-  size_t tb = 0;
-  BUILD_TRY(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, d_keys, (int64_t *)nullptr, n, 0, 64, s), "sort size");
-  BUILD_TRY(sorted.alloc(n * sizeof(int64_t)), "sorted keys");
-  BUILD_TRY(tmp.alloc(tb), "sort scratch");
+  DevBuf a, b, tmp, flag;
+  BUILD_TRY(a.alloc(n * sizeof(int64_t)), "sorted keys");
+  BUILD_TRY(b.alloc(n * sizeof(int64_t)), "sorted keys (alt)");
+  BUILD_TRY(tmp.alloc(radix_sort_temp_bytes(n)), "sort scratch");
   BUILD_TRY(flag.alloc(sizeof(uint32_t)), "flag");
-  BUILD_TRY(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, d_keys, sorted.as<int64_t>(), n, 0, 64, s), "sort keys");
+  BUILD_TRY(hipMemcpyAsync(a.p, d_keys, n * sizeof(int64_t), hipMemcpyDeviceToDevice, s), "key copy");
+  bool in_alt = false;
+  BUILD_TRY(radix_sort_keys_u64(a.as<uint64_t>(), b.as<uint64_t>(), n, tmp.p, s, &in_alt), "sort keys");
+  const int64_t *sorted = in_alt ? b.as<int64_t>() : a.as<int64_t>();
   auto test = [&](uint64_t L, bool *yes) -> int {
     uint32_t h = 0;
     BUILD_TRY(hipMemsetAsync(flag.p, 0, sizeof(uint32_t), s), "flag reset");
-    hipLaunchKernelGGL(has_run, dim3(grid_of(n, 256)), dim3(256), 0, s, sorted.as<int64_t>(), n, L, flag.as<uint32_t>());
+    hipLaunchKernelGGL(has_run, dim3(grid_of(n, 256)), dim3(256), 0, s, sorted, n, L, flag.as<uint32_t>());
     BUILD_TRY(hipGetLastError(), "has_run");
     BUILD_TRY(hipMemcpyAsync(&h, flag.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "flag read");
     BUILD_TRY(hipStreamSynchronize(s), "flag sync");
@@ -246,19 +249,17 @@ int build_chain_device(const int64_t *d_keys, uint64_t n, hipStream_t s, uint64_
   }
   BUILD_TRY(scan_tmp.alloc(scan_u64_temp_bytes(size + 1)), "scan scratch");
   BUILD_TRY(scan_exclusive_u32(cnt.as<uint32_t>(), off.as<uint32_t>(), size + 1, nullptr, scan_tmp.p, s), "offset scan");
+  const uint32_t *idx_sorted = idx.as<uint32_t>();
   if (n) {
     // stable LSD radix sort by bucket: equal buckets keep ascending tuple order (push_back order)
-    const int end_bit = bits ? (int)bits : 1;
-    size_t sb = 0;
-    BUILD_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, sb, bid.as<uint32_t>(), bid_s.as<uint32_t>(),
-                                                 idx.as<uint32_t>(), idx_s.as<uint32_t>(), n, 0, end_bit, s),
-              "sort size");
-    BUILD_TRY(sort_tmp.alloc(sb), "sort scratch");
-    BUILD_TRY(hipcub::DeviceRadixSort::SortPairs(sort_tmp.p, sb, bid.as<uint32_t>(), bid_s.as<uint32_t>(),
-                                                 idx.as<uint32_t>(), idx_s.as<uint32_t>(), n, 0, end_bit, s),
+    bool in_alt = false;
+    BUILD_TRY(sort_tmp.alloc(radix_sort_temp_bytes(n)), "sort scratch");
+    BUILD_TRY(radix_sort_pairs_u32(bid.as<uint32_t>(), bid_s.as<uint32_t>(), idx.as<uint32_t>(), idx_s.as<uint32_t>(), n,
+                                   bits ? bits : 1, sort_tmp.p, s, &in_alt),
               "bucket sort");
+    if (in_alt) idx_sorted = idx_s.as<uint32_t>();
   }
-  hipLaunchKernelGGL(chain_gather, dim3(grid_of(n_pad, 256)), dim3(256), 0, s, d_keys, idx_s.as<uint32_t>(), n, n_pad,
+  hipLaunchKernelGGL(chain_gather, dim3(grid_of(n_pad, 256)), dim3(256), 0, s, d_keys, idx_sorted, n, n_pad,
                      chain.as<int64_t>(), row.as<uint32_t>());
   BUILD_TRY(hipGetLastError(), "chain gather");
   hipLaunchKernelGGL(chain_records, dim3(std::min<unsigned>(grid_of(n_rec8, 256), 4096)), dim3(256), 0, s, off.as<uint32_t>(),

@@ -111,7 +111,8 @@ struct ProbeParams {
   const uint64_t *chunk_base;
   const uint64_t *out_base;
   // Fixed-capacity partitioned input (ccj_probe_partitioned): chunk c's live rows are the first
-  // min(seg_count[g*seg_parts + d] - offset, chunk) of it, segment d*8+g = positions / seg_cap.
+  // min(seg_count[seg_cursor_index(seg_parts, g, d)] - offset, chunk) of it, segment d*8+g =
+  // positions / seg_cap.
   const uint32_t *seg_count;
   uint32_t seg_parts;
   uint64_t seg_cap;
@@ -177,6 +178,8 @@ hipError_t launch_unsplit_words(const uint2 *runs, const uint32_t *ovf_runs, con
 hipError_t launch_ordered_emit(int kind, const ProbeParams &p, hipStream_t s);
 // C5 payload columns of a finished probe: out_cols[q][slot] = payload row of pos[slot], column q.
 hipError_t launch_gather_payload(const ProbeParams &p, const uint32_t *pos, hipStream_t s);
+// the gather kernel this thread's last launch_gather_payload chose (ccj_last_gather_kernel)
+const char *last_gather_kernel();
 hipError_t launch_gen_reference_keys(int64_t *out, uint64_t first, uint64_t n, uint64_t n_total, uint64_t cf,
                                      hipStream_t s);
 hipError_t launch_fill(int64_t *p, uint64_t n, int64_t v, hipStream_t s);
@@ -264,7 +267,8 @@ size_t slot_partition_workspace(uint64_t n, const SlotPlan &pl);
 hipError_t launch_slot_partition(const int64_t *keys, uint64_t n, const SlotPlan &pl, int64_t *out_keys,
                                  uint32_t *out_rows, void *ws, hipStream_t s);
 // One-pass fixed-capacity form: segment (partition d, XCD group g) = positions [(d*8+g)*cap, +cap);
-// cursors[g*parts + d] = rows that went to it (may exceed cap: CCJ_FLAG_PART_OVERFLOW raised).
+// cursors[seg_cursor_index(parts, g, d)] = rows that went to it (may exceed cap:
+// CCJ_FLAG_PART_OVERFLOW raised); the overflow cursors follow at ovf_cursor_index(parts, k).
 uint64_t slot_seg_cap(uint64_t n, const SlotPlan &pl, uint32_t chunk);
 // Exclusive prefix sums of n values (ccj_scan.hip): out[i] = in[0] + ... + in[i-1] (in may be
 // out; u32 sums wrap as the values do); *total (optional, device) = the sum of all n.  tmp:
@@ -274,6 +278,14 @@ hipError_t scan_exclusive_u64(const uint64_t *in, uint64_t *out, uint64_t n, uin
                               hipStream_t s);
 hipError_t scan_exclusive_u32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *total, void *tmp,
                               hipStream_t s);
+// Stable LSD radix sort, 8-bit digits (ccj_sort.hip, the chaining build's bucket sort): sorts by bits
+// [0, end_bit) of the keys, ping-ponging between keys/vals and keys_alt/vals_alt; *in_alt = the
+// result is in the _alt arrays.  Digits equal in every key are skipped.  tmp: radix_sort_temp_bytes(n).
+size_t radix_sort_temp_bytes(uint64_t n);
+hipError_t radix_sort_pairs_u32(uint32_t *keys, uint32_t *keys_alt, uint32_t *vals, uint32_t *vals_alt, uint64_t n,
+                                uint32_t end_bit, void *tmp, hipStream_t s, bool *in_alt);
+hipError_t radix_sort_keys_u64(uint64_t *keys, uint64_t *keys_alt, uint64_t n, void *tmp, hipStream_t s,
+                               bool *in_alt);
 // cursors[ovf_cursor_index(parts, k)] = rows put in overflow sub-area k < kOvfSubs (tile group
 // k / kOvfPerGroup) = [ovf_base + k * ovf_sub, + ovf_sub) (ovf_sub = 0: no overflow area); the last
 // 64 positions of the area [ovf_base, ovf_base + ovf_cap) are the pipelined form's sink; cursors

@@ -65,6 +65,14 @@ def _keys(case):
         k = np.concatenate([ref_keys(5000, 1), np.full(300, 1234, np.int64)])
         g.shuffle(k)
         return k
+    if case == "all_equal":  # one chain of every key: the radix sort skips every pass, max_dup = n
+        return np.full(70000, -5, np.int64)
+    if case == "wide_dups":  # keys over all 64 bits (every byte of the max_dup sort varies), dups 1..6
+        base = g.integers(-(1 << 63), (1 << 63) - 1, size=150000, dtype=np.int64)
+        k = np.repeat(base, g.integers(1, 6, size=150000))
+        k = np.concatenate([k, np.full(6, base[3], np.int64)])
+        g.shuffle(k)
+        return k
     if case == "c3_size":  # 2^22 reference keys (C3 / C4 per-GPU shape, scaled)
         return ref_keys(1 << 22, 1)
     raise ValueError(case)
@@ -91,7 +99,7 @@ def _assert_same(host_t, dev_t):
 
 
 @pytest.mark.parametrize("case", ["empty", "one", "three", "ref_cf1", "ref_cf7", "random_dups", "long_chain",
-                                  "c3_size"])
+                                  "all_equal", "wide_dups", "c3_size"])
 def test_device_chain_build_byte_identical_to_host(case):
     keys = _keys(case)
     host_t = ccj.Table.from_host(ccj.CHAIN, keys)
@@ -107,6 +115,10 @@ def test_device_chain_build_byte_identical_to_host(case):
         assert a["bucket8"] is None and host_t.max_dup == 301 and host_t.max_rounds >= 301
     if case == "random_dups":
         assert host_t.max_dup == 9
+    if case == "all_equal":
+        assert dev_t.max_dup == 70000 and dev_t.max_rounds == 70000
+    if case == "wide_dups":
+        assert dev_t.max_dup == int(np.unique(keys, return_counts=True)[1].max())
 
 
 @pytest.mark.parametrize("n,cf", [(1000, 1), (1 << 20, 1), (1 << 20, 3), (999999, 40)])
