@@ -107,6 +107,10 @@ def parse():
     ap.add_argument("--no-other", action="store_true", help="C2: do not time the other paths beside the headline")
     ap.add_argument("--no-other-workloads", action="store_true",
                     help="C2: do not run C3 and C5 after the headline (other_workloads)")
+    ap.add_argument("--no-scaling-reference", action="store_true",
+                    help="C2: do not run the multi-GPU protocol at N = 1 on the C4 per-GPU shape (scaling_reference)")
+    ap.add_argument("--no-n1-same-shape", action="store_true",
+                    help="N > 1: do not time the same per-GPU shape at N = 1 (n1_same_shape_ms)")
     ap.add_argument("--no-rows", action="store_true",
                     help="partitioned path without CCJ_PART_ROWS (the walk writes every output; A/B)")
     ap.add_argument("--lib", default="product",
@@ -258,6 +262,31 @@ def cpu_baseline(args):
     }
 
 
+def profile_traffic(workload, path, n_probe, n_build):
+    """HBM bytes per step of a path's kernels from its committed counter profile
+    (profiles/pmc_<workload>_<path>.json, tools/profile.sh + tools/prof_summary.py), used only when
+    the profile was taken on this shape AND on the build this process loaded (its csrc_hash equals
+    ccj_build_hash): a profile of an older kernel is reported as stale with traffic null."""
+    res = {"traffic": None, "kernels_ms": None, "profile": None, "profile_tag": None, "profile_csrc_hash": None,
+           "traffic_stale": None}
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{workload}_{path}.json")
+    if not os.path.exists(pmc_path):
+        return res
+    try:
+        pmc = json.load(open(pmc_path))
+    except (OSError, ValueError):
+        return res
+    res.update(profile=os.path.relpath(pmc_path, ROOT), profile_tag=pmc.get("tag"),
+               profile_csrc_hash=pmc.get("csrc_hash"))
+    if pmc.get("n_probe") != n_probe or pmc.get("n_build") != n_build:
+        return res
+    stale = pmc.get("csrc_hash") != ccj.build_hash()
+    res["traffic_stale"] = stale
+    if not stale:
+        res.update(traffic=pmc.get("hbm_bytes_per_launch"), kernels_ms=pmc.get("kernels_ms"))
+    return res
+
+
 PHASE_KERNELS = {  # which kernels sit between the phase boundaries of each path (ccj.h ccj_set_phase_events)
     "partitioned": ("slot_split_pipe (hash, home partition, keys + rows to their positions)",
                     "probe_walk2 (match + advance, fused; compacts the chunks with misses)",
@@ -277,7 +306,7 @@ def phase_report(pev, path, c5=False):
     t = [p.ms() for p in pev]
     mean = [sum(x[i] for x in t) / len(t) for i in range(3)]
     k = PHASE_KERNELS.get(path, ("?", "?", "?"))
-    gather_k = "gather_payload_cols<8> (8 payload columns, stores transposed through LDS)" if c5 else k[2]
+    gather_k = (ccj.last_gather_kernel() or "?") if c5 else k[2]
     return {"schema": "reference CycleProfiler phases (profiler.h:262-290)",
             "hash_find_bucket_ms": mean[0], "match_tuples_and_advance_pointers_ms": mean[1],
             "gather_tuples_ms": mean[2],
@@ -423,23 +452,27 @@ def bench_c3(args, dev, stream):
                                   f"{O.count_c3(SEED, 0, n_ref, n_build, 1, threads=args.cpu_threads)[0]})"),
                        "cpu_model": cpu_model()}
     n_bar, m_bar = examined / n_probe, matches / n_probe
-    alg = 8 + 8 + 8 * n_bar + 12 * m_bar  # key + off[b], off[b+1] + chain keys + (sel, payload)
-    c3_traffic = None  # DRAM bytes of the probe kernels per step (tools/profile.sh, profiles/pmc_c3_<path>.json)
-    pmc_path = os.path.join(ROOT, "profiles", f"pmc_c3_{args.path}.json")
-    if os.path.exists(pmc_path):
-        try:
-            pmc = json.load(open(pmc_path))
-            if pmc.get("n_probe") == n_probe and pmc.get("n_build") == n_build:
-                c3_traffic = pmc.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            pass
-    achieved = alg * n_probe / (probe_ms * 1e-3) / 1e9
+    # SURVEY §8(d) for chaining: 8 (probe key) + 4 (bucket offset) + 8·N̄ (chain keys visited) +
+    # 12·m̄ (u32 row id + payload per match); the step also compacts every match (NaiveCompactor,
+    # compactor.cpp:5-41): per match it reads the row id (4) and payload (8) and writes the dense
+    # u64 row (8), the carried key column (8) and the payload (8) = 36 B.  frac = those bytes over
+    # the step's kernel time, probe + compaction.
+    alg_probe = 8 + 4 + 8 * n_bar + 12 * m_bar
+    alg_compact = 36 * m_bar
+    alg = alg_probe + alg_compact
+    step_kern_ms = probe_ms + comp_ms
+    prof = profile_traffic("c3", args.path, n_probe, n_build)  # DRAM bytes of the probe kernels per step
+    c3_traffic = prof["traffic"]
+    achieved = alg * n_probe / (step_kern_ms * 1e-3) / 1e9
+    # round 5's figure (kept as frac_csr): both CSR offsets (8 B) and no compaction, over the probe alone
+    alg_csr = 8 + 8 + 8 * n_bar + 12 * m_bar
+    achieved_csr = alg_csr * n_probe / (probe_ms * 1e-3) / 1e9
     # the chain keys a walk that stops at the first match examines (distinct build keys: the
-    # partitioned walk); the bucket record counts as the offsets' 8 B
+    # partitioned walk)
     fm = part_mode and int(table.max_dup) <= 1
     n_walk = (walked if fm else examined) / n_probe
-    alg_walked = 8 + 8 + 8 * n_walk + 12 * m_bar
-    achieved_walked = alg_walked * n_probe / (probe_ms * 1e-3) / 1e9
+    alg_walked = 8 + 4 + 8 * n_walk + 12 * m_bar + alg_compact
+    achieved_walked = alg_walked * n_probe / (step_kern_ms * 1e-3) / 1e9
     line = {
         "metric": METRIC, "value": n_probe / (wall / args.steps), "unit": "probe tuples/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall * 1e3 / args.steps,
@@ -448,13 +481,23 @@ def bench_c3(args, dev, stream):
         "config": {"workload": "C3: 1xMI355X chaining_ht + compactor, Zipf-skewed keys, ~10% match rate, "
                                f"{n_build} build / {n_probe} probe, chunk={chunk}", "parallelism": "dp1"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": c3_traffic,
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "frac_basis": ("SURVEY §8(d): 8 + 4 + 8·N̄ + 12·m̄ per probe tuple, + 36·m̄ of compaction, over "
+                                    "the step's kernel time (probe + compaction)"),
+                     "traffic": c3_traffic,
+                     "traffic_scope": "DRAM bytes per step of the probe kernels (split + walk), not the compaction",
+                     "traffic_profile": prof["profile"], "traffic_profile_tag": prof["profile_tag"],
+                     "traffic_profile_csrc_hash": prof["profile_csrc_hash"], "traffic_stale": prof["traffic_stale"],
                      "traffic_GBps": c3_traffic / (probe_ms * 1e-3) / 1e9 if c3_traffic else None,
-                     "kernel": ("ccj_probe_partitioned (bucket-range split + probe_chain_filt)" if part_mode
+                     "kernel": ("ccj_probe_partitioned (bucket-range split + probe_chain_filt) + ccj_compact" if part_mode
                                 else "ccj_probe_ordered (bucket split with runs + chain_words_filt + unsplit_words + "
-                                     "emit_ordered<CHAIN>)" if args.path == "ordered"
-                                else "probe_chunks<CHAIN,2>"),
-                     "kernel_ms": probe_ms, "alg_bytes_per_tuple": alg, "chain_keys_per_tuple": n_bar,
+                                     "emit_ordered<CHAIN>) + ccj_compact" if args.path == "ordered"
+                                else "probe_chunks<CHAIN,2> + ccj_compact"),
+                     "kernel_ms": step_kern_ms, "probe_kernel_ms": probe_ms, "compaction_kernel_ms": comp_ms,
+                     "alg_bytes_per_tuple": alg, "alg_probe_bytes_per_tuple": alg_probe,
+                     "alg_compaction_bytes_per_tuple": alg_compact, "chain_keys_per_tuple": n_bar,
+                     "frac_csr": achieved_csr / HBM_PEAK_GBS,
+                     "frac_csr_basis": "8 + 8 + 8·N̄ + 12·m̄ (both CSR offsets) over the probe kernels alone (round 5's figure)",
                      "m_bar": m_bar, "frac_walked": achieved_walked / HBM_PEAK_GBS,
                      "alg_bytes_walked_per_tuple": alg_walked, "chain_keys_walked_per_tuple": n_walk,
                      "walk": "first match" if fm else "whole chain",
@@ -638,9 +681,61 @@ def main():
     if world > 1 or args.sharded:
         return bench_multi(args, world, rank, local, dev, stream, dist)
     line = bench_c3(args, dev, stream) if args.workload == "c3" else bench_single(args, dev, stream)
+    if args.workload == "c2" and not (args.no_other_workloads and args.no_scaling_reference):
+        # the headline stands on its own if a later workload takes the process down
+        log("[c2 line] " + json.dumps(line))
     if args.workload == "c2" and not args.no_other_workloads:
         line["other_workloads"] = other_workloads(args, dev, stream)
+    if args.workload == "c2" and not args.no_scaling_reference:
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        line["scaling_reference"] = same_shape_n1(args, verify=not args.no_verify)
     print(json.dumps(line), flush=True)
+
+
+def same_shape_n1(args, verify=True, steps=None, warmup=None):
+    """The multi-GPU protocol at N = 1 on the per-GPU shape of the N > 1 lines (C4: --n-build-per-gpu
+    build keys, --n-probe probe keys): owner split (one owner) + local copy + local probe, run by
+    `bench.py --sharded` in a child process (its own one-rank launcher; this process never execs).
+    The N = 1 point of the 1 -> 8 curve is THIS value, not the C2 headline: the same
+    work per GPU as every N > 1 line, so value_N / (N * value_1) is the weak-scaling efficiency."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--sharded", "--gpus", "1", "--no-cpu",
+           "--steps", str(steps or min(args.steps, 10)), "--warmup", str(warmup if warmup is not None else min(args.warmup, 2)),
+           "--n-build-per-gpu", str(args.n_build_per_gpu), "--n-probe", str(args.n_probe), "--chunk", str(args.chunk),
+           "--batches", str(args.batches), "--scaling", "weak"]
+    if args.group:
+        cmd += ["--group", str(args.group)]
+    if not verify:
+        cmd.append("--no-verify")
+    if args.lib != "product":
+        cmd += ["--lib", args.lib]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID", "GROUP_WORLD_SIZE", "ROLE_WORLD_SIZE")}
+    t0 = time.perf_counter()
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": "timed out (600 s)"}
+    ln = None
+    for t in p.stdout.splitlines():
+        t = t.strip()
+        if t.startswith("{") and '"metric"' in t:
+            try:
+                ln = json.loads(t)
+            except ValueError:
+                pass
+    if p.returncode != 0 or ln is None:
+        return {"error": f"rc {p.returncode}: {p.stderr[-400:]}"}
+    par = ln.get("parity", {})
+    return {"protocol": "bench.py --sharded at N = 1 (owner split, local copy of the own segment, local probe)",
+            "config": ln.get("config"), "ms_per_step": ln["ms_per_step"], "value": ln["value"], "unit": ln["unit"],
+            "steps": ln["steps"], "warmup": ln["warmup"], "partition_ms": ln.get("partition_ms"),
+            "exchange_ms": ln.get("exchange_ms"), "local_probe_ms": ln.get("local_probe_ms"),
+            "l1_ok": par.get("l1_ok"), "l2_ok": par.get("l2_ok"), "matches": par.get("matches"),
+            "expected_matches": par.get("expected_matches"), "wall_s": time.perf_counter() - t0,
+            "use": "the N = 1 point of the multi-GPU curve (same per-GPU work as every N > 1 line)"}
 
 
 def other_workloads(args, dev, stream):
@@ -654,7 +749,10 @@ def other_workloads(args, dev, stream):
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
         a = copy.copy(args)
-        a.workload, a.path, a.no_cpu, a.no_other = w, "partitioned", True, True
+        # C3 keeps its CPU baseline (the reference's chaining loop on 2^26 keys of the same stream,
+        # bench_c3); C5 has no reference counterpart (the reference gathers no payload columns)
+        a.workload, a.path, a.no_cpu, a.no_other = w, "partitioned", args.no_cpu or w != "c3", True
+        a.cpu_sample = min(args.cpu_sample, 1 << 28)
         a.steps, a.warmup = max(1, min(args.steps, 10)), min(args.warmup, 2)
         t0 = time.perf_counter()
         try:
@@ -665,7 +763,7 @@ def other_workloads(args, dev, stream):
         keep = {"workload": ln["config"]["workload"], "value": ln["value"], "unit": ln["unit"],
                 "ms_per_step": ln["ms_per_step"], "steps": a.steps, "warmup": a.warmup, "path": ln.get("path"),
                 "roofline": ln["roofline"], "phases": ln.get("phases"), "parity": ln["parity"],
-                "wall_s": time.perf_counter() - t0}
+                "cpu_baseline": ln.get("cpu_baseline"), "wall_s": time.perf_counter() - t0}
         if "compaction_ms" in ln:
             keep["compaction_ms"] = ln["compaction_ms"]
         res.append(keep)
@@ -850,18 +948,10 @@ def bench_single(args, dev, stream):
     walked_bytes_per_tuple = 8 + 8 * s_walk + m_bar * (12 + 16 * P)
     window_bytes_per_tuple = 8 + 32 * windows / n_probe + m_bar * (12 + 16 * P)
     achieved_walked = walked_bytes_per_tuple * n_probe / (kern_ms * 1e-3) / 1e9
-    traffic = None
-    kernels_ms = None
-    # DRAM bytes per step of THIS path's kernels, from tools/profile.sh + tools/prof_summary.py
-    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}_{args.path}.json")
-    if os.path.exists(pmc_path):
-        try:
-            pmc = json.load(open(pmc_path))
-            if pmc.get("n_probe") == n_probe and pmc.get("n_build") == n_build:
-                traffic = pmc.get("hbm_bytes_per_launch")
-                kernels_ms = pmc.get("kernels_ms")
-        except (OSError, ValueError):
-            pass
+    # DRAM bytes per step of THIS path's kernels, from tools/profile.sh + tools/prof_summary.py (null
+    # unless the profile was taken on this build: profile_traffic)
+    prof = profile_traffic(args.workload, args.path, n_probe, n_build)
+    traffic, kernels_ms = prof["traffic"], prof["kernels_ms"]
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and not c5:  # the reference has no payload gather
@@ -884,6 +974,9 @@ def bench_single(args, dev, stream):
             "hbm_gbs_algorithmic": achieved,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_profile": prof["profile"], "traffic_profile_tag": prof["profile_tag"],
+                         "traffic_profile_csrc_hash": prof["profile_csrc_hash"],
+                         "traffic_stale": prof["traffic_stale"],
                          # measured DRAM bytes (whole 128-B lines per random slot read) per second
                          "traffic_GBps": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
                          "kernel": (("ccj_probe_partitioned, CCJ_PART_ROWS (slot_split_pipe writing keys + rows, "
@@ -892,6 +985,7 @@ def bench_single(args, dev, stream):
                                     ("ccj_probe_partitioned (slot_split_pipe + probe_win<3> with positions + "
                                      "gather_payload_cols<8>)") if c5 and args.path == "partitioned" else
                                     "probe_chunks<LP,2> + gather_payload_cols<8>" if c5 else PATH_KERNELS[args.path]),
+                         "gather_kernel_run": ccj.last_gather_kernel() if c5 else None,
                          "kernel_ms": kern_ms, "rocprof_kernels_ms": kernels_ms,
                          "alg_bytes_per_tuple": alg_bytes_per_tuple, "s_bar": s_bar, "m_bar": m_bar,
                          # the same step on the bytes its walk reads: slot words through the first
@@ -1069,8 +1163,23 @@ def bench_multi(args, world, rank, local, dev, stream, dist):
             "cpu_baseline": None,
             "parity": parity,
         }
-        print(json.dumps(line), flush=True)
     dist.destroy_process_group()
+    if rank == 0:
+        if world > 1 and ops is None and not args.no_n1_same_shape:
+            # the N = 1 point of this line's curve: the same per-GPU shape through the same protocol
+            # (a child process on this rank's GPU, after the other ranks are done with theirs)
+            torch.cuda.synchronize()
+            del sp, keys
+            torch.cuda.empty_cache()
+            a1 = argparse.Namespace(**vars(args))
+            if args.scaling == "strong":
+                a1.n_probe = n_probe  # per-GPU probe keys of this line
+            ref = same_shape_n1(a1, verify=False)
+            line["n1_same_shape"] = ref
+            line["n1_same_shape_ms"] = ref.get("ms_per_step")
+            if ref.get("value"):
+                line["per_gpu_value_vs_n1_same_shape"] = value / world / ref["value"]
+        print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

@@ -30,6 +30,7 @@ PART_RANK = 4  # the rank walk (LDS window index; libccj_tuning.so only) instead
 PART_SHARE = 8  # the split leaves 1/4 of the CUs to other streams (ccj.h CCJ_PART_SHARE; multi-GPU step)
 
 _lib = None
+ABI_VERSION = 15  # include/ccj.h CCJ_ABI_VERSION this binding is written against
 
 
 class CCJError(RuntimeError):
@@ -80,7 +81,8 @@ EXPORTS = ["ccj_last_error", "ccj_abi_version", "ccj_device_init", "ccj_table_bu
            "ccj_partition_grouped_workspace_size", "ccj_partition_by_owner_grouped", "ccj_partition_grouped_sub_cap",
            "ccj_probe_ordered_workspace_size", "ccj_probe_ordered", "ccj_probe_visits",
            "ccj_stream_create_cu_masked", "ccj_stream_destroy", "ccj_device_cus", "ccj_copy_device",
-           "ccj_table_get_arrays", "ccj_probe_cost_walk", "ccj_set_phase_events"]
+           "ccj_table_get_arrays", "ccj_probe_cost_walk", "ccj_set_phase_events", "ccj_build_hash",
+           "ccj_last_gather_kernel"]
 
 MAX_JOINS = 8
 COMPACT_NONE, COMPACT_FULL = 0, 1
@@ -108,6 +110,11 @@ def lib():
         vp, u64, i32 = C.c_void_p, C.c_uint64, C.c_int
         L.ccj_last_error.restype = C.c_char_p
         L.ccj_abi_version.restype = i32
+        if L.ccj_abi_version() != ABI_VERSION:  # a stale build would shift every later argument
+            raise CCJError(f"{LIB_PATH} has ABI {L.ccj_abi_version()}, this binding needs {ABI_VERSION}: "
+                           f"rebuild it (`make -C {HERE}`)")
+        L.ccj_build_hash.restype = C.c_char_p
+        L.ccj_last_gather_kernel.restype = C.c_char_p
         L.ccj_device_init.argtypes = [i32]
         L.ccj_table_build_reference.argtypes = [i32, u64, u64, i32, vp, C.POINTER(vp)]
         L.ccj_table_build_from_host.argtypes = [i32, vp, u64, C.POINTER(vp)]
@@ -161,6 +168,29 @@ def lib():
         L.ccj_copy_device.argtypes = [vp, vp, u64, vp]
         _lib = L
     return _lib
+
+
+def source_hash() -> str:
+    """The build hash (Makefile SRC_HASH) of the sources in this tree: SHA-256 of csrc/*.hip and
+    csrc/*.h in sorted path order, then include/ccj.h, as 16 hex digits."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(HERE, "csrc", "*.hip")) + glob.glob(os.path.join(HERE, "csrc", "*.h")))
+    for f in files + [os.path.join(HERE, "..", "include", "ccj.h")]:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_hash() -> str:
+    """The build hash compiled into the loaded library (ccj_build_hash)."""
+    return lib().ccj_build_hash().decode()
+
+
+def last_gather_kernel() -> str:
+    """The payload-gather kernel this thread's last probe with payload columns ran."""
+    return lib().ccj_last_gather_kernel().decode()
 
 
 def check(rc: int, what: str):

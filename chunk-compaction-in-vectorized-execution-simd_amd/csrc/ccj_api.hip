@@ -449,6 +449,13 @@ int ccj_set_phase_events(void *const *events, uint32_t n) {
 
 int ccj_abi_version(void) { return CCJ_ABI_VERSION; }
 
+#ifndef CCJ_SRC_HASH
+#define CCJ_SRC_HASH "unknown"
+#endif
+const char *ccj_build_hash(void) { return CCJ_SRC_HASH; }
+
+const char *ccj_last_gather_kernel(void) { return ccj::last_gather_kernel(); }
+
 int ccj_device_init(int device) {
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);

@@ -1539,7 +1539,9 @@ __device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *
       typedef long long i64x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
       for (int j = 0; j < (int)kJ; j += 2) {
-        const uint32_t i = u0 + urow(j);  // even; row i + 1 is inside the unit's 256 positions
+        // even; row i + 1 is inside the unit's 256 positions; chunk is a multiple of kFiltUnit, so
+        // the pair is 16-byte aligned (chain_filt_applies)
+        const uint32_t i = u0 + urow(j);
         const i64x2 v = __builtin_nontemporal_load(reinterpret_cast<const i64x2 *>(p.keys + kc * chunk + (i < uend ? i : u0)));
         kk[j] = v.x;
         kk[j + 1] = v.y;
@@ -1917,6 +1919,17 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// A pair of consecutive keys (rows i, i + 1, i even) for the walks' staging: one 16-byte load when
+// the pair is 16-byte aligned (an even chunk: every chunk base of the partitioned workspace is),
+// else two 8-byte loads (odd chunks; a16 is wave-uniform, so this is a scalar branch).  Row i + 1
+// may lie past the chunk's live rows (the caller discards it): an aligned pair never leaves the
+// 16-byte granule of row i, so it stays inside the key array's allocation.
+typedef long long key_pair_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ key_pair_t load_key_pair(const int64_t *q, bool a16) {
+  if (a16) return __builtin_nontemporal_load(reinterpret_cast<const key_pair_t *>(q));
+  return key_pair_t{__builtin_nontemporal_load(q), __builtin_nontemporal_load(q + 1)};
+}
+
 template <uint32_t kWaveRows, bool HOME, typename SM>
 __device__ __forceinline__ void walk_stage(const ProbeParams &p, SM &sm, uint64_t base, uint32_t w0,
                                            uint32_t wend, uint32_t lane) {
@@ -1926,10 +1939,11 @@ __device__ __forceinline__ void walk_stage(const ProbeParams &p, SM &sm, uint64_
   constexpr int kH = (int)(kWaveRows / (2 * kWave));
   static_assert(kWaveRows % (2 * kWave) == 0, "pairs of rows per lane");
   i64x2 v[kH];
+  const bool a16 = ((uintptr_t)(p.keys + base) & 15u) == 0u;
 #pragma unroll
   for (int j = 0; j < kH; ++j) {
     const uint32_t i = w0 + (uint32_t)j * 2u * kWave + 2u * lane;
-    v[j] = i < wend ? __builtin_nontemporal_load(reinterpret_cast<const i64x2 *>(p.keys + base + i)) : i64x2{0, 0};
+    v[j] = i < wend ? load_key_pair(p.keys + base + i, a16) : i64x2{0, 0};
     if (i + 1 >= wend) v[j].y = 0;
   }
 #pragma unroll
@@ -2693,11 +2707,11 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
   if (p.key_aux == 0u) {
 #endif
     typedef long long i64x2 __attribute__((ext_vector_type(2)));
+    const bool a16 = ((uintptr_t)(p.keys + base) & 15u) == 0u;
 #pragma unroll
     for (int j = 0; j < kJ; j += 2) {
       const uint32_t i = row_of(j);  // even: the pair (i, i + 1) lies inside the wave's 512 rows
-      const i64x2 v = i < wend ? __builtin_nontemporal_load(reinterpret_cast<const i64x2 *>(p.keys + base + i))
-                               : i64x2{0, 0};
+      const i64x2 v = i < wend ? load_key_pair(p.keys + base + i, a16) : i64x2{0, 0};
       k[j] = v.x;
       k[j + 1] = i + 1 < wend ? v.y : 0;
     }
@@ -3392,6 +3406,8 @@ __global__ __launch_bounds__(256) void gather_payload_cols(GatherParams g) {
   }
 }
 
+thread_local const char *t_gather_kernel = "";
+
 template <int NP>
 hipError_t launch_gather_np(const GatherParams &g, uint64_t n_chunks, hipStream_t s) {
   const bool vec = (g.stride % 2 == 0) && ((uintptr_t)g.pay % 16 == 0);
@@ -3413,13 +3429,22 @@ hipError_t launch_gather_np(const GatherParams &g, uint64_t n_chunks, hipStream_
     else
 #endif
     hipLaunchKernelGGL(gather_payload_cols<8>, dim3((unsigned)n_chunks), dim3(256), 0, s, g);
+    t_gather_kernel = "gather_payload_cols<8> (stores transposed through LDS)";
+  } else if (NP == 8 && vec) {
+    hipLaunchKernelGGL((gather_payload_quad<4>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
+    t_gather_kernel = "gather_payload_quad<4> (16-byte row pieces, column-unaligned fallback)";
+  } else if (vec) {
+    hipLaunchKernelGGL((gather_payload<NP, true>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
+    t_gather_kernel = "gather_payload<NP, vec> (16-byte row loads)";
+  } else {
+    hipLaunchKernelGGL((gather_payload<NP, false>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
+    t_gather_kernel = "gather_payload<NP, scalar> (8-byte loads)";
   }
-  else if (NP == 8 && vec) hipLaunchKernelGGL((gather_payload_quad<4>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
-  else if (vec) hipLaunchKernelGGL((gather_payload<NP, true>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
-  else hipLaunchKernelGGL((gather_payload<NP, false>), dim3((unsigned)n_chunks), dim3(256), 0, s, g);
   return hipGetLastError();
 }
 }  // namespace
+
+const char *last_gather_kernel() { return t_gather_kernel; }
 
 hipError_t launch_gather_payload(const ProbeParams &p, const uint32_t *pos, hipStream_t s) {
   GatherParams g{};

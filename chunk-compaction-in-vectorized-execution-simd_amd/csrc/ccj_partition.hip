@@ -235,7 +235,8 @@ hipError_t launch_partition_fixed(const int64_t *keys, uint64_t n, uint32_t part
 }
 
 namespace {
-// cursors[g * parts + d] (u32, group-major) -> counts[d * 8 + g] (u64, destination-major)
+// cursors[seg_cursor_index(parts, g, d)] (u32, group-major, group stride max(parts, 32)) ->
+// counts[d * 8 + g] (u64, destination-major)
 __global__ void grouped_counts(const uint32_t *cur, uint32_t parts, uint64_t *out) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < parts * 8) out[i] = cur[seg_cursor_index(parts, i % 8, i / 8)];
@@ -1047,6 +1048,9 @@ hipError_t launch_slot_split_fixed(const int64_t *keys, uint64_t n, const SlotPl
   if ((ovf_cap >= 128 || sink) && ccj_tune_int("CCJ_SPLIT_PIPE", 1)) {
     // (the kOvfSubs overflow sub-areas of ovf_sub positions end at least 64 positions before the area's end)
     const uint64_t oc = ovf_sub;
+    // only the <= 64-partition instantiation (the owner split's) maps the own rank's partition last
+    // (dest_of); refuse self_last for any other route rather than ignore it
+    if (self_last < parts && (runs || parts > 64 || per != kSplitPer)) return hipErrorInvalidValue;
     int64_t *sink_k = sink ? (int64_t *)sink : out_keys + ovf_base + ovf_cap - 64;
     uint32_t *sink_r = sink ? (uint32_t *)((char *)sink + kSplitSinkBytes / 16 * 8) : out_rows + ovf_base + ovf_cap - 64;
 #define CCJ_PIPE_LAUNCH(C, MAXP, P)                                                                                   \

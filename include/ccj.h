@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CCJ_ABI_VERSION 14  /* 14: ccj_partition_by_owner_grouped's self_last (the own rank's segment last); 13: ccj_compact_args.key_cols, per-XCD overflow sub-areas of the partitioned layout; 12: chaining tables built on the device (stable bucket sort), ccj_table_get_arrays; 11: the rank walk in the tuning build only; 10: CCJ_PART_ROWS with positions / payload columns; 9: CCJ_PART_SHARE, CU-masked streams; 8: CCJ_PART_RANK; 7: CCJ_PART_ROWS */
+#define CCJ_ABI_VERSION 15  /* 15: ccj_build_hash, ccj_last_gather_kernel; 14: ccj_partition_by_owner_grouped's self_last (the own rank's segment last); 13: ccj_compact_args.key_cols, per-XCD overflow sub-areas of the partitioned layout; 12: chaining tables built on the device (stable bucket sort), ccj_table_get_arrays; 11: the rank walk in the tuning build only; 10: CCJ_PART_ROWS with positions / payload columns; 9: CCJ_PART_SHARE, CU-masked streams; 8: CCJ_PART_RANK; 7: CCJ_PART_ROWS */
 
 enum ccj_status {
   CCJ_OK = 0,
@@ -85,6 +85,14 @@ typedef struct ccj_table_info {
 /* ---- device / errors ---------------------------------------------------------------------- */
 const char *ccj_last_error(void);
 int ccj_abi_version(void);
+/* 16 hex digits of the SHA-256 of the sources this library was compiled from (the .hip and .h files of csrc,
+ * include/ccj.h, in that order; Makefile SRC_HASH): bench.py uses it to refuse a counter profile
+ * taken on another build.  No reference counterpart (build bookkeeping). */
+const char *ccj_build_hash(void);
+/* Name of the payload-gather kernel the calling thread's last probe with payload columns launched
+ * ("" if none): the vectorised transposed-store form needs an even cap, no out_base and 16-byte
+ * aligned columns, else a fallback runs.  No reference counterpart (the reference has no gather). */
+const char *ccj_last_gather_kernel(void);
 /* Phase timing in the reference's 4-phase schema (CycleProfiler, profiler.h:262-290: 0 "Hash & Find
  * Bucket", 1 "Match Tuples", 2 "Gather Tuples", 3 "Advance Pointers"): the caller's hipEvent_t
  * handles (n <= 4; NULL / 0 clears), recorded on the call's stream by this thread's later probe

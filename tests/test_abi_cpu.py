@@ -27,7 +27,15 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert ccj.lib().ccj_abi_version() == 14
+    assert ccj.lib().ccj_abi_version() == ccj.ABI_VERSION == 15
+
+
+def test_build_hash_matches_the_tree():
+    """The library was built from the sources in this tree (ccj_build_hash == the hash of csrc/ and
+    include/ccj.h): bench.py relies on it to tell a counter profile of this build from a stale one."""
+    h = ccj.build_hash()
+    assert len(h) == 16 and int(h, 16) >= 0
+    assert h == ccj.source_hash()
 
 
 def test_fails_loudly_without_device():

@@ -27,7 +27,7 @@ def run_bench(*extra):
 
 
 def test_bench_c2_with_other_paths():
-    line = run_bench()
+    line = run_bench("--n-build-per-gpu", str(1 << 21))
     par = line["parity"]
     assert par["status_flags"] == 0 and par["l1_ok"] and par["l2_ok"]
     paths = {o["path"]: o for o in line["other_paths"]}
@@ -43,11 +43,23 @@ def test_bench_c2_with_other_paths():
         assert o["parity"]["status_flags"] == 0 and o["parity"]["l1_ok"] and o["parity"]["l2_ok"]
     assert ow["C3"]["parity"]["compaction_keeps_all"] and ow["C3"]["compaction_ms"] > 0
     assert ow["C5"]["parity"]["payload_cols_ok"]
+    # C3's frac on SURVEY §8(d)'s bytes over probe + compaction; round 5's figure kept beside it
+    r3 = ow["C3"]["roofline"]
+    assert r3["frac_csr"] > 0 and r3["kernel_ms"] == pytest.approx(r3["probe_kernel_ms"] + r3["compaction_kernel_ms"])
+    assert r3["alg_probe_bytes_per_tuple"] == pytest.approx(8 + 4 + 8 * r3["chain_keys_per_tuple"] + 12 * r3["m_bar"])
+    # the gather kernel that actually ran, and no traffic pasted from a profile of another shape / build
+    assert ow["C5"]["roofline"]["gather_kernel_run"].startswith("gather_payload_cols<8>")
+    for r in (line["roofline"], r3, ow["C5"]["roofline"]):
+        assert r["traffic"] is None or r["traffic_stale"] is False
+    # the multi-GPU protocol at N = 1 on the C4 per-GPU shape: the N = 1 point of the curve
+    sr = line["scaling_reference"]
+    assert sr["ms_per_step"] > 0 and sr["l1_ok"] and sr["l2_ok"], sr
+    assert sr["config"]["n_build_total"] == 1 << 21 and sr["config"]["n_probe_per_gpu"] == 1 << 24
 
 
 def test_bench_c2_tuning_build_with_rank_ab():
     """--lib tuning: the same line, with the rank walk (tuning build only) timed beside the headline."""
-    line = run_bench("--lib", "tuning", "--no-other-workloads")
+    line = run_bench("--lib", "tuning", "--no-other-workloads", "--no-scaling-reference")
     par = line["parity"]
     assert par["status_flags"] == 0 and par["l1_ok"] and par["l2_ok"]
     paths = {o["path"]: o for o in line["other_paths"]}
@@ -58,7 +70,7 @@ def test_bench_c2_tuning_build_with_rank_ab():
 
 
 def test_bench_c2_ordered_headline():
-    line = run_bench("--path", "ordered", "--no-other", "--no-other-workloads")
+    line = run_bench("--path", "ordered", "--no-other", "--no-other-workloads", "--no-scaling-reference")
     assert line["path"] == "ordered" and line["parity"]["l1_ok"] and line["parity"]["l2_ok"]
 
 

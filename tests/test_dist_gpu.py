@@ -242,7 +242,8 @@ def test_bench_multi_rank_on_one_gpu(world, scaling):
     env["OMP_NUM_THREADS"] = "2"
     p = subprocess.run([sys.executable, "bench.py", "--gpus", str(world), "--backend", "gloo", "--same-device",
                         "--steps", "2", "--warmup", "1", "--no-cpu", "--n-build-per-gpu", str(1 << 19),
-                        "--n-probe", str(3 << 20), "--batches", "3", "--group", "2", "--scaling", scaling],
+                        "--n-probe", str(3 << 20), "--batches", "3", "--group", "2", "--scaling", scaling]
+                       + (["--no-n1-same-shape"] if world == 8 else []),
                        cwd=root, capture_output=True, text=True, timeout=600, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
@@ -253,3 +254,9 @@ def test_bench_multi_rank_on_one_gpu(world, scaling):
     assert line["parity"]["l1_ok"] and line["parity"]["l2_ok"], line["parity"]
     assert line["parity"]["exact_size_fallback_steps"] == 0
     assert line["xgmi_bytes_per_step"] > 0 and line["local_probe_ms"] > 0
+    if world == 2:  # the curve's N = 1 point: the same per-GPU shape through the one-rank protocol
+        ref = line["n1_same_shape"]
+        assert line["n1_same_shape_ms"] == ref["ms_per_step"] > 0, ref
+        assert ref["config"]["n_probe_per_gpu"] == line["config"]["n_probe_per_gpu"]
+        assert ref["config"]["n_build_total"] == line["config"]["n_build_total"] // world
+        assert line["per_gpu_value_vs_n1_same_shape"] > 0

@@ -62,3 +62,15 @@ def test_walk_dpp_address_checks_on_the_tuning_build():
                        timeout=900)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-2000:]
     assert " passed" in p.stdout and "failed" not in p.stdout
+
+
+def test_every_timing_ablation_runs_clean_on_the_tuning_build():
+    """tests/ablation_checks.py: each timing-only ablation bit of the tuning build (CCJ_ABLATE,
+    CCJ_OWNER_ABLATE, CCJ_GATHER_ABLATE) once on every path that reads it, small sizes, one child
+    process: no fault, only defined status flags, and clean runs afterwards."""
+    assert os.path.exists(TUNING), "libccj_tuning.so missing: make -C chunk-compaction-in-vectorized-execution-simd_amd"
+    env = dict(os.environ, CCJ_LIB_PATH=TUNING)
+    p = subprocess.run([sys.executable, "-m", "pytest", os.path.join(ROOT, "tests", "ablation_checks.py"), "-q", "-x",
+                        "-p", "no:cacheprovider"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-2000:]
+    assert " passed" in p.stdout and "failed" not in p.stdout

@@ -21,7 +21,7 @@ for ((r = 0; r < REPS; r++)); do
     case $WL in
       c3split) env $envs timeout -k 10 200 python -u tools/exp_split_c3.py --lib "$lib" c3 > "$log" 2>&1 || exit 1
                grep split "$log" | sed "s|^|$v |" >> "gpurun_out/${TAG}_all.log" ;;
-      *) args="--no-cpu --no-other --no-other-workloads --no-verify --steps 10 --warmup 3"
+      *) args="--no-cpu --no-other --no-other-workloads --no-scaling-reference --no-verify --steps 10 --warmup 3"
          case $WL in c2ord) args="$args --path ordered" ;; c3) args="$args --workload c3" ;; c5) args="$args --workload c5" ;; esac
          env $envs timeout -k 10 200 python -u bench.py --lib "$lib" $args > "$log" 2>&1 || exit 1
          python3 - "$log" "$v" >> "gpurun_out/${TAG}_all.log" <<'PY' || exit 1

@@ -52,7 +52,9 @@ def main():
             for r in csv.DictReader(f):
                 pmc[r["Kernel_Name"]][r["Counter_Name"]] = float(r["Counter_Value"])
                 pmc[r["Kernel_Name"]]["VGPR_Count"] = int(r["VGPR_Count"])
-    out = {"tag": a.tag, "kernel_stats": stats, "pmc": pmc}
+    hp = os.path.join(src, "build_hash.txt")  # tools/profile.sh: ccj_build_hash of the profiled library
+    csrc_hash = open(hp).read().strip() if os.path.exists(hp) else None
+    out = {"tag": a.tag, "csrc_hash": csrc_hash, "kernel_stats": stats, "pmc": pmc}
     names = a.kernel.split(",")
     per = {}
     for name in names:
@@ -79,7 +81,7 @@ def main():
                           "bytes_per_probe_tuple": traffic / a.n_probe,
                           "hbm_GBps": traffic / avg_ns if avg_ns else None}
         with open(os.path.join(dst, f"pmc_{a.workload}_{a.path}.json"), "w") as f:
-            json.dump({"tag": a.tag, "kernels": names, "n_probe": a.n_probe, "n_build": a.n_build,
+            json.dump({"tag": a.tag, "csrc_hash": csrc_hash, "kernels": names, "n_probe": a.n_probe, "n_build": a.n_build,
                        "hbm_bytes_per_launch": traffic, "kernels_ms": {n: v["avg_ns"] / 1e6 if v["avg_ns"] else None
                                                                     for n, v in per.items()},
                        "per_kernel": per, "kernels_avg_ns_sum": avg_ns}, f, indent=1)

@@ -10,6 +10,8 @@ cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
+# the build the counters belong to (ccj_build_hash; bench.py refuses the traffic of another build)
+python3 -c "import sys; sys.path.insert(0, 'chunk-compaction-in-vectorized-execution-simd_amd'); import ccj; print(ccj.build_hash())" > "$OUT/build_hash.txt" || exit 1
 echo "[profile] kernel trace: bench.py $ARGS"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -f csv -d "$OUT/kt" -o kt -- python3 bench.py $ARGS > "$OUT/kt_bench.log" 2>&1 || exit $?
 for grp in FETCH_SIZE WRITE_SIZE "TCC_REQ_sum TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" \
