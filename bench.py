@@ -980,7 +980,8 @@ def bench_single(args, dev, stream):
                          # measured DRAM bytes (whole 128-B lines per random slot read) per second
                          "traffic_GBps": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
                          "kernel": (("ccj_probe_partitioned, CCJ_PART_ROWS (slot_split_pipe writing keys + rows, "
-                                     "probe_walk2<POS> writing match positions, gather_payload_cols<8>)") if c5 and
+                                     "probe_walk2<POS> writing each chunk's matches by payload slab, "
+                                     + ccj.last_gather_kernel() + ")") if c5 and
                                     args.path == "partitioned" and rows_mode else
                                     ("ccj_probe_partitioned (slot_split_pipe + probe_win<3> with positions + "
                                      "gather_payload_cols<8>)") if c5 and args.path == "partitioned" else

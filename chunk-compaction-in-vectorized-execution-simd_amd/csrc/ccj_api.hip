@@ -665,19 +665,33 @@ uint64_t ccj_probe_partitioned_positions(const ccj_table *t, uint64_t n_rows, ui
   return part_layout(t, n_rows, chunk).positions;
 }
 
-size_t ccj_probe_partitioned_workspace_size(const ccj_table *t, uint64_t n_rows, uint32_t chunk) {
-  if (!t) return 0;
-  const PartLayout L = part_layout(t, n_rows, chunk);
-  // partitioned keys (positions) + the fixed split's cursors, or the exact split's pass scratch
+namespace {
+// The partitioned probe's workspace without the C5 sub-range starts (part_ws_sub_bytes), which
+// follow it: partitioned keys (positions) + the fixed split's cursors, or the exact split's pass
+// scratch, + the rank walk's per-block hit masks, hit counts and partition counters.
+size_t part_ws_base_bytes(const ccj_table *t, const PartLayout &L, uint64_t n_rows) {
   const size_t fixed = align256(ccj::split_cursor_count(L.parts) * 4);
   const size_t exact = ccj::slot_partition_workspace(n_rows, L.pl);
-  // + the rank walk's per-block hit masks, hit counts and partition counters
 #ifdef CCJ_RANK_WALK
   const size_t rank = t->d_ckeys && L.pl.lo_bits ? ccj::rank_workspace(L.positions, L.parts) : 0;
 #else
   const size_t rank = 0;
+  (void)t;
 #endif
   return align256(L.positions * 8) + align256(fixed > exact ? fixed : exact) + rank;
+}
+// 8 u32 sub-range starts per output chunk (walk_emit_pos_sub), for tables with payload columns
+size_t part_ws_sub_bytes(const ccj_table *t, const PartLayout &L, uint32_t chunk) {
+  if (!t->n_pay || !L.pl.lo_bits) return 0;
+  const uint64_t out_chunks = (L.positions + chunk - 1) / chunk;
+  return align256(out_chunks * 8 * 4);
+}
+}  // namespace
+
+size_t ccj_probe_partitioned_workspace_size(const ccj_table *t, uint64_t n_rows, uint32_t chunk) {
+  if (!t) return 0;
+  const PartLayout L = part_layout(t, n_rows, chunk);
+  return part_ws_base_bytes(t, L, n_rows) + part_ws_sub_bytes(t, L, chunk);
 }
 
 int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t flags, uint32_t *out_row_map,
@@ -711,9 +725,10 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
     return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: CCJ_PART_ROWS needs an LP table of >= 16 slots with distinct "
                                  "keys, cap == chunk, out_payload (with positions / payload columns: <= 2^31 slots)");
   if (a->n_rows == 0) return CCJ_OK;
-  if ((!out_row_map && !rows) || !ws || ws_bytes < ccj_probe_partitioned_workspace_size(t, a->n_rows, a->chunk))
-    return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: missing row map or workspace too small");
   const PartLayout L = part_layout(t, a->n_rows, a->chunk);
+  const size_t ws_base = part_ws_base_bytes(t, L, a->n_rows);
+  if ((!out_row_map && !rows) || !ws || ws_bytes < ws_base)
+    return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: missing row map or workspace too small");
   const bool exact = (flags & CCJ_PART_EXACT) != 0;
   if (L.pl.lo_bits && !exact && !a->status)
     return fail(CCJ_ERR_INVALID, "ccj_probe_partitioned: the fixed-capacity split needs args->status");
@@ -832,9 +847,24 @@ int ccj_probe_partitioned(const ccj_table *t, const ccj_probe_args *a, uint32_t 
   ccj::ProbeParams q = p;
   q.out_pos = pos;
   q.n_pay = 0;
+  // Slab order (round 6): the walk writes each chunk's matches by sub-range of their slot — 8 per
+  // partition window, a 4 MiB slab of payload rows at C5 — and the gather takes one slab per XCD at
+  // a time, so the rows it reads stay in that XCD's L2.  Where the 16-byte column form applies:
+  // rows mode, the fixed split's segments (>= 8 partitions, one XCD's range each), 8 columns,
+  // unpacked even-capacity outputs, and the workspace holds the sub-range starts.
+  bool sub = rows && !exact && L.pl.lo_bits && L.parts >= 8 && L.parts % 8 == 0 && L.pl.window_bits >= 3 &&
+             p.n_pay == 8 && p.cap % 2 == 0 && !p.out_base && t->n_pay % 2 == 0 && (uintptr_t)t->d_pay % 16 == 0 &&
+             ws_bytes >= ws_base + part_ws_sub_bytes(t, L, a->chunk) && ccj_tune_int("CCJ_GATHER_SUB", 1);
+  for (uint32_t c = 0; c < p.n_pay; ++c) sub = sub && (uintptr_t)p.out_cols[c] % 16 == 0;
+  if (sub) {
+    q.out_sub = p.out_sub = (uint32_t *)((char *)ws + ws_base);
+    q.sub_shift = p.sub_shift = L.pl.window_bits - 3;
+  }
   hipError_t e = ccj::launch_probe_flat(t->info.kind, q, s);
   phase_mark(s, 2);
-  if (e == hipSuccess) e = ccj::launch_gather_payload(p, pos, s);
+  if (e == hipSuccess)
+    e = sub ? ccj::launch_gather_payload(p, pos, s, L.parts, L.seg_cap / a->chunk * 8)
+            : ccj::launch_gather_payload(p, pos, s);
   phase_mark(s, 3);
   if (!p.out_pos) (void)hipFreeAsync(pos, s);
   HIP_TRY(e, "partitioned probe + payload gather launch");

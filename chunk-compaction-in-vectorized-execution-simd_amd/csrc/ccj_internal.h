@@ -158,6 +158,12 @@ struct ProbeParams {
   // in LDS; NULL: probe_chain_win
   const uint32_t *filt;
   uint32_t filt_wb;
+  // C5 under CCJ_PART_ROWS (walk_emit_pos_sub): each chunk's matches written in order of their slot's
+  // sub-range (slot >> sub_shift) & 7 — 8 sub-ranges of a partition's window, each a 4 MiB slab of
+  // payload rows at C5 — with out_sub[c * 8 + s] = where sub-range s starts in chunk c, so the payload
+  // gather can take one slab of every chunk of a partition at a time (NULL: row order)
+  uint32_t *out_sub;
+  uint32_t sub_shift;
 };
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 constexpr uint32_t kEmitWave = 0xFFFFFFFFu;
@@ -177,7 +183,12 @@ hipError_t launch_unsplit_words(const uint2 *runs, const uint32_t *ovf_runs, con
                                 uint32_t *status, hipStream_t s, bool w16);
 hipError_t launch_ordered_emit(int kind, const ProbeParams &p, hipStream_t s);
 // C5 payload columns of a finished probe: out_cols[q][slot] = payload row of pos[slot], column q.
-hipError_t launch_gather_payload(const ProbeParams &p, const uint32_t *pos, hipStream_t s);
+// With p.out_sub (the walk's sub-range order, 8 columns): the partitioned layout's chunks are taken
+// slab by slab — XCD x, partition d of its range, sub-range s, a group of the partition's chunks —
+// so that the slab's payload rows stay in that XCD's L2 (parts partitions of cpp chunks each, the
+// overflow area's chunks after them in plain order).
+hipError_t launch_gather_payload(const ProbeParams &p, const uint32_t *pos, hipStream_t s, uint32_t parts = 0,
+                                 uint64_t cpp = 0);
 // the gather kernel this thread's last launch_gather_payload chose (ccj_last_gather_kernel)
 const char *last_gather_kernel();
 hipError_t launch_gen_reference_keys(int64_t *out, uint64_t first, uint64_t n, uint64_t n_total, uint64_t cf,

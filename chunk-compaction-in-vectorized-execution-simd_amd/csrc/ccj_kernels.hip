@@ -2467,6 +2467,119 @@ __device__ __forceinline__ void walk_emit_pos(const ProbeParams &p, SM &sm, uint
   emit_wg_stores<2, kWave * NW>(p, sm, obase, tot, true);
   if (threadIdx.x == 0) sm.total = tot;
 }
+// walk_emit_pos with p.out_sub (C5, round 6): every chunk's matches written in order of their slot's
+// sub-range b = (slot >> sub_shift) & 7 (then row order), so the payload gather can take one 4 MiB
+// slab of payload rows per XCD at a time (launch_gather_payload).  The output order inside a chunk
+// is free on the partitioned path (L1 / L2), so this is a permutation of what walk_emit_pos writes:
+// the rows the split stored at the chunk's output slots, the keys staged in LDS and the slots are
+// placed in LDS in (sub-range, wave, row group, lane) order — ranks from 8 ballots per row group, a
+// per-wave running count per sub-range, the waves' counts through LDS — and written with 16-byte
+// stores (sel, payload, pos: 16 B per match instead of the 4 B of positions alone); out_sub[c * 8 + b]
+// = where sub-range b starts.  LDS: the idle DMA ring holds the per-wave counts, then the slots.
+// The rows the split stored at a chunk's output slots, in walk_emit_pos_sub's mapping (row
+// w0 + 64 j + lane): loaded while the walk runs, so the emit does not wait on them.
+template <int kJ>
+__device__ __forceinline__ void load_emit_rows(const ProbeParams &p, uint64_t c, uint32_t w0, uint32_t wend,
+                                               uint32_t lane, uint32_t (&rid)[kJ]) {
+  const uint32_t *sel_c = p.out_sel + c * p.cap;  // (a uniform base: 32-bit lane offsets)
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) {  // (a dead row reads slot 0)
+    const uint32_t i = w0 + (uint32_t)j * kWave + lane;
+    rid[j] = sel_c[i < wend ? i : 0u];
+  }
+}
+template <uint32_t kWaveRows, int NW, typename SM>
+__device__ __forceinline__ void walk_emit_pos_sub(const ProbeParams &p, SM &sm, uint64_t c, uint32_t w0,
+                                                  uint32_t wend, uint32_t lane, uint32_t wave,
+                                                  const uint32_t (&rid)[kWaveRows / kWave]) {
+  constexpr int kJ = (int)(kWaveRows / kWave);
+  constexpr uint32_t kSubs = 8;
+  static_assert(sizeof(sm.ring) >= kMaxChunk * 4, "the ring holds the chunk's slots");
+  const uint64_t obase = c * p.cap;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  // LDS beside the slots' first half: per wave and sub-range a running count, then the offsets and
+  // the chunk's total
+  uint32_t *s_cnt = reinterpret_cast<uint32_t *>(sm.ring + kMaxChunk * 2);  // [NW][8]
+  uint32_t *s_off = s_cnt + NW * kSubs;                                     // [NW][8], then the total
+  if (lane < kSubs) s_cnt[wave * kSubs + lane] = 0;
+  uint32_t h[kJ], rk[kJ];  // rk: sub-range | rank inside the wave's sub-range << 3
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) {
+    const uint32_t i = w0 + (uint32_t)j * kWave + lane;
+    h[j] = i < wend ? sm.hc[i] : 0u;
+    const bool hit = (h[j] >> 31) != 0u;
+    const uint32_t b = ((h[j] & 0x7FFFFFFFu) >> p.sub_shift) & (kSubs - 1u);
+    // the lanes of this row group with the same sub-range (3 ballots on its bits) and their order
+    uint64_t peers = __ballot(hit);
+#pragma unroll
+    for (uint32_t bit = 0; bit < 3; ++bit) {
+      const uint64_t on = __ballot((b >> bit) & 1u);
+      peers &= ((b >> bit) & 1u) ? on : ~on;
+    }
+    const uint32_t before = (uint32_t)__popcll(peers & lt);
+    const uint32_t cur = hit ? s_cnt[wave * kSubs + b] : 0u;  // every lane reads before the group's first writes
+    rk[j] = b | (cur + before) << 3;
+    __builtin_amdgcn_wave_barrier();
+    if (hit && before == 0) s_cnt[wave * kSubs + b] = cur + (uint32_t)__popcll(peers);
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  if (threadIdx.x < kWave) {  // wave 0: offset of (wave w, sub-range b) — sub-range major, wave minor —
+    // as an exclusive scan over lanes x = b * NW + w (x < 32) of the counts
+    const uint32_t x = lane, b = x / NW, w = x % NW;
+    const uint32_t v = x < NW * kSubs ? s_cnt[w * kSubs + b] : 0u;
+    const uint32_t incl = wave_incl_scan(v);
+    if (x < NW * kSubs) {
+      s_off[w * kSubs + b] = incl - v;
+      if (w == 0) p.out_sub[c * kSubs + b] = incl - v;  // where sub-range b starts in the chunk
+    }
+    if (x == NW * kSubs - 1) s_off[NW * kSubs] = incl;  // the chunk's matches
+  }
+  __syncthreads();
+  const uint32_t tot = s_off[NW * kSubs];
+  // two placements, so that fewer values are live at once (the walk's registers set its occupancy):
+  // rows (sm.hc, whose reads all happened before the barrier above) and slots (the ring, once its
+  // counts are read), then the keys (in place in sm.key)
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) {  // each match's place, with the hit in bit 31
+    rk[j] = (s_off[wave * kSubs + (rk[j] & 7u)] + (rk[j] >> 3)) | (h[j] & 0x80000000u);
+    if (rk[j] >> 31) sm.hc[rk[j] & 0x7FFFFFFFu] = rid[j];
+  }
+  __syncthreads();  // the counts and offsets (in the ring) are read: the ring takes the slots
+  uint32_t *s_pos = reinterpret_cast<uint32_t *>(sm.ring);
+#pragma unroll
+  for (int j = 0; j < kJ; ++j)
+    if (rk[j] >> 31) s_pos[rk[j] & 0x7FFFFFFFu] = h[j] & 0x7FFFFFFFu;
+  __syncthreads();
+  emit_wg_stores<2, kWave * NW>(p, sm, obase, tot, false);  // sel
+  const auto rq = __builtin_amdgcn_make_buffer_rsrc(p.out_pos + obase, (short)0, (int)(p.cap * 4), 0x00020000);
+  for (uint32_t q = threadIdx.x; q * 4 < tot; q += kWave * NW) {
+    const u32x4 v = *reinterpret_cast<const u32x4 *>(&s_pos[4 * q]);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rq, (int)(16 * q), 0, 2);
+  }
+  int64_t k[kJ];
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) {
+    const uint32_t i = w0 + (uint32_t)j * kWave + lane;
+    k[j] = sm.key[i & (kMaxChunk - 1)];
+  }
+  __syncthreads();  // every key is read before any moves
+#pragma unroll
+  for (int j = 0; j < kJ; ++j)
+    if (rk[j] >> 31) sm.key[rk[j] & 0x7FFFFFFFu] = k[j];
+  __syncthreads();
+  {  // payload (the keys), 16-byte stores
+    const auto rp = __builtin_amdgcn_make_buffer_rsrc(p.out_payload + obase, (short)0, (int)(p.cap * 8), 0x00020000);
+    for (uint32_t q = threadIdx.x; q * 2 < tot; q += kWave * NW) {
+      const u32x4 v = *reinterpret_cast<const u32x4 *>(&sm.key[2 * q]);
+      __builtin_amdgcn_raw_buffer_store_b128(v, rp, (int)(16 * q), 0, 2);
+    }
+  }
+  __syncthreads();  // the ring's slots are stored: its first words take the emit's total again
+  if (threadIdx.x == 0) sm.total = tot;
+}
 // The ordered walks' output (MM): every row's round word at its position, coalesced (16-bit words,
 // 8 per lane as one 16-byte store, for full 512-row waves of chunks that are multiples of 8).
 template <uint32_t kWaveRows, typename SM>
@@ -2636,7 +2749,13 @@ __global__ __launch_bounds__(kWave * NW) void probe_walk1(ProbeParams p) {
     return;
   }
   if (POS) {  // CCJ_PART_ROWS with match positions (C5): sel and payload are the split's
-    walk_emit_pos<kWaveRows, NW>(p, sm, c, w0, wend, lane, wave, sm.wtot, phys);
+    if (p.out_sub) {
+      uint32_t rid[kWaveRows / kWave];
+      load_emit_rows(p, c, w0, wend, lane, rid);
+      walk_emit_pos_sub<kWaveRows, NW>(p, sm, c, w0, wend, lane, wave, rid);
+    } else {
+      walk_emit_pos<kWaveRows, NW>(p, sm, c, w0, wend, lane, wave, sm.wtot, phys);
+    }
     walk_finish(p, sm, c, lane, lane_rounds, 0u, t0, t1, t2, steps);
     return;
   }
@@ -2682,7 +2801,7 @@ __device__ __forceinline__ void stage_keys_aux(const int64_t *keys, uint32_t phy
 // continuing rows keeping their first window's hits — measured slower than probe_walk1<MM>: 7.75
 // against 7.49 ms, same box; the ~16 % of rows that go on are walked lane by lane in phase B.)
 template <bool POS, int NB = 1>
-__global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
+__global__ __launch_bounds__(kWave * 4, POS && NB == 1 ? 5 : 1) void probe_walk2(ProbeParams p) {
   constexpr int NW = 4;
   constexpr uint32_t kWaveRows = kMaxChunk / NW;      // rows per wave
   constexpr int kJ = (int)(kWaveRows / kWave);         // row groups (phase-A steps) per wave
@@ -2734,6 +2853,9 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
     sm.key[row_of(j)] = k[j];
     h[j] = (uint32_t)murmurhash64((uint64_t)k[j]) & p.mask;
   }
+  // slab order (C5): the rows the split stored at the outputs arrive while the chunk is walked
+  uint32_t rid_e[kJ];
+  if (POS && p.out_sub) load_emit_rows(p, c, w0, wend, lane, rid_e);
   CCJ_STAMP(t1);
   char *ring = sm.ring + wave * NB * kRingSlot;
   const uint32_t ring_lds = (uint32_t)__builtin_amdgcn_readfirstlane(
@@ -2859,7 +2981,8 @@ __global__ __launch_bounds__(kWave * 4) void probe_walk2(ProbeParams p) {
   }
   __syncthreads();
   if (POS) {
-    walk_emit_pos<kWaveRows, NW>(p, sm, c, w0, wend, lane, wave, sm.wtot, phys);
+    if (p.out_sub) walk_emit_pos_sub<kWaveRows, NW>(p, sm, c, w0, wend, lane, wave, rid_e);
+    else walk_emit_pos<kWaveRows, NW>(p, sm, c, w0, wend, lane, wave, sm.wtot, phys);
     walk_finish(p, sm, c, lane, 0u, 0u, t0, t1, t2, steps);
     return;
   }
@@ -3248,6 +3371,11 @@ struct GatherParams {
   uint32_t shift;  // timing only (tuning build, CCJ_GATHER_SHIFT): row = position >> shift
   uint32_t mask;   // timing only (tuning build, CCJ_GATHER_MASK): row = (position >> shift) & mask
   uint32_t ablate; // timing only (tuning build, CCJ_GATHER_ABLATE): 1 = no column stores
+  // slab order (gather_payload_cols_sub): the walk's sub-range starts per chunk, the partitions'
+  // chunk ranges (parts x cpp chunks, then the overflow area's), chunk groups per (partition, slab)
+  const uint32_t *sub;
+  uint32_t parts, groups;
+  uint64_t cpp, main_chunks, n_main_items;
 };
 
 template <int NP, bool VEC>
@@ -3406,6 +3534,138 @@ __global__ __launch_bounds__(256) void gather_payload_cols(GatherParams g) {
   }
 }
 
+// gather_payload_cols in slab order (round 6, with the walk's sub-range order, walk_emit_pos_sub):
+// workgroup b takes, for XCD x = b & 7 (the hardware deals workgroups to the XCDs in turn),
+// partition d of x's range, sub-range s and a group of G of d's chunks, the piece of each chunk
+// whose matches fall in sub-range s — so an XCD's workgroups work through one slab of 2^sub_shift
+// slots (4 MiB of payload rows at C5, ~1.8 MiB of them touched) at a time and its rows stay in that
+// XCD's L2 instead of being fetched from the fabric once per match (the slab walk of the whole
+// 32 MiB partition slice did: 1.62x the rows' bytes read).  The pieces, widened to even bounds so
+// the transposed column stores stay 16-byte pairs (a boundary row is written twice, with the same
+// values), are concatenated into the 512-row steps of gather_payload_cols; a step row finds its
+// piece among G wave-uniform bounds.  The overflow area's chunks follow, one whole chunk each.
+template <int U, int G>
+__global__ __launch_bounds__(256, 5) void gather_payload_cols_sub(GatherParams g) {
+  constexpr uint32_t kStep = 64 * U;
+  typedef long long i64x2 __attribute__((ext_vector_type(2)));
+  static_assert(kStep / 2 == 256 && G <= 64, "one column per store step (U = 8)");
+  __shared__ int64_t s_t[8][kStep];  // 32 KiB, five workgroups per CU (as gather_payload_cols)
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t q = threadIdx.x & 3u, r0 = threadIdx.x >> 2;
+  uint64_t c0, nch;
+  uint32_t s = 0;
+  bool whole;
+  if ((uint64_t)blockIdx.x < g.n_main_items) {
+    const uint64_t x = blockIdx.x & 7u, i = blockIdx.x >> 3;
+    const uint64_t per_part = 8ull * g.groups;
+    const uint64_t d = x * (g.parts / 8u) + i / per_part;
+    s = (uint32_t)((i / g.groups) % 8u);
+    c0 = d * g.cpp + (i % g.groups) * (uint64_t)G;
+    const uint64_t cend = (d + 1) * g.cpp;
+    nch = cend - c0 < (uint64_t)G ? cend - c0 : (uint64_t)G;
+    whole = false;
+  } else {
+    c0 = g.main_chunks + ((uint64_t)blockIdx.x - g.n_main_items);
+    nch = 1;
+    whole = true;
+  }
+  // lane p < nch: chunk c0 + p's piece [a, e), widened to even bounds
+  uint32_t pa = 0, pl_ = 0;
+  if (lane < nch) {
+    const uint64_t cc = c0 + lane;
+    const uint32_t n = g.count[cc];
+    uint32_t a = whole ? 0u : g.sub[cc * 8 + s];
+    uint32_t e = (whole || s == 7u) ? n : g.sub[cc * 8 + s + 1];
+    a &= ~1u;
+    e = (e + 1u) & ~1u;
+    e = e < n ? e : n;
+    pa = a;
+    pl_ = e > a ? e - a : 0u;
+  }
+  const uint32_t vl = (pl_ + 1u) & ~1u;  // the piece's rows in the step list (even)
+  uint32_t incl = vl;
+#pragma unroll
+  for (uint32_t dd = 1; dd < (uint32_t)G; dd <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)incl, dd);
+    if (lane >= dd) incl += t;
+  }
+  // the pieces' bounds stay in lanes 0 .. G - 1 (a piece is found by comparing against the G
+  // uniform starts, its fields fetched by ds_bpermute: select chains over per-piece arrays became
+  // a scratch lookup table)
+  const uint32_t vst_l = incl - vl;
+  const uint64_t ob_l = (c0 + (uint64_t)lane) * g.cap + pa;
+  uint32_t vst[G];
+#pragma unroll
+  for (int pp = 0; pp < G; ++pp) vst[pp] = (uint32_t)__builtin_amdgcn_readlane((int)vst_l, pp);
+  const uint32_t V = (uint32_t)__builtin_amdgcn_readlane((int)incl, G - 1);  // rows in the step list
+  if (V == 0) return;
+  // a valid position index for the list's dead rows: the first live piece's
+  const uint64_t live_mask = __ballot(lane < (uint32_t)G && pl_ != 0u);
+  const int first = (int)__builtin_ctzll(live_mask | (1ull << (G - 1)));
+  const uint64_t fb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ob_l, first) |
+                      (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ob_l >> 32), first) << 32;
+  // step-list row vr -> its piece, offset in it, its length and output base
+  auto locate = [&](uint32_t vr, uint32_t &off, uint32_t &len, uint64_t &base) {
+    uint32_t pc = 0;
+#pragma unroll
+    for (int pp = 1; pp < G; ++pp) pc += vr >= vst[pp] ? 1u : 0u;
+    off = vr - (uint32_t)__shfl((int)vst_l, (int)pc);
+    len = (uint32_t)__shfl((int)pl_, (int)pc);
+    base = (uint64_t)(uint32_t)__shfl((int)(uint32_t)ob_l, (int)pc) |
+           (uint64_t)(uint32_t)__shfl((int)(uint32_t)(ob_l >> 32), (int)pc) << 32;
+  };
+  uint32_t pl[U / 4];
+  i64x2 v[U];
+  auto load_pos = [&](uint32_t b) {
+#pragma unroll
+    for (int h = 0; h < U / 4; ++h) {  // row (4h + lane / 16) * 64 + 16 wave + lane % 16 of the step
+      const uint32_t j = b + (uint32_t)(4 * h + (lane >> 4)) * 64u + wave * 16u + (lane & 15u);
+      uint32_t off, len;
+      uint64_t base;
+      locate(j, off, len, base);
+      pl[h] = g.pos[j < V && off < len ? base + off : fb];
+    }
+  };
+  auto load_rows = [&]() {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t pu = (uint32_t)__shfl((int)pl[u / 4], (int)(((u & 3) << 4) | (lane >> 2)));
+      v[u] = reinterpret_cast<const i64x2 *>(g.pay + (uint64_t)((pu >> g.shift) & g.mask) * g.stride)[q];
+    }
+  };
+  load_pos(0);
+  load_rows();
+  if (kStep < V) load_pos(kStep);
+  for (uint32_t base = 0; base < V; base += kStep) {
+    __syncthreads();  // the previous tile is stored
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // (the XOR swizzle of gather_payload_cols)
+      s_t[2 * q][(u * 64 + r0) ^ (8u * q)] = v[u].x;
+      s_t[2 * q + 1][(u * 64 + r0) ^ (8u * q)] = v[u].y;
+    }
+    __syncthreads();
+    if (base + kStep < V) load_rows();
+    if (base + 2 * kStep < V) load_pos(base + 2 * kStep);
+    __builtin_amdgcn_sched_barrier(0);
+    // this thread's rows pr, pr + 1 of the step, the same in every column: their place once
+    const uint32_t pr = threadIdx.x * 2u;
+    uint32_t off, len;
+    uint64_t ob0;
+    locate(base + pr, off, len, ob0);
+    const bool live = base + pr < V && off < len, pair = off + 1 < len;
+    const uint64_t at = ob0 + off;
+#pragma unroll
+    for (int k = 0; k < U; ++k) {  // column k
+      const i64x2 x = *reinterpret_cast<const i64x2 *>(&s_t[k][pr ^ (8u * ((uint32_t)k >> 1))]);
+      if (!live) continue;
+      if (CCJ_ABLATED(g.ablate, 1u) && (x.x ^ x.y) != 0x5A5A5A5A5A5A5A5All) continue;
+      int64_t *dst = g.cols[k] + at;
+      if (pair) __builtin_nontemporal_store(x, reinterpret_cast<i64x2 *>(dst));
+      else __builtin_nontemporal_store((int64_t)x.x, dst);
+    }
+  }
+}
+
 thread_local const char *t_gather_kernel = "";
 
 template <int NP>
@@ -3446,7 +3706,8 @@ hipError_t launch_gather_np(const GatherParams &g, uint64_t n_chunks, hipStream_
 
 const char *last_gather_kernel() { return t_gather_kernel; }
 
-hipError_t launch_gather_payload(const ProbeParams &p, const uint32_t *pos, hipStream_t s) {
+hipError_t launch_gather_payload(const ProbeParams &p, const uint32_t *pos, hipStream_t s, uint32_t parts,
+                                 uint64_t cpp) {
   GatherParams g{};
   g.count = p.out_count;
   g.pos = pos;
@@ -3458,6 +3719,23 @@ hipError_t launch_gather_payload(const ProbeParams &p, const uint32_t *pos, hipS
   g.shift = (uint32_t)ccj_tune_int("CCJ_GATHER_SHIFT", 0);
   g.mask = (uint32_t)ccj_tune_int("CCJ_GATHER_MASK", -1);
   g.ablate = (uint32_t)ccj_tune_int("CCJ_GATHER_ABLATE", 0);
+  if (p.out_sub) {  // the walk wrote each chunk in sub-range order: the slab-order gather (8 columns)
+    constexpr int kG = 8;
+    bool ok = p.n_pay == 8 && parts >= 8 && parts % 8 == 0 && cpp && p.out_base == nullptr && p.cap % 2 == 0 &&
+              g.stride % 2 == 0 && (uintptr_t)g.pay % 16 == 0 && (uint64_t)parts * cpp <= p.n_chunks;
+    for (int q = 0; q < 8; ++q) ok = ok && (uintptr_t)g.cols[q] % 16 == 0;
+    if (!ok) return hipErrorInvalidValue;  // (the caller asks for sub-range order only where this holds)
+    g.sub = p.out_sub;
+    g.parts = parts;
+    g.cpp = cpp;
+    g.groups = (uint32_t)((cpp + kG - 1) / kG);
+    g.main_chunks = (uint64_t)parts * cpp;
+    g.n_main_items = (uint64_t)parts * 8u * g.groups;
+    const uint64_t grid = g.n_main_items + (p.n_chunks - g.main_chunks);
+    hipLaunchKernelGGL((gather_payload_cols_sub<8, kG>), dim3((unsigned)grid), dim3(256), 0, s, g);
+    t_gather_kernel = "gather_payload_cols_sub<8> (slab order: one 4 MiB payload slab per XCD at a time)";
+    return hipGetLastError();
+  }
   switch (p.n_pay) {
     case 1: return launch_gather_np<1>(g, p.n_chunks, s);
     case 2: return launch_gather_np<2>(g, p.n_chunks, s);

@@ -48,7 +48,7 @@ def test_bench_c2_with_other_paths():
     assert r3["frac_csr"] > 0 and r3["kernel_ms"] == pytest.approx(r3["probe_kernel_ms"] + r3["compaction_kernel_ms"])
     assert r3["alg_probe_bytes_per_tuple"] == pytest.approx(8 + 4 + 8 * r3["chain_keys_per_tuple"] + 12 * r3["m_bar"])
     # the gather kernel that actually ran, and no traffic pasted from a profile of another shape / build
-    assert ow["C5"]["roofline"]["gather_kernel_run"].startswith("gather_payload_cols<8>")
+    assert ow["C5"]["roofline"]["gather_kernel_run"].startswith("gather_payload_cols_sub<8>")  # slab order
     for r in (line["roofline"], r3, ow["C5"]["roofline"]):
         assert r["traffic"] is None or r["traffic_stale"] is False
     # the multi-GPU protocol at N = 1 on the C4 per-GPU shape: the N = 1 point of the curve

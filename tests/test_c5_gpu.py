@@ -154,3 +154,68 @@ def test_c5_partitioned_rows(chunk, n_probe, spread):
     assert len(np.unique(prow)) == len(prow)  # distinct keys: one match per probe row at most
     m, _ = O.count_uniform(77 + spread, 0, n_probe, rng, n_build, 1)
     assert len(prow) == m
+
+
+@pytest.mark.parametrize("chunk,n_probe,spread,before_payload", [(2048, 1 << 22, 8, False), (2048, (1 << 22) + 777, 0, False),
+                                                                 (1000, 3000001, 8, False), (2048, 1 << 22, 2, True),
+                                                                 (1001, 3000001, 8, False), (2048, 1 << 22, -1, False)])
+def test_c5_partitioned_rows_slab_order(chunk, n_probe, spread, before_payload):
+    """C5 with >= 8 partitions (2^20 build keys: 2^22 slots, 8 windows): the walk writes each chunk's
+    matches in order of their slot's sub-range (walk_emit_pos_sub) and the gather takes one slab of
+    payload rows per XCD at a time (gather_payload_cols_sub).  Within every chunk the positions'
+    sub-ranges never decrease; sel / payload / positions / every payload column stay consistent,
+    each probe row once, the count exact.  before_payload: the workspace was sized before the
+    payload columns existed (no room for the sub-range starts): row order and the row-order gather.
+    An odd chunk (1001) keeps row order (the 16-byte column pairs need an even capacity); spread -1:
+    every 16th probe on one key, so the split's overflow area holds that partition's extra runs (its
+    chunks are gathered whole, after the slabs)."""
+    n_build = 1 << 20
+    bkeys = ref_keys(n_build, 1)
+    pay = payload_rows(n_build)
+    table = ccj.Table.on_device(ccj.LP, torch.from_numpy(bkeys).cuda())
+    assert table.size == 1 << 22
+    rng = n_build + (n_build // spread if spread > 0 else 0)
+    keys_np = O.uniform_keys(91 + spread, 0, n_probe, rng)
+    if spread < 0:  # skew: every 16th probe on one key, so its partition's runs overflow into the area
+        keys_np[::16] = 5
+    keys = torch.from_numpy(keys_np).cuda()
+    part = table.alloc_partitioned(n_probe, chunk) if before_payload else None
+    table.set_payload(torch.from_numpy(pay.reshape(-1)).cuda(), P)
+    out = table.probe_partitioned(keys, chunk, pos=True, payload_cols=P, rows=True, part=part)
+    torch.cuda.synchronize()
+    kern = ccj.last_gather_kernel()
+    slab = not before_payload and chunk % 2 == 0
+    assert kern.startswith("gather_payload_cols_sub<8>" if slab else "gather_payload_cols<8>" if chunk % 2 == 0
+                           else "gather_payload_quad"), kern
+    assert int(out["status"].item()) == 0
+    nc, cap = out["n_chunks"], out["cap"]
+    cnt = out["count"].cpu().numpy()[:nc].astype(np.int64)
+    valid2 = np.arange(cap)[None, :] < cnt[:, None]
+    valid = valid2.reshape(-1)
+    pos = out["pos"].cpu().numpy()[:nc * cap].view(np.uint32).reshape(nc, cap).astype(np.int64)
+    if slab:  # sub-range order inside each chunk (window bits 19: sub-range = bits 16-18)
+        sub = (pos >> 16) & 7
+        sub = np.where(valid2, sub, 8)
+        assert (np.diff(sub, axis=1)[:, :] >= 0)[valid2[:, 1:]].all()
+    prow = out["sel"].cpu().numpy()[:nc * cap].view(np.uint32)[valid].astype(np.int64)
+    keys_h = keys.cpu().numpy()
+    assert np.array_equal(out["payload"].cpu().numpy()[:nc * cap][valid], keys_h[prow])
+    assert np.array_equal(table_slots(table)[pos.reshape(-1)[valid]], keys_h[prow])
+    col0 = out["payload_cols"][0].cpu().numpy()[:nc * cap][valid]
+    order = np.argsort(pay[:, 0])
+    at = np.searchsorted(pay[order, 0], col0)
+    assert (at < n_build).all() and np.array_equal(pay[order[np.minimum(at, n_build - 1)], 0], col0)
+    brow = order[at]
+    assert np.array_equal(bkeys[brow], keys_h[prow])
+    for c in range(1, P):
+        assert np.array_equal(out["payload_cols"][c].cpu().numpy()[:nc * cap][valid], pay[brow, c])
+    assert len(np.unique(prow)) == len(prow)
+    if spread >= 0:
+        m, _ = O.count_uniform(91 + spread, 0, n_probe, rng, n_build, 1)
+    else:  # reference keys 0 .. n_build - 1 (cf 1): a probe hits iff its key is below n_build
+        m = int((keys_np < n_build).sum())
+    assert len(prow) == m
+
+
+def table_slots(table):
+    return table.arrays()["table"]
