@@ -2483,9 +2483,9 @@ __device__ __forceinline__ void load_emit_rows(const ProbeParams &p, uint64_t c,
                                                uint32_t lane, uint32_t (&rid)[kJ]) {
   const uint32_t *sel_c = p.out_sel + c * p.cap;  // (a uniform base: 32-bit lane offsets)
 #pragma unroll
-  for (int j = 0; j < kJ; ++j) {  // (a dead row reads slot 0)
+  for (int j = 0; j < kJ; ++j) {  // (a dead row reads slot 0; streamed: non-temporal, as the keys)
     const uint32_t i = w0 + (uint32_t)j * kWave + lane;
-    rid[j] = sel_c[i < wend ? i : 0u];
+    rid[j] = __builtin_nontemporal_load(sel_c + (i < wend ? i : 0u));
   }
 }
 template <uint32_t kWaveRows, int NW, typename SM>
@@ -3732,6 +3732,16 @@ hipError_t launch_gather_payload(const ProbeParams &p, const uint32_t *pos, hipS
     g.main_chunks = (uint64_t)parts * cpp;
     g.n_main_items = (uint64_t)parts * 8u * g.groups;
     const uint64_t grid = g.n_main_items + (p.n_chunks - g.main_chunks);
+#ifdef CCJ_TUNING
+    if (ccj_tune_int("CCJ_GATHER_G", kG) == 16) {  // (tuning: 16 chunks per workgroup)
+      g.groups = (uint32_t)((cpp + 15) / 16);
+      g.n_main_items = (uint64_t)parts * 8u * g.groups;
+      const uint64_t grid16 = g.n_main_items + (p.n_chunks - g.main_chunks);
+      hipLaunchKernelGGL((gather_payload_cols_sub<8, 16>), dim3((unsigned)grid16), dim3(256), 0, s, g);
+      t_gather_kernel = "gather_payload_cols_sub<8> (slab order, 16 chunks per workgroup)";
+      return hipGetLastError();
+    }
+#endif
     hipLaunchKernelGGL((gather_payload_cols_sub<8, kG>), dim3((unsigned)grid), dim3(256), 0, s, g);
     t_gather_kernel = "gather_payload_cols_sub<8> (slab order: one 4 MiB payload slab per XCD at a time)";
     return hipGetLastError();
