@@ -11,7 +11,7 @@
 //   F_s       = pass-through results before result s;  E(t) = t == 0 ? 0 : ceil(t / chunk) - 1
 //   pass-through result s   -> output chunk E(t_s) + F_s (keeping its own row count)
 //   P-row u (chunk k = u/B)  -> output chunk k + #{pass-through s : E(t_s) <= k}, row u % B
-// Kernels: per-chunk segment sums -> exclusive scans (hipCUB) -> full-result E list -> one wave
+// Kernels: per-chunk segment sums -> exclusive scans (ccj_scan.hip) -> full-result E list -> one wave
 // per probe chunk copies its rows (DataChunk::Append's gather, base.cpp:15-27) -> chunk counts.
 
 #include <cstdlib>
