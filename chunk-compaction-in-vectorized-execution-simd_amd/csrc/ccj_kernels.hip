@@ -1608,6 +1608,9 @@ __device__ __forceinline__ void chain_filt_body(const ProbeParams &p, uint32_t *
         const uint32_t len = rec8 ? (uint32_t)(rec[jj] >> 32) & 0xFFu : (uint32_t)(rec[jj] >> 32);
         lim = ps ? st + len : 0u;
         cur = ps ? (rec8 ? rec8_first(rec[jj], kfp[jj]) : st) : 0u;
+        // (timing only, tuning build: three rows in four read their record but walk no chain — the
+        // hits of the 0x8000 ablation with the full record working set; wrong results)
+        if (CCJ_ABLATED(p.ablate, 0x40000u) && (urow(jj) & 3u)) lim = cur;
       };
       // queue index of every chain row (slot-major); WORDS: the other rows' words now, coalesced
       uint64_t qm[kJ];  // wave-uniform: slot jj's chain rows, and the queue index of its first

@@ -21,8 +21,8 @@ N_BUILD, N_PROBE, CHUNK = 1 << 18, 1 << 21, 2048
 
 # bits read by the probe walks (ProbeParams::ablate), the slot split (its ablate word) and the
 # gather; the owner split's (CCJ_OWNER_ABLATE) words below
-PROBE_BITS = [0x1, 0x2, 0x10, 0x20, 0x40, 0x80, 0x100, 0x200, 0x400, 0x2000, 0x4000, 0x8000, 0x10000, 0x100000,
-              0x200000]
+PROBE_BITS = [0x1, 0x2, 0x10, 0x20, 0x40, 0x80, 0x100, 0x200, 0x400, 0x2000, 0x4000, 0x8000, 0x10000, 0x40000,
+              0x100000, 0x200000]
 OWNER_BITS = [0x10, 0x20, 0x40, 0x80, 0x2000, 0x100000, 0x200000]
 
 
