@@ -1,0 +1,182 @@
+"""Seeded random sweep over the probe entry points, each case checked against the oracle.
+
+Each case draws its configuration from its seed:
+  - table kind (LP / chaining);
+  - build keys: distinct, or with duplicates;
+  - probe keys: hits, misses, a hot key (skew), empty markers (-1) and other negative keys;
+  - chunk width from 1 to 2048, and a ragged last chunk.
+Every entry point that takes the configuration is run on it, through the C ABI:
+  ccj_probe              L3: every Next's rows in round-major order equal the oracle's
+                         (oracle/ccj_oracle.c, after linear_probing_ht.cpp:62-115 /
+                         chaining_ht.cpp:82-107), in the rounds view and the merged view
+  ccj_probe_ordered      L3: the same comparison
+  ccj_probe_partitioned  L1 + L2: the multiset of (probe row, payload) equals the oracle's
+  LP, distinct keys:     rows mode (CCJ_PART_ROWS) gives the same multiset; with 8 payload columns
+                         and match positions, on both the chunk path (L3: positions equal the
+                         oracle's) and the partitioned path (slab order where it applies), every
+                         gathered column is the matched build tuple's.
+The cases complement the fixed-shape tests: shapes nobody picked by hand."""
+import numpy as np
+import pytest
+
+from helpers import assert_trace_equal, views_from_rounds
+from oracle import oracle as O
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import ccj  # noqa: E402
+
+N_CASES = 64
+GATHERS = set()  # the gather kernels the partitioned payload probes ran (ccj_last_gather_kernel)
+P = 8  # payload columns
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ccj.device_init(0)
+
+
+def draw(case):
+    """The case's configuration: (kind, build keys, probe keys, chunk)."""
+    r = np.random.default_rng(7001 + case)
+    kind = ccj.CHAIN if case % 3 == 2 else ccj.LP
+    n_build = int(r.choice([1, 5, 300, 4096, 50000, 1 << 18, (1 << 20) + 17, 1 << 21]))
+    distinct = bool(r.random() < 0.6)
+    base = int(r.integers(0, 1 << 40))
+    if distinct:
+        bk = base + r.permutation(2 * n_build)[:n_build].astype(np.int64)
+    else:
+        bk = base + r.integers(0, max(1, n_build // 3), n_build, dtype=np.int64)
+    chunk = int(r.choice([1, 2, 63, 64, 100, 256, 1000, 1023, 2047, 2048, 2048, 2048]))
+    n_probe = int(r.choice([1, 999, 1 << 16, 300001, 1 << 20, (1 << 22) - 5]))
+    if not distinct or chunk < 64:
+        n_probe = min(n_probe, 1 << 18)  # outputs of chunk * max_dup rows per chunk
+    hit = float(r.random())
+    keys = np.where(r.random(n_probe) < hit, bk[r.integers(0, n_build, n_probe)],
+                    base + 2 * n_build + r.integers(0, 2 * n_build + 1, n_probe))
+    if r.random() < 0.3:  # a hot key: one build key in ~1/5 of the rows
+        keys[r.random(n_probe) < 0.2] = bk[0]
+    if r.random() < 0.3:  # the empty marker and other negative keys never match
+        keys[::101] = -1
+        keys[50::103] = -(1 << 62)
+    return kind, bk.astype(np.int64), keys.astype(np.int64), chunk
+
+
+def payload_rows(n):
+    g = np.arange(n, dtype=np.uint64)[:, None] * np.uint64(P) + np.arange(P, dtype=np.uint64)[None, :]
+    return O.fmix64(g).view(np.int64)
+
+
+def host(o):
+    torch.cuda.synchronize()
+
+    def conv(v):
+        if isinstance(v, torch.Tensor):
+            return v.cpu().numpy()
+        return [conv(x) for x in v] if isinstance(v, list) else v
+    return {k: conv(v) for k, v in o.items()}
+
+
+def valid_of(count, n_chunks, cap):
+    cnt = np.asarray(count[:n_chunks]).view(np.uint32).astype(np.int64)
+    return cnt, (np.arange(cap)[None, :] < cnt[:, None]).reshape(-1)
+
+
+def pairs(rows, pay):
+    rows = np.asarray(rows, np.int64)
+    pay = np.asarray(pay, np.int64)
+    o = np.lexsort((pay, rows))
+    return rows[o], pay[o]
+
+
+def assert_same_pairs(got, want, what):
+    g, w = pairs(*got), pairs(*want)
+    assert len(g[0]) == len(w[0]), (what, len(g[0]), len(w[0]))
+    assert np.array_equal(g[0], w[0]) and np.array_equal(g[1], w[1]), what
+
+
+def assert_l3(out, want, kind):
+    for merged in ((False, True) if kind == ccj.CHAIN else (False,)):
+        g = views_from_rounds(out["count"], out["sel"].view(np.uint32), out["payload"], out["rounds"],
+                              out["round_counts"], out["cap"], out["max_rounds"], merged=merged)
+        w = views_from_rounds(want["count"], want["sel"], want["payload"], want["rounds"], want["round_counts"],
+                              want["cap"], want["max_rounds"], merged=merged)
+        assert_trace_equal(g, w)
+
+
+@pytest.mark.parametrize("case", range(N_CASES))
+def test_sweep_case(case):
+    kind, bk, keys, chunk = draw(case)
+    n = len(keys)
+    table = ccj.Table.from_host(kind, bk)
+    otab = O.Table(kind, bk)
+    dup = max(1, int(table.max_dup))
+    d_keys = torch.from_numpy(keys).cuda()
+
+    # L3: the chunk path and the ordered path, against the oracle
+    out = host(table.probe(d_keys, chunk))
+    assert out["status"][0] == 0, hex(int(out["status"][0]))
+    want = otab.probe(keys, chunk, cap_factor=dup, max_rounds=out["max_rounds"])
+    assert_l3(out, want, kind)
+    ordered = host(table.probe_ordered(d_keys, chunk))
+    assert ordered["status"][0] == 0, hex(int(ordered["status"][0]))
+    assert_l3(ordered, want, kind)
+
+    # the oracle's matches as (probe row, payload)
+    n_chunks = (n + chunk - 1) // chunk
+    wcnt, wvalid = valid_of(want["count"], n_chunks, want["cap"])
+    wrow = np.repeat(np.arange(n_chunks, dtype=np.int64), wcnt) * chunk + want["sel"][wvalid].astype(np.int64)
+    wpay = want["payload"][wvalid]
+    wpos = want["pos"][wvalid]
+
+    # L1 + L2: the partitioned probe (the row map takes a position back to its row)
+    part = table.probe_partitioned(d_keys, chunk)
+    h = host(part)
+    assert h["status"][0] == 0, hex(int(h["status"][0]))
+    cnt, valid = valid_of(h["count"], h["n_chunks"], h["cap"])
+    gpos = np.repeat(np.arange(h["n_chunks"], dtype=np.int64), cnt) * chunk + \
+        h["sel"].view(np.uint32)[:h["n_chunks"] * h["cap"]][valid].astype(np.int64)
+    grow = h["row_map"].view(np.uint32)[gpos].astype(np.int64)
+    assert_same_pairs((grow, h["payload"][:h["n_chunks"] * h["cap"]][valid]), (wrow, wpay), "partitioned")
+
+    if kind != ccj.LP or dup != 1 or table.size < 16:
+        table.free()
+        return
+    # LP, distinct keys (a table of >= 16 slots): rows mode
+    h = host(table.probe_partitioned(d_keys, chunk, rows=True))
+    assert h["status"][0] == 0, hex(int(h["status"][0]))
+    cnt, valid = valid_of(h["count"], h["n_chunks"], h["cap"])
+    grow = h["sel"].view(np.uint32)[:h["n_chunks"] * h["cap"]][valid].astype(np.int64)
+    assert_same_pairs((grow, h["payload"][:h["n_chunks"] * h["cap"]][valid]), (wrow, wpay), "rows mode")
+    # payload columns: the chunk path (positions at L3) and the partitioned path (slab order)
+    pay = payload_rows(len(bk))
+    table.set_payload(torch.from_numpy(pay.reshape(-1)).cuda(), P)
+    h = host(table.probe(d_keys, chunk, pos=True, payload_cols=P))
+    assert h["status"][0] == 0, hex(int(h["status"][0]))
+    assert np.array_equal(h["count"].view(np.uint32), want["count"])
+    _, valid = valid_of(h["count"], n_chunks, h["cap"])
+    pos = h["pos"].view(np.uint32)[valid]
+    assert np.array_equal(pos, wpos)
+    for c in range(P):
+        assert np.array_equal(h["payload_cols"][c][valid], pay[otab.rows[pos], c]), ("chunk path column", c)
+    h = host(table.probe_partitioned(d_keys, chunk, rows=True, pos=True, payload_cols=P))
+    GATHERS.add(ccj.last_gather_kernel().split("<")[0])
+    assert h["status"][0] == 0, hex(int(h["status"][0]))
+    cnt, valid = valid_of(h["count"], h["n_chunks"], h["cap"])
+    lim = h["n_chunks"] * h["cap"]
+    grow = h["sel"].view(np.uint32)[:lim][valid].astype(np.int64)
+    gkey = h["payload"][:lim][valid]
+    assert_same_pairs((grow, gkey), (wrow, wpay), "payload columns")
+    pos = h["pos"].view(np.uint32)[:lim][valid]
+    assert np.array_equal(otab.table[pos], gkey)  # the position holds the row's key
+    for c in range(P):
+        assert np.array_equal(h["payload_cols"][c][:lim][valid], pay[otab.rows[pos], c]), ("partitioned column", c)
+    table.free()
+
+
+def test_sweep_ran_both_gathers():
+    """The sweep reached the slab-order gather and the per-chunk one (runs after the cases)."""
+    assert {"gather_payload_cols", "gather_payload_cols_sub"} <= GATHERS, GATHERS
