@@ -10,6 +10,9 @@ Every entry point that takes the configuration is run on it, through the C ABI:
                          (oracle/ccj_oracle.c, after linear_probing_ht.cpp:62-115 /
                          chaining_ht.cpp:82-107), in the rounds view and the merged view
   ccj_probe_ordered      L3: the same comparison
+  ccj_compact            the chunk path's Next results re-chunked: every row's output slot, the
+                         output chunk counts and the carried columns equal the oracle's sequential
+                         compactor on the oracle's Next results (threshold and key-column options drawn)
   ccj_probe_partitioned  L1 + L2: the multiset of (probe row, payload) equals the oracle's
   LP, distinct keys:     rows mode (CCJ_PART_ROWS) gives the same multiset; with 8 payload columns
                          and match positions, on both the chunk path (L3: positions equal the
@@ -107,6 +110,41 @@ def assert_l3(out, want, kind):
         assert_trace_equal(g, w)
 
 
+def check_compaction(case, out_d, want, keys, d_keys, chunk):
+    """ccj_compact of the chunk path's Next results against the oracle's sequential NaiveCompactor
+    (compact_plan: compactor.cpp:5-41, the :36 fix) run on the ORACLE's Next results: output chunk
+    counts and every row's global row, payload and carried columns (DataChunk::Append, base.cpp:15-27),
+    with the case's pass-through threshold and, for odd cases, the key column filled from the payload."""
+    r = np.random.default_rng(9001 + case)
+    threshold = int(r.choice([0, 1, max(1, chunk // 2), chunk]))
+    extra = (np.arange(len(keys), dtype=np.int64) * 7 - 3)
+    d_extra = torch.from_numpy(extra).cuda()
+    key_cols = [0] if case % 2 else []
+    comp = ccj.compact(out_d, chunk, cols=[d_keys, d_extra], threshold=threshold, key_cols=key_cols)
+    torch.cuda.synchronize()
+    assert int(comp["status"].item()) == 0
+    cap, mr = want["cap"], want["max_rounds"]
+    segs, rows, pays = [], [], []
+    for c in range(len(want["count"])):
+        k = int(want["count"][c])
+        segs.extend(int(x) for x in want["round_counts"][c * mr:c * mr + int(want["rounds"][c])])
+        rows.append(c * chunk + want["sel"][c * cap:c * cap + k].astype(np.int64))
+        pays.append(want["payload"][c * cap:c * cap + k])
+    rows = np.concatenate(rows) if rows else np.zeros(0, np.int64)
+    pays = np.concatenate(pays) if pays else np.zeros(0, np.int64)
+    dest, occ = O.compact_plan(np.array(segs, np.uint32), chunk, threshold)
+    dest = dest.astype(np.int64)
+    n_out = int(comp["n"].item())
+    assert n_out == len(occ)
+    assert np.array_equal(comp["counts"].cpu().numpy()[:n_out].view(np.uint32), occ)
+    lim = n_out * chunk
+    assert np.array_equal(comp["row"].cpu().numpy()[:lim][dest], rows)
+    assert np.array_equal(comp["payload"].cpu().numpy()[:lim][dest], pays)
+    assert np.array_equal(comp["cols"][0].cpu().numpy()[:lim][dest], keys[rows])
+    assert np.array_equal(comp["cols"][1].cpu().numpy()[:lim][dest], extra[rows])
+    assert int(occ.sum()) == len(rows)  # nothing lost, nothing added
+
+
 @pytest.mark.parametrize("case", range(N_CASES))
 def test_sweep_case(case):
     kind, bk, keys, chunk = draw(case)
@@ -117,10 +155,12 @@ def test_sweep_case(case):
     d_keys = torch.from_numpy(keys).cuda()
 
     # L3: the chunk path and the ordered path, against the oracle
-    out = host(table.probe(d_keys, chunk))
+    out_d = table.probe(d_keys, chunk)
+    out = host(out_d)
     assert out["status"][0] == 0, hex(int(out["status"][0]))
     want = otab.probe(keys, chunk, cap_factor=dup, max_rounds=out["max_rounds"])
     assert_l3(out, want, kind)
+    check_compaction(case, out_d, want, keys, d_keys, chunk)
     ordered = host(table.probe_ordered(d_keys, chunk))
     assert ordered["status"][0] == 0, hex(int(ordered["status"][0]))
     assert_l3(ordered, want, kind)
