@@ -797,14 +797,17 @@ __global__ __launch_bounds__(256) void lp_runs(const int64_t *slots, uint64_t n_
     const bool occ = i < n_slots && slots[i] != -1;
     uint64_t m = __ballot(occ);
     if (i - lane >= n_slots) break;  // wave-uniform
+    // the step's slots: 64, or fewer in a table of < 64 slots (the table's end is bit valid - 1)
+    const uint32_t valid = n_slots - (b + s) < 64u ? (uint32_t)(n_slots - (b + s)) : 64u;
+    const bool all = m == (valid == 64u ? ~0ull : (1ull << valid) - 1ull);
     // run continuing from the previous step
-    const uint32_t lo = m == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~m);
+    const uint32_t lo = all ? valid : (uint32_t)__builtin_ctzll(~m);
     if (in_lead) {
       lead += lo;
-      if (lo < 64) in_lead = false;
+      if (!all) in_lead = false;
     }
-    if (lo == 64) {
-      cur += 64;
+    if (all) {
+      cur += valid;
     } else {
       cur += lo;
       best = cur > best ? cur : best;
@@ -817,7 +820,11 @@ __global__ __launch_bounds__(256) void lp_runs(const int64_t *slots, uint64_t n_
         ++inner;
       }
       best = inner > best ? inner : best;
-      cur = m == 0 ? 0u : (uint32_t)__builtin_clzll(~m);  // trailing run (top bits)
+      // trailing run: the occupied slots that end at the step's last slot (bit valid - 1; round 6:
+      // bit 63 was taken as the table's end, so a run wrapping round a table of < 64 slots lost its
+      // tail and max_rounds / max_dup came out short)
+      const uint64_t top = m << (64u - valid);
+      cur = top == 0 ? 0u : (uint32_t)__builtin_clzll(~top);
     }
     best = cur > best ? cur : best;
   }

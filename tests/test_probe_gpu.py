@@ -144,6 +144,27 @@ def test_device_lp_build_run_stats_match_host_layout():
     assert host_t.max_rounds == dev_t.max_rounds  # the occupied set is insertion-order independent
 
 
+@pytest.mark.parametrize("n", [2, 3, 5, 9, 15])
+@pytest.mark.parametrize("dups", [False, True])
+def test_device_lp_build_tiny_table_wrapping_run(n, dups):
+    """Tables of < 64 slots (n < 16 keys): a run that wraps round the table's end.  The device
+    build's run statistics (lp_runs) must see the table end at slot size - 1, not at the step's bit
+    63 — found by tests/test_sweep_gpu.py: 5 equal keys gave max_dup 4 and a short max_rounds."""
+    size = 1
+    while size < 4 * n:
+        size <<= 1
+    cand = np.arange(1, 1 << 16, dtype=np.int64)
+    home = (_np_murmur(cand.astype(np.uint64)) & np.uint64(size - 1)).astype(np.int64)
+    k0 = int(cand[home == size - 1][0])  # its run starts at the last slot and wraps
+    keys = np.full(n, k0, np.int64) if dups else np.concatenate([[k0], cand[home == size - 1][1:n]])
+    host_t = ccj.Table.from_host(ccj.LP, keys)
+    dev_t = ccj.Table.on_device(ccj.LP, to_dev(keys))
+    assert (dev_t.size, dev_t.max_rounds, dev_t.max_dup) == (host_t.size, host_t.max_rounds, host_t.max_dup)
+    assert dev_t.max_rounds == n and dev_t.max_dup == (n if dups else 1)
+    out = host(dev_t.probe(to_dev(keys), 64))
+    assert out["status"][0] == 0 and int(out["count"][0]) == (n * n if dups else n)
+
+
 @pytest.mark.parametrize("kind", [ccj.LP, ccj.CHAIN])
 def test_l1_l2_large_membership(kind):
     n, n_probe, rng = 1 << 22, 1 << 26, 3 << 21

@@ -14,6 +14,8 @@ Every entry point that takes the configuration is run on it, through the C ABI:
                          output chunk counts and the carried columns equal the oracle's sequential
                          compactor on the oracle's Next results (threshold and key-column options drawn)
   ccj_probe_partitioned  L1 + L2: the multiset of (probe row, payload) equals the oracle's
+  device-built tables    the same keys built by ccj_table_build_on_device: chaining (byte-identical
+                         to the host build) at L3, LP (atomicCAS placement) at L1 + L2
   LP, distinct keys:     rows mode (CCJ_PART_ROWS) gives the same multiset; with 8 payload columns
                          and match positions, on both the chunk path (L3: positions equal the
                          oracle's) and the partitioned path (slab order where it applies), every
@@ -171,6 +173,20 @@ def test_sweep_case(case):
     wrow = np.repeat(np.arange(n_chunks, dtype=np.int64), wcnt) * chunk + want["sel"][wvalid].astype(np.int64)
     wpay = want["payload"][wvalid]
     wpos = want["pos"][wvalid]
+
+    # the device build of the same keys (ccj_table_build_on_device): chaining is byte-identical to
+    # the host build, so L3 holds; the LP device build places keys by atomicCAS: L1 + L2
+    dt = ccj.Table.on_device(kind, torch.from_numpy(bk).cuda())
+    assert int(dt.max_dup) == dup
+    h = host(dt.probe(d_keys, chunk))
+    assert h["status"][0] == 0, hex(int(h["status"][0]))
+    if kind == ccj.CHAIN:
+        assert_l3(h, want, kind)
+    else:
+        cnt, valid = valid_of(h["count"], n_chunks, h["cap"])
+        grow = np.repeat(np.arange(n_chunks, dtype=np.int64), cnt) * chunk + h["sel"].view(np.uint32)[valid]
+        assert_same_pairs((grow, h["payload"][valid]), (wrow, wpay), "device-built LP")
+    dt.free()
 
     # L1 + L2: the partitioned probe (the row map takes a position back to its row)
     part = table.probe_partitioned(d_keys, chunk)
