@@ -20,11 +20,16 @@ Every entry point that takes the configuration is run on it, through the C ABI:
                          and match positions, on both the chunk path (L3: positions equal the
                          oracle's) and the partitioned path (slab order where it applies), every
                          gathered column is the matched build tuple's.
+  filtered input         a drawn selection vector and per-chunk counts (the pipeline's chunk form):
+                         the chunk path at L3 against the oracle on the same sel / counts
+  ccj_pipeline_run       1-4 joins of drawn tables and columns, no compaction / NaiveCompactor /
+                         drawn thresholds, against the oracle's join-by-join restatement of
+                         main.cpp:119-191 (tests/helpers.py oracle_pipeline): the result table in order
 The cases complement the fixed-shape tests: shapes nobody picked by hand."""
 import numpy as np
 import pytest
 
-from helpers import assert_trace_equal, views_from_rounds
+from helpers import assert_trace_equal, oracle_pipeline, views_from_rounds
 from oracle import oracle as O
 
 torch = pytest.importorskip("torch")
@@ -236,3 +241,70 @@ def test_sweep_case(case):
 def test_sweep_ran_both_gathers():
     """The sweep reached the slab-order gather and the per-chunk one (runs after the cases)."""
     assert {"gather_payload_cols", "gather_payload_cols_sub"} <= GATHERS, GATHERS
+
+
+def test_sweep_filtered_input():
+    """Chunks with a selection vector and per-chunk counts (a chunk's rows are sel[c*B, c*B + counts[c]),
+    in sel's order; linear_probing_ht.cpp:39-60 takes (join_key, count, sel)): L3 against the oracle."""
+    for case in range(8):
+        kind, bk, keys, chunk = draw(100 + case)
+        r = np.random.default_rng(5001 + case)
+        n_chunks = (len(keys) + chunk - 1) // chunk
+        keys = np.concatenate([keys, np.full(n_chunks * chunk - len(keys), -1, np.int64)])  # whole chunks
+        sel = np.concatenate([r.permutation(chunk) for _ in range(n_chunks)]).astype(np.uint32)
+        counts = r.integers(0, chunk + 1, n_chunks).astype(np.uint32)
+        table = ccj.Table.from_host(kind, bk)
+        otab = O.Table(kind, bk)
+        out = host(table.probe(torch.from_numpy(keys).cuda(), chunk, sel=torch.from_numpy(sel.view(np.int32)).cuda(),
+                               counts=torch.from_numpy(counts.view(np.int32)).cuda()))
+        assert out["status"][0] == 0, (case, hex(int(out["status"][0])))
+        want = otab.probe(keys, chunk, sel=sel, counts=counts, cap_factor=max(1, int(table.max_dup)),
+                          max_rounds=out["max_rounds"])
+        assert_l3(out, want, kind)
+        table.free()
+
+
+def draw_pipeline(case):
+    r = np.random.default_rng(8001 + case)
+    joins = int(r.integers(1, 5))
+    B = int(r.choice([1, 7, 64, 100, 256, 1000, 2048]))
+    n = int(r.choice([1, 500, 5000, 20000]))
+    if B < 64:
+        n = min(n, 3000)
+    tables, cols = [], []
+    for _ in range(joins):
+        kind = ccj.LP if r.random() < 0.5 else ccj.CHAIN
+        nb = int(r.choice([1, 10, 300, 4000]))
+        base = int(r.integers(0, 1 << 40))
+        if r.random() < 0.5:
+            bk = base + r.permutation(2 * nb)[:nb].astype(np.int64)
+        else:
+            bk = base + r.integers(0, max(1, nb // 2), nb, dtype=np.int64)
+        hit = float(r.random())
+        col = np.where(r.random(n) < hit, bk[r.integers(0, nb, n)], base + 2 * nb + r.integers(0, 100, n))
+        tables.append((kind, bk.astype(np.int64)))
+        cols.append(col.astype(np.int64))
+    compact = bool(r.random() < 0.6)
+    thresholds = [int(r.choice([0, 1, max(1, B // 2), B])) for _ in range(joins)] if compact and r.random() < 0.5 \
+        else None
+    return tables, cols, B, compact, thresholds
+
+
+@pytest.mark.parametrize("case", range(16))
+def test_sweep_pipeline(case):
+    tables, cols, B, compact, thresholds = draw_pipeline(case)
+    dt = [ccj.Table.from_host(kind, bk) for kind, bk in tables]
+    ot = [O.Table(kind, bk) for kind, bk in tables]
+    cf = max(max(1, int(t.max_dup)) for t in dt)
+    want = oracle_pipeline(ot, cols, B, compact, cap_factor=cf, max_rounds=1 + max(int(t.max_rounds) for t in dt),
+                           thresholds=thresholds)
+    pl = ccj.Pipeline(dt, B, compact)
+    if thresholds is not None:
+        pl.set_thresholds(thresholds)
+    pl.run([torch.from_numpy(c).cuda() for c in cols])
+    joins = len(dt)
+    got = pl.result_columns()
+    got = got[:joins] + [got[joins + 2 * l + 1] for l in range(joins)]
+    assert pl.res.n_out == len(want[0]), (pl.res.n_out, len(want[0]))
+    for g, w in zip(got, want):
+        np.testing.assert_array_equal(g, w)
