@@ -2,7 +2,7 @@
 
 Each case draws its configuration from its seed:
   - table kind (LP / chaining);
-  - build keys: distinct, or with duplicates;
+  - build keys: distinct, or with duplicates, some negative;
   - probe keys: hits, misses, a hot key (skew), empty markers (-1) and other negative keys;
   - chunk width from 1 to 2048, and a ragged last chunk.
 Every entry point that takes the configuration is run on it, through the C ABI:
@@ -72,7 +72,12 @@ def draw(case):
     if r.random() < 0.3:  # the empty marker and other negative keys never match
         keys[::101] = -1
         keys[50::103] = -(1 << 62)
-    return kind, bk.astype(np.int64), keys.astype(np.int64), chunk
+    bk, keys = bk.astype(np.int64), keys.astype(np.int64)
+    if np.random.default_rng(99 + case).random() < 0.25:
+        # negative build keys, the same keys negated in both columns (never -1: the LP empty marker)
+        bk = np.where((bk > 1) & (bk % 5 == 0), -bk, bk)
+        keys = np.where((keys > 1) & (keys % 5 == 0), -keys, keys)
+    return kind, bk, keys, chunk
 
 
 def payload_rows(n):
