@@ -822,8 +822,9 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
 
 // owner_split_direct: the owner split (<= 64 destinations) without the workgroup's tile image.
 // Per tile:
-//   rank (one ballot per destination-index bit; the wave's running count of destination p in lane
-//   p) | the wave's 64 x PER keys written to its own LDS image in destination order | barrier |
+//   rank (ATOM: an LDS atomic on the wave's counter of the key's destination; else one ballot per
+//   destination-index bit, the wave's running count of destination p in lane p) | the wave's
+//   64 x PER keys written to its own LDS image in destination order | barrier |
 //   one reservation atomic per destination for the workgroup's whole run, split into the waves'
 //   runs | barrier | each wave stores its image in order
 // A wave's image holds whole runs of ~64 x PER / parts keys, as slot_split_pipe's image does for
@@ -834,7 +835,7 @@ __global__ __launch_bounds__(THREADS) void slot_split_pipe(const int64_t *keys, 
 // slot_split_pipe's small form (partition_grouped_sub_cap sizes them); the order inside a
 // segment is free ("in any order").  Inactive lanes store to the per-XCD sink, so every store is
 // unconditional (as in the pipe).
-template <int PER>
+template <int PER, bool ATOM>
 __global__ __launch_bounds__(256) void owner_split_direct(const int64_t *keys, uint64_t n, uint32_t shift,
                                                           uint32_t parts, uint64_t n_tiles, uint32_t *cur,
                                                           uint64_t cap, int64_t *out_k, uint32_t *out_r,
@@ -870,21 +871,37 @@ __global__ __launch_bounds__(256) void owner_split_direct(const int64_t *keys, u
     const uint64_t w0 = t * kTile + wave * kWaveKeys;  // the wave's first key
     uint32_t dr[PER];  // destination | rank in the wave's run << 8 (0xFFFFFFFF: no key)
     uint32_t cum = 0;  // lane p < parts: the wave's keys of destination p so far
+    if (ATOM) {
+      // ranks from LDS atomics on the wave's own counters (the LDS runs one wave's operations in
+      // order: the zeroing lands before the adds, the adds before the read of the totals; the
+      // previous tile's reservation read the counters before the barrier that ended it)
+      if (lane < parts) s_cnt[wave][lane] = 0;
 #pragma unroll
-    for (int it = 0; it < PER; ++it) {
-      const bool lv = w0 + (uint32_t)it * 64u + lane < n;
-      const uint32_t d =
-          self_slot((murmurhash64_hi((uint64_t)kc[it]) >> ((shift - 32u) & 31u)) & mask, self_last, parts);
-      uint64_t mine = __ballot(lv), pm = mine;
-      for (uint32_t b = 0; (1u << b) < parts; ++b) {
-        const uint64_t bb = __ballot((d >> b) & 1u);
-        mine &= (d >> b) & 1u ? bb : ~bb;
-        pm &= (lane >> b) & 1u ? bb : ~bb;
+      for (int it = 0; it < PER; ++it) {
+        const bool lv = w0 + (uint32_t)it * 64u + lane < n;
+        const uint32_t d =
+            self_slot((murmurhash64_hi((uint64_t)kc[it]) >> ((shift - 32u) & 31u)) & mask, self_last, parts);
+        dr[it] = lv ? d | atomicAdd(&s_cnt[wave][d], 1u) << 8 : 0xFFFFFFFFu;
       }
-      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
-      const uint32_t pre = (uint32_t)__shfl((int)cum, (int)d);
-      dr[it] = lv ? d | (pre + below) << 8 : 0xFFFFFFFFu;
-      cum += (uint32_t)__popcll(pm);
+      cum = lane < parts ? s_cnt[wave][lane] : 0u;
+    } else {
+#pragma unroll
+      for (int it = 0; it < PER; ++it) {
+        const bool lv = w0 + (uint32_t)it * 64u + lane < n;
+        const uint32_t d =
+            self_slot((murmurhash64_hi((uint64_t)kc[it]) >> ((shift - 32u) & 31u)) & mask, self_last, parts);
+        uint64_t mine = __ballot(lv), pm = mine;
+        for (uint32_t b = 0; (1u << b) < parts; ++b) {
+          const uint64_t bb = __ballot((d >> b) & 1u);
+          mine &= (d >> b) & 1u ? bb : ~bb;
+          pm &= (lane >> b) & 1u ? bb : ~bb;
+        }
+        const uint32_t below =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
+        const uint32_t pre = (uint32_t)__shfl((int)cum, (int)d);
+        dr[it] = lv ? d | (pre + below) << 8 : 0xFFFFFFFFu;
+        cum += (uint32_t)__popcll(pm);
+      }
     }
     // lane p: destination p's offset in the wave image (wloc); the image's length (wtot)
     const uint32_t mine_cnt = lane < parts ? cum : 0u;
@@ -900,7 +917,7 @@ __global__ __launch_bounds__(256) void owner_split_direct(const int64_t *keys, u
         s_wr[wave][q] = ((uint32_t)it * 64u + lane) | d << 16;
       }
     }
-    if (lane < parts) s_cnt[wave][lane] = cum;
+    if (!ATOM && lane < parts) s_cnt[wave][lane] = cum;
     __syncthreads();
     if (tid < parts) {
       uint32_t tot = 0;
@@ -921,7 +938,8 @@ __global__ __launch_bounds__(256) void owner_split_direct(const int64_t *keys, u
     }
     __syncthreads();
     // lane p < parts: its run's base minus its image offset, so entry q of destination d is stored
-    // at position base_d + q (mod 2^32)
+    // at position base_d + q (mod 2^32).  (Round 6: each wave reserving its own runs, no barriers,
+    // measured 0.156 -> 0.204 ms per 2^25 keys at 8 owners — runs of 64 keys instead of 256.)
     const uint32_t adj = lane < parts ? s_base[wave][lane] - wloc : 0u;
 #pragma unroll
     for (int it = 0; it < PER; ++it) {
@@ -979,9 +997,18 @@ static hipError_t launch_owner_split_small(const int64_t *keys, uint64_t n, uint
   const uint32_t per_cu = (uint32_t)ccj_tune_int("CCJ_OWNER_PER_CU", kOwnerDirectPerCu);
   uint64_t grid = per_cu ? (uint64_t)stream_cus(s) * per_cu / 8 * 8 : (n_tiles + 7) / 8 * 8;
   grid = grid < 8 ? 8 : grid;
-  if (ccj_tune_int("CCJ_OWNER_DIRECT", 1))
-    hipLaunchKernelGGL(owner_split_direct<kPer>, dim3((unsigned)grid), dim3(kT), 0, s, keys, n, shift, parts, n_tiles,
-                       cur, sub_cap, out_keys, out_rows, status, row_base, sink_k, sink_r, self_last, abl);
+  // ranks: LDS atomics from 4 destinations up (8 owners 0.161 -> 0.154 ms per 2^25 keys, same box,
+  // profiles/r6_ab_owner_rank.log); one or two destinations by ballots (one owner: 64 lanes on one
+  // counter made the atomics 0.144 -> 0.177 ms)
+  const bool atom = parts >= 4 && ccj_tune_int("CCJ_OWNER_RANK", 1);
+  // (Round 6, same box: 4096-key tiles — PER 16, 137 VGPRs, three workgroups per CU — 0.155 ->
+  // 0.157 ms per 2^25 keys at 8 owners; not kept.)
+  if (ccj_tune_int("CCJ_OWNER_DIRECT", 1) && atom)
+    hipLaunchKernelGGL((owner_split_direct<kPer, true>), dim3((unsigned)grid), dim3(kT), 0, s, keys, n, shift, parts,
+                       n_tiles, cur, sub_cap, out_keys, out_rows, status, row_base, sink_k, sink_r, self_last, abl);
+  else if (ccj_tune_int("CCJ_OWNER_DIRECT", 1))
+    hipLaunchKernelGGL((owner_split_direct<kPer, false>), dim3((unsigned)grid), dim3(kT), 0, s, keys, n, shift, parts,
+                       n_tiles, cur, sub_cap, out_keys, out_rows, status, row_base, sink_k, sink_r, self_last, abl);
   else
     hipLaunchKernelGGL((slot_split_pipe<false, kT, 64, kPer, false>), dim3((unsigned)grid), dim3(kT), 0, s, keys, n,
                        shift, parts, n_tiles, cur, sub_cap, (uint64_t)0, (uint64_t)0, out_keys, out_rows, status,

@@ -105,7 +105,9 @@ def test_partition_fixed_overflow_flags_and_stays_in_bounds():
 
 @pytest.mark.parametrize("parts,n,base,self_last", [(1, 1000, 0, -1), (2, 100000, 7, -1), (8, 1234567, 1 << 20, -1),
                                                     (64, 500000, 3, -1), (1, 1000, 0, 0), (2, 100000, 7, 0),
-                                                    (8, 1234567, 1 << 20, 3), (8, 300000, 5, 7), (64, 500000, 3, 17)])
+                                                    (8, 1234567, 1 << 20, 3), (8, 300000, 5, 7), (64, 500000, 3, 17),
+                                                    (4, 777777, 11, -1), (4, 200000, 0, 2), (16, 400000, 1, 5),
+                                                    (32, 300000, 2, -1)])
 def test_partition_grouped_segments(parts, n, base, self_last):
     """ccj_partition_by_owner_grouped (the one-pass split with the owner as partition): the 8
     sub-segments of destination d's slot hold exactly the owner-d (key, base + row) pairs between

@@ -1,7 +1,8 @@
 """Owner split alone (ON THE GPU BOX): ms per 2^25-key batch of ccj_partition_by_owner_grouped for
-1 and 8 owners, on an unmasked stream (the default half-CU grid) and on CU-masked streams of 64 / 128
+1, 2, 4 and 8 owners, on an unmasked stream (the default half-CU grid) and on CU-masked streams of 64 / 128
 CUs (one workgroup per CU), nothing else running.  python3 tools/owner_split_bench.py [--lib tuning|PATH]
 [--unmasked].  Tuning-build knobs: CCJ_OWNER_DIRECT=0 (round 4's slot_split_pipe form),
+CCJ_OWNER_RANK=0 (owner_split_direct's ballot ranking at every owner count),
 CCJ_OWNER_PER_CU (persistent workgroups per CU; 0: one per tile), CCJ_OWNER_ABLATE (0x10 no stores,
 0x20 no key reads, 0x2000 no hash, 0x100000 no reservation atomics, 0x200000 no image scatter;
 the last two in the round-4 form)."""
@@ -50,7 +51,7 @@ def main():
                "masked 128 CUs": ccj.cu_masked_stream(ccj.cu_mask_groups(set(range(16, 32))))}
     if "--unmasked" in sys.argv:
         streams = {k: v for k, v in streams.items() if k.startswith("unmasked")}
-    for parts in (1, 8):
+    for parts in (1, 2, 4, 8):
         for name, s in streams.items():
             ms = run(parts, s)
             print(f"owners {parts}  {name:24s} {ms:7.3f} ms per 2^25 keys  ({(1 << 25) * 20 / ms / 1e6:7.1f} GB/s of 20 B/key)")
