@@ -175,8 +175,10 @@ hipError_t radix_sort(K *keys, K *keys_alt, uint32_t *vals, uint32_t *vals_alt, 
   unsigned long long *or_and = (unsigned long long *)w;
   uint32_t *cnt = (uint32_t *)(w + 256);
   void *scan_tmp = w + 256 + ((kDigits * tiles * 4 + 255) & ~(uint64_t)255);
-  unsigned long long init[2] = {0ull, ~0ull}, got[2];
-  hipError_t e = hipMemcpyAsync(or_and, init, sizeof(init), hipMemcpyHostToDevice, s);
+  unsigned long long got[2];
+  // OR starts at 0, AND at all ones (memsets: no host buffer that must outlive the call)
+  hipError_t e = hipMemsetAsync(or_and, 0, 8, s);
+  if (!e) e = hipMemsetAsync(or_and + 1, 0xFF, 8, s);
   if (e) return e;
   const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(sort_key_bits<K>, dim3(grid), dim3(256), 0, s, keys, n, or_and);
