@@ -445,12 +445,12 @@ def bench_c3(args, dev, stream):
             t = p.stdout.split()
             if p.returncode == 0 and "BENCH" in t:
                 rm, rs = int(t[t.index("BENCH") + 2]), float(t[t.index("BENCH") + 4])
+                want_ref = O.count_c3(SEED, 0, n_ref, n_build, 1, threads=args.cpu_threads)[0]
                 cpu = {"value": n_ref / rs, "unit": "probe tuples/s", "cores": 1, "kind": "reference",
-                       "sample": (f"the reference's HashTable(2^26, 1) + Probe/Next loop (chaining_ht.cpp, compiled "
+                       "sample": (f"the reference's HashTable({n_build}, 1) + Probe/Next loop (chaining_ht.cpp, compiled "
                                   f"from its sources), one thread, on the first {n_ref} keys of the same C3 stream: "
-                                  f"{rs:.2f} s, {rm} matches (expected "
-                                  f"{O.count_c3(SEED, 0, n_ref, n_build, 1, threads=args.cpu_threads)[0]})"),
-                       "cpu_model": cpu_model()}
+                                  f"{rs:.2f} s, {rm} matches (expected {want_ref})"),
+                       "matches_ok": rm == want_ref, "cpu_model": cpu_model()}
     n_bar, m_bar = examined / n_probe, matches / n_probe
     # SURVEY §8(d) for chaining: 8 (probe key) + 4 (bucket offset) + 8·N̄ (chain keys visited) +
     # 12·m̄ (u32 row id + payload per match); the step also compacts every match (NaiveCompactor,

@@ -83,6 +83,19 @@ def test_bench_c3(path):
     assert line["path"] == path
 
 
+def test_bench_c3_reference_cpu_baseline():
+    """C3's cpu_baseline: the reference's own chaining loop (oracle/_ref/ref_driver, compiled from its
+    sources) on a sample of the same stream, its match count checked against the oracle's."""
+    if not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "ref_driver")):
+        pytest.skip("oracle/_ref/ref_driver not built")
+    p = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--n-build", str(1 << 21),
+                        "--n-probe", str(1 << 24), "--workload", "c3", "--cpu-sample", str(1 << 22)], cwd=ROOT,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    cpu = json.loads(p.stdout.strip().splitlines()[-1])["cpu_baseline"]
+    assert cpu is not None and cpu["kind"] == "reference" and cpu["matches_ok"] and cpu["value"] > 0, cpu
+
+
 def test_bench_c5():
     line = run_bench("--workload", "c5")
     par = line["parity"]
