@@ -37,7 +37,11 @@ pytestmark = pytest.mark.gpu
 
 import ccj  # noqa: E402
 
-N_CASES = 64
+import os  # noqa: E402
+
+# 64 fixed cases by default; CCJ_SWEEP_CASES / CCJ_SWEEP_BASE run a longer exploratory sweep
+N_CASES = int(os.environ.get("CCJ_SWEEP_CASES", "64"))
+BASE = int(os.environ.get("CCJ_SWEEP_BASE", "0"))
 GATHERS = set()  # the gather kernels the partitioned payload probes ran (ccj_last_gather_kernel)
 P = 8  # payload columns
 
@@ -51,7 +55,7 @@ def _device():
 
 def draw(case):
     """The case's configuration: (kind, build keys, probe keys, chunk)."""
-    r = np.random.default_rng(7001 + case)
+    r = np.random.default_rng(7001 + BASE + case)
     kind = ccj.CHAIN if case % 3 == 2 else ccj.LP
     n_build = int(r.choice([1, 5, 300, 4096, 50000, 1 << 18, (1 << 20) + 17, 1 << 21]))
     distinct = bool(r.random() < 0.6)
@@ -73,7 +77,7 @@ def draw(case):
         keys[::101] = -1
         keys[50::103] = -(1 << 62)
     bk, keys = bk.astype(np.int64), keys.astype(np.int64)
-    if np.random.default_rng(99 + case).random() < 0.25:
+    if np.random.default_rng(99 + BASE + case).random() < 0.25:
         # negative build keys, the same keys negated in both columns (never -1: the LP empty marker)
         bk = np.where((bk > 1) & (bk % 5 == 0), -bk, bk)
         keys = np.where((keys > 1) & (keys % 5 == 0), -keys, keys)
@@ -127,7 +131,7 @@ def check_compaction(case, out_d, want, keys, d_keys, chunk):
     (compact_plan: compactor.cpp:5-41, the :36 fix) run on the ORACLE's Next results: output chunk
     counts and every row's global row, payload and carried columns (DataChunk::Append, base.cpp:15-27),
     with the case's pass-through threshold and, for odd cases, the key column filled from the payload."""
-    r = np.random.default_rng(9001 + case)
+    r = np.random.default_rng(9001 + BASE + case)
     threshold = int(r.choice([0, 1, max(1, chunk // 2), chunk]))
     extra = (np.arange(len(keys), dtype=np.int64) * 7 - 3)
     d_extra = torch.from_numpy(extra).cuda()
@@ -270,7 +274,7 @@ def test_sweep_filtered_input():
 
 
 def draw_pipeline(case):
-    r = np.random.default_rng(8001 + case)
+    r = np.random.default_rng(8001 + BASE + case)
     joins = int(r.integers(1, 5))
     B = int(r.choice([1, 7, 64, 100, 256, 1000, 2048]))
     n = int(r.choice([1, 500, 5000, 20000]))
@@ -295,7 +299,7 @@ def draw_pipeline(case):
     return tables, cols, B, compact, thresholds
 
 
-@pytest.mark.parametrize("case", range(16))
+@pytest.mark.parametrize("case", range(max(16, N_CASES // 4)))
 def test_sweep_pipeline(case):
     tables, cols, B, compact, thresholds = draw_pipeline(case)
     dt = [ccj.Table.from_host(kind, bk) for kind, bk in tables]
