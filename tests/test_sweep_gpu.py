@@ -26,6 +26,8 @@ Every entry point that takes the configuration is run on it, through the C ABI:
                          drawn thresholds, against the oracle's join-by-join restatement of
                          main.cpp:119-191 (tests/helpers.py oracle_pipeline): the result table in order
 The cases complement the fixed-shape tests: shapes nobody picked by hand."""
+import os
+
 import numpy as np
 import pytest
 
@@ -36,8 +38,6 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 import ccj  # noqa: E402
-
-import os  # noqa: E402
 
 # 64 fixed cases by default; CCJ_SWEEP_CASES / CCJ_SWEEP_BASE run a longer exploratory sweep
 N_CASES = int(os.environ.get("CCJ_SWEEP_CASES", "64"))
