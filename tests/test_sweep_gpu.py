@@ -248,7 +248,10 @@ def test_sweep_case(case):
 
 
 def test_sweep_ran_both_gathers():
-    """The sweep reached the slab-order gather and the per-chunk one (runs after the cases)."""
+    """The sweep reached the slab-order gather and the per-chunk one (collected by the cases above;
+    skipped when they were not run in this session)."""
+    if not GATHERS:
+        pytest.skip("needs test_sweep_case's payload cases in the same session")
     assert {"gather_payload_cols", "gather_payload_cols_sub"} <= GATHERS, GATHERS
 
 
